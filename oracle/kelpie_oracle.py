@@ -1,0 +1,768 @@
+"""CPU restatement of the Kelpie relevance-engine hot path (TEST INFRASTRUCTURE).
+
+This module is the parity ORACLE.  Only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import it, and only as the checker /
+the timed CPU baseline; the product package ``kelpie_amd`` never imports it.
+
+It restates, in plain numpy (float32 arrays, the dtype the reference trains
+in) plus the torch CPU generator for the random draws, the reference's
+post-training relevance path:
+
+* dataset indices and filters ............ ``src/data/dataset.py:104-141,319-352``
+* per-entity kelpie view ................. ``src/data/kelpie_dataset.py:10-203``
+* engine, relevance formulas, rank ....... ``src/relevance_engines/post_training_engine.py:17-207``
+* conversion-entity selection ............ ``src/relevance_engines/engine.py:22-126``
+* TransE / ComplEx / ConvE scorers ....... ``src/link_prediction/models/{transe,complex,conve}.py``
+* Kelpie optimizers (one trainable row) .. ``src/link_prediction/optimization/*.py``
+* stochastic explanation builder ......... ``src/explanation_builders/stochastic_builder.py:33-192``
+
+Gradients are the hand-derived single-row gradients of SURVEY.md Appendix C,
+computed from the FULL score matrices (no algebraic shortcuts), so the oracle
+is an independent check of the decompositions the HIP kernels use.
+
+Parity pinning: every function here is checked against golden vectors that
+``tests/golden/make_golden.py`` captured by running the reference itself
+(CPU-redirected import) in the development container; see
+``tests/test_oracle_golden.py``.
+"""
+from __future__ import annotations
+
+import math
+import random
+from collections import Counter, OrderedDict, defaultdict
+from itertools import combinations
+
+import numpy as np
+import torch
+
+ONE_TO_ONE, ONE_TO_MANY, MANY_TO_ONE, MANY_TO_MANY = "1-1", "1-N", "N-1", "N-N"
+F32 = np.float32
+
+
+# =============================================================================
+# data layer
+# =============================================================================
+class OracleDataset:
+    """Index / filter semantics of ``Dataset.__init__`` (dataset.py:104-141)."""
+
+    def __init__(self, num_entities, num_relations, train, valid, test):
+        self.num_entities = int(num_entities)
+        self.num_relations = int(num_relations)
+        self.training_triples = np.asarray(train, dtype=np.int64).reshape(-1, 3)
+        self.validation_triples = np.asarray(valid, dtype=np.int64).reshape(-1, 3)
+        self.testing_triples = np.asarray(test, dtype=np.int64).reshape(-1, 3)
+        e2tr, e2va, e2te = defaultdict(list), defaultdict(list), defaultdict(list)
+        for dst, arr in ((e2tr, self.training_triples), (e2va, self.validation_triples),
+                         (e2te, self.testing_triples)):
+            for s, p, o in arr.tolist():
+                dst[s].append((s, p, o))
+                dst[o].append((s, p, o))
+        # dataset.py:114-125 -- the three dedup loops all rewrite the TRAINING lists
+        for e in list(e2tr):
+            e2tr[e] = list(set(e2tr[e]))
+        for e in list(e2va):
+            e2tr[e] = list(set(e2tr[e]))
+        for e in list(e2te):
+            e2tr[e] = list(set(e2tr[e]))
+        self.entity_to_training_triples = e2tr
+        self.entity_to_validation_triples = e2va
+        self.entity_to_testing_triples = e2te
+        self.entity_to_degree = {e: len(t) for e, t in e2tr.items()}
+        R = self.num_relations
+        self.train_to_filter = defaultdict(list)
+        for s, p, o in self.training_triples.tolist():
+            self.train_to_filter[(s, p)].append(o)
+            self.train_to_filter[(o, p + R)].append(s)
+        self.to_filter = defaultdict(list)
+        for arr in (self.training_triples, self.validation_triples, self.testing_triples):
+            for s, p, o in arr.tolist():
+                self.to_filter[(s, p)].append(o)
+                self.to_filter[(o, p + R)].append(s)
+        self._relation_types()
+
+    def _relation_types(self):
+        # dataset.py:282-317
+        s_num, o_num = defaultdict(list), defaultdict(list)
+        for (e, r) in self.train_to_filter:
+            n = len(self.to_filter[(e, r)])
+            if r >= self.num_relations:
+                s_num[r - self.num_relations].append(n)
+            else:
+                o_num[r].append(n)
+        self.relation_to_type = {}
+        for r in s_num:
+            a_s = np.average(s_num[r])
+            a_o = np.average(o_num[r])
+            if a_s > 1.2 and a_o > 1.2:
+                t = MANY_TO_MANY
+            elif a_s > 1.2 and a_o <= 1.2:
+                t = MANY_TO_ONE
+            elif a_s <= 1.2 and a_o > 1.2:
+                t = ONE_TO_MANY
+            else:
+                t = ONE_TO_ONE
+            self.relation_to_type[r] = t
+
+    def invert_triples(self, triples):
+        # dataset.py:319-331
+        t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        out = t.copy()
+        out[:, 0] = t[:, 2]
+        out[:, 2] = t[:, 0]
+        out[:, 1] += self.num_relations
+        return out
+
+
+def replace_entity(triple, old, new):
+    # dataset.py:333-341
+    s, p, o = triple
+    return (new if s == old else s, p, new if o == old else o)
+
+
+class OracleKelpieView:
+    """The per-entity view of ``KelpieDataset`` (kelpie_dataset.py:10-203).
+
+    Filters are multisets (``to_filter`` lists of the reference, where
+    ``list.remove`` drops one occurrence)."""
+
+    def __init__(self, ds: OracleDataset, entity: int):
+        self.ds = ds
+        self.original_entity = entity
+        self.kelpie_entity = ds.num_entities
+        self.num_entities = ds.num_entities + 1
+        k = self.kelpie_entity
+        self.base_training = [replace_entity(t, entity, k) for t in ds.entity_to_training_triples[entity]]
+        kva = [replace_entity(t, entity, k) for t in ds.entity_to_validation_triples.get(entity, [])]
+        kte = [replace_entity(t, entity, k) for t in ds.entity_to_testing_triples.get(entity, [])]
+        R = ds.num_relations
+        self.filter = defaultdict(Counter)  # only keys touched by kelpie triples
+        for s, p, o in self.base_training + kva + kte:
+            self.filter[(s, p)][o] += 1
+            self.filter[(o, p + R)][s] += 1
+        self.index = {t: i for i, t in enumerate(self.base_training)}
+
+    def as_kelpie(self, triple):
+        if self.original_entity not in triple:
+            raise Exception(f"Could not find the original entity {self.original_entity} in {triple}")
+        return replace_entity(triple, self.original_entity, self.kelpie_entity)
+
+    def removed(self, triples):
+        """(training rows, filter for ranking) after ``remove_training_triples`` (:130-158)."""
+        k = self.kelpie_entity
+        R = self.ds.num_relations
+        conv = [replace_entity(tuple(t), self.original_entity, k) for t in triples]
+        idx = [self.index[x] for x in conv]  # KeyError like the reference
+        keep = np.ones(len(self.base_training), bool)
+        keep[idx] = False
+        rows = [t for t, f in zip(self.base_training, keep) if f]
+        filt = defaultdict(Counter, {key: Counter(v) for key, v in self.filter.items()})
+        for s, p, o in conv:
+            for key, val in (((s, p), o), ((o, p + R), s)):
+                if filt[key][val] <= 0:
+                    raise ValueError("list.remove(x): x not in list")
+                filt[key][val] -= 1
+        return rows, filt
+
+    def added(self, triples):
+        """(training rows, filter) after ``add_training_triples`` (:92-128)."""
+        k = self.kelpie_entity
+        R = self.ds.num_relations
+        conv = [replace_entity(tuple(t), self.original_entity, k) for t in triples]
+        rows = list(self.base_training) + conv
+        filt = defaultdict(Counter, {key: Counter(v) for key, v in self.filter.items()})
+        for s, p, o in conv:
+            filt[(s, p)][o] += 1
+            filt[(o, p + R)][s] += 1
+        return rows, filt
+
+
+def filter_list(filt, s, p):
+    c = filt.get((s, p))
+    if not c:
+        return []
+    return [e for e, n in c.items() if n > 0]
+
+
+# =============================================================================
+# models (frozen tables; scoring)
+# =============================================================================
+class OracleModel:
+    """Frozen weights of one reference model family."""
+
+    def __init__(self, name, weights: dict, dim: int, model_params: dict | None = None):
+        self.name = name
+        self.E = np.ascontiguousarray(weights["entity_embeddings"], dtype=F32)
+        self.R = np.ascontiguousarray(weights["relation_embeddings"], dtype=F32)
+        self.w = {k: np.asarray(v, dtype=F32) for k, v in weights.items()}
+        self.dim = dim  # hp dimension (ComplEx: real dimension)
+        self.params = dict(model_params or {})
+        if name == "ComplEx":
+            self.dimension = 2 * dim
+            self.init_scale = float(self.params.get("init_scale", 1e-3))
+        else:
+            self.dimension = dim
+        if name == "ConvE":
+            self.hidden_dropout = float(self.params.get("hidden_dropout_rate", 0.0))
+            self.input_dropout = float(self.params.get("input_dropout_rate", 0.0))
+            self.fmap_dropout = float(self.params.get("feature_map_dropout_rate", 0.0))
+            self.ew, self.eh = 20, dim // 20
+            self.bn = {}
+            for i in (1, 2, 3):
+                inv = (1.0 / np.sqrt(self.w[f"bn{i}_var"].astype(np.float64) + 1e-5)).astype(F32)
+                alpha = (inv * self.w[f"bn{i}_weight"]).astype(F32)
+                beta = (self.w[f"bn{i}_bias"] - self.w[f"bn{i}_mean"] * alpha).astype(F32)
+                self.bn[i] = (alpha, beta)
+
+    def is_minimizer(self):
+        return self.name == "TransE"
+
+    # ------------------------------------------------------------ scorers
+    def complex_query(self, lhs, rel):
+        d = self.dim
+        a, b = lhs[..., :d], lhs[..., d:]
+        c, dd = rel[..., :d], rel[..., d:]
+        return np.concatenate([a * c - b * dd, a * dd + b * c], axis=-1).astype(F32)
+
+    def conve_encode(self, lhs, rel, hidden_mask=None):
+        """ConvE encoder (conve.py:133-153).  Returns (x, cache for backward)."""
+        b = lhs.shape[0]
+        d = self.dim
+        img = np.concatenate([lhs.reshape(b, 20, self.eh), rel.reshape(b, 20, self.eh)], axis=1)  # (b,40,eh)
+        a1, b1 = self.bn[1]
+        img_bn = (img * a1[0] + b1[0]).astype(F32)
+        W = self.w["conv_weight"][:, 0]  # (32,3,3)
+        H, Wd = 38, self.eh - 2
+        conv = np.zeros((b, 32, H, Wd), F32)
+        for ky in range(3):
+            for kx in range(3):
+                patch = img_bn[:, ky:ky + H, kx:kx + Wd]  # (b,H,Wd)
+                conv += W[None, :, ky, kx, None, None] * patch[:, None]
+        conv += self.w["conv_bias"][None, :, None, None]
+        a2, b2 = self.bn[2]
+        c_bn = (conv * a2[None, :, None, None] + b2[None, :, None, None]).astype(F32)
+        c_relu = np.maximum(c_bn, 0).astype(F32)
+        flat = c_relu.reshape(b, -1)
+        fc = (flat @ self.w["fc_weight"].T + self.w["fc_bias"]).astype(F32)
+        if hidden_mask is not None:
+            fc_d = (fc * hidden_mask).astype(F32)
+        else:
+            fc_d = fc
+        a3, b3 = self.bn[3]
+        h_bn = (fc_d * a3 + b3).astype(F32)
+        x = np.maximum(h_bn, 0).astype(F32)
+        return x, (c_bn, h_bn, hidden_mask)
+
+    def conve_backward_lhs(self, dx, cache):
+        """d loss / d lhs-embedding through the frozen encoder (ConvE)."""
+        c_bn, h_bn, mask = cache
+        b = dx.shape[0]
+        a3, _ = self.bn[3]
+        g = dx * (h_bn > 0)
+        g = g * a3
+        if mask is not None:
+            g = g * mask
+        dflat = (g @ self.w["fc_weight"]).astype(F32)  # (b, hidden)
+        H, Wd = 38, self.eh - 2
+        dc = dflat.reshape(b, 32, H, Wd) * (c_bn > 0)
+        a2, _ = self.bn[2]
+        dc = dc * a2[None, :, None, None]
+        W = self.w["conv_weight"][:, 0]
+        dimg = np.zeros((b, 40, self.eh), F32)
+        for ky in range(3):
+            for kx in range(3):
+                dimg[:, ky:ky + H, kx:kx + Wd] += np.einsum("bchw,c->bhw", dc, W[:, ky, kx])
+        a1, _ = self.bn[1]
+        dimg = dimg * a1[0]
+        return dimg[:, :20, :].reshape(b, self.dim).astype(F32)
+
+    def all_scores(self, triples, kelpie_row=None):
+        """``Model.all_scores`` over the entity table (+ optional kelpie row at index |E|)."""
+        t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        E = self.E if kelpie_row is None else np.vstack([self.E, kelpie_row[None].astype(F32)])
+        lhs = E[t[:, 0]]
+        rel = self.R[t[:, 1]]
+        if self.name == "TransE":
+            tr = (lhs + rel).astype(F32)
+            diff = tr[:, None, :] - E[None, :, :]
+            return np.sqrt((diff.astype(np.float64) ** 2).sum(-1)).astype(F32)
+        if self.name == "ComplEx":
+            q = self.complex_query(lhs, rel)
+            return (q @ E.T).astype(F32)
+        x, _ = self.conve_encode(lhs, rel)
+        s = (x @ E.T).astype(F32)
+        return (1.0 / (1.0 + np.exp(-s.astype(np.float64)))).astype(F32)
+
+
+# =============================================================================
+# optimizers (torch semantics, float32)
+# =============================================================================
+class AdagradState:
+    # torch.optim.Adagrad, lr_decay 0, eps 1e-10, initial accumulator 0
+    def __init__(self, n, lr, eps=1e-10):
+        self.sum = np.zeros(n, F32)
+        self.lr, self.eps = F32(lr), F32(eps)
+
+    def step(self, x, g):
+        self.sum = (self.sum + g * g).astype(F32)
+        std = (np.sqrt(self.sum) + self.eps).astype(F32)
+        return (x - self.lr * (g / std)).astype(F32)
+
+
+class AdamState:
+    # torch.optim.Adam (single-tensor path), weight_decay 0, amsgrad False
+    def __init__(self, n, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.m = np.zeros(n, F32)
+        self.v = np.zeros(n, F32)
+        self.t = 0
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+
+    def step(self, x, g):
+        self.t += 1
+        self.m = (self.m + F32(1 - self.b1) * (g - self.m)).astype(F32)
+        self.v = (self.v * F32(self.b2) + F32(1 - self.b2) * g * g).astype(F32)
+        bc1 = 1 - self.b1 ** self.t
+        bc2 = 1 - self.b2 ** self.t
+        step_size = self.lr / bc1
+        denom = (np.sqrt(self.v) / F32(math.sqrt(bc2)) + F32(self.eps)).astype(F32)
+        return (x - F32(step_size) * (self.m / denom)).astype(F32)
+
+
+class SGDState:
+    def __init__(self, n, lr):
+        self.lr = F32(lr)
+
+    def step(self, x, g):
+        return (x - self.lr * g).astype(F32)
+
+
+# =============================================================================
+# post-training (one trainable kelpie row; SURVEY App. C gradients)
+# =============================================================================
+def _rows_with_inverses(ds, triples):
+    t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+    return np.vstack([t, ds.invert_triples(t)])
+
+
+def posttrain_complex(model: OracleModel, ds, triples, x0, hp, rng):
+    """KelpieMultiClassNLLOptimizer (multiclass_nll_optimizer.py:57-99,138-164)."""
+    k = ds.num_entities
+    rows = _rows_with_inverses(ds, triples)
+    n = rows.shape[0]
+    bs = min(int(hp["batch_size"]), n)
+    x = x0.astype(F32).copy()
+    D = model.dimension
+    name = hp["optimizer_name"]
+    if name == "Adagrad":
+        opt = AdagradState(D, hp["lr"])
+    elif name == "Adam":
+        opt = AdamState(D, hp["lr"], (hp["decay1"], hp["decay2"]))
+    else:
+        opt = SGDState(D, hp["lr"])
+    w_reg = float(hp.get("regularizer_weight", 0.0))
+    for _ in range(int(hp["epochs"])):
+        perm = rng.randperm(n)
+        prow = rows[perm]
+        start = 0
+        while start < n:
+            batch = prow[start:start + bs]
+            E = np.vstack([model.E, x[None]])
+            lhs = E[batch[:, 0]]
+            rel = model.R[batch[:, 1]]
+            q = model.complex_query(lhs, rel)
+            logits = (q @ E.T).astype(np.float64)
+            logits -= logits.max(1, keepdims=True)
+            p = np.exp(logits)
+            p /= p.sum(1, keepdims=True)
+            b = batch.shape[0]
+            G = p.copy()
+            G[np.arange(b), batch[:, 2]] -= 1.0
+            G /= b
+            g = (G[:, k:k + 1] * q).sum(0)  # kelpie as candidate tail
+            dq = G @ E.astype(np.float64)  # (b, D)
+            hk = batch[:, 0] == k
+            if hk.any():
+                d = model.dim
+                gr, gi = dq[hk, :d], dq[hk, d:]
+                c, dd = rel[hk, :d].astype(np.float64), rel[hk, d:].astype(np.float64)
+                g[:d] += (gr * c + gi * dd).sum(0)
+                g[d:] += (-gr * dd + gi * c).sum(0)
+            if w_reg != 0.0:
+                d = model.dim
+                for side, mask in ((lhs, hk), (E[batch[:, 2]], batch[:, 2] == k)):
+                    if mask.any():
+                        a_, b_ = side[mask, :d].astype(np.float64), side[mask, d:].astype(np.float64)
+                        mod = np.sqrt(a_ ** 2 + b_ ** 2)
+                        g[:d] += (3 * w_reg / b * mod * a_).sum(0)
+                        g[d:] += (3 * w_reg / b * mod * b_).sum(0)
+            x = opt.step(x, g.astype(F32))
+            start += int(hp["batch_size"])
+    return x
+
+
+def posttrain_transe(model: OracleModel, ds, triples, x0, hp, rng):
+    """KelpiePairwiseRankingOptimizer (pairwise_ranking_optimizer.py:55-98,139-157,160-203)."""
+    k = ds.num_entities
+    N = ds.num_entities + 1
+    rows = _rows_with_inverses(ds, triples)
+    n = rows.shape[0]
+    ratio = int(hp["negative_triples_ratio"])
+    bs = int(hp["batch_size"])
+    margin = F32(hp["margin"])
+    lam = float(hp["regularizer_weight"])
+    x = x0.astype(F32).copy()
+    d = model.dimension
+    opt = AdamState(d, hp["lr"])
+    for _ in range(int(hp["epochs"])):
+        rng.np_shuffle(rows)  # in place, compounding across epochs
+        rep = np.repeat(rows, ratio, axis=0)
+        ents = rng.randint(N, rep.shape[0])
+        hot = rng.randint(2, rep.shape[0])
+        neg = rep.copy()
+        neg[:, 0] = np.where(hot == 1, ents, rep[:, 0])
+        neg[:, 2] = np.where(hot == 1, rep[:, 2], ents)
+        start = 0
+        while start < n:
+            end = min(start + bs, n)
+            pos, ng = rep[start:end], neg[start:end]
+            B = pos.shape[0]
+            E = np.vstack([model.E, x[None]])
+            g = np.zeros(d, np.float64)
+            vs = []
+            for tri in (pos, ng):
+                v = (E[tri[:, 0]] + model.R[tri[:, 1]] - E[tri[:, 2]]).astype(F32)
+                f = np.sqrt((v.astype(np.float64) ** 2).sum(1))
+                vs.append((v, f, tri))
+            act = (vs[0][1] - vs[1][1] + float(margin)) > 0
+            for sign, (v, f, tri) in ((1.0, vs[0]), (-1.0, vs[1])):
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    u = np.where(f[:, None] > 0, v / f[:, None], 0.0)
+                coef = sign * act / B
+                g += ((coef * (tri[:, 0] == k))[:, None] * u).sum(0)
+                g -= ((coef * (tri[:, 2] == k))[:, None] * u).sum(0)
+            if lam != 0.0:
+                cnt = sum(int((tri[:, 0] == k).sum() + (tri[:, 2] == k).sum()) for tri in (pos, ng))
+                g += lam / (3.0 * B * d) * cnt * x.astype(np.float64)
+            x = opt.step(x, g.astype(F32))
+            start += bs
+    return x
+
+
+def posttrain_conve(model: OracleModel, ds, triples, x0, hp, rng):
+    """KelpieBCEOptimizer (bce_optimizer.py:45-112,161-208): Adam(lr=1e-3), no shuffle."""
+    k = ds.num_entities
+    N = ds.num_entities + 1
+    rows = _rows_with_inverses(ds, triples)
+    er = OrderedDict()
+    for h, r, t in rows.tolist():
+        er.setdefault((h, r), []).append(t)
+    pairs = list(er.keys())
+    ls = float(hp["label_smoothing"])
+    bs = int(hp["batch_size"])
+    x = x0.astype(F32).copy()
+    d = model.dimension
+    opt = AdamState(d, 1e-3)
+    p_hid = model.hidden_dropout
+    for _ in range(int(hp["epochs"])):
+        start = 0
+        while start < len(pairs):
+            batch = pairs[start:start + bs]
+            b = len(batch)
+            hs = np.array([p[0] for p in batch], np.int64)
+            rs = np.array([p[1] for p in batch], np.int64)
+            y = np.zeros((b, N), F32)
+            for i, pr in enumerate(batch):
+                y[i, er[pr]] = 1.0
+            if ls:
+                y = (F32(1.0 - ls) * y).astype(F32)
+                y = (y + F32(1.0 / N)).astype(F32)
+            mask = rng.dropout_mask((b, d), p_hid) if p_hid > 0 else None
+            E = np.vstack([model.E, x[None]])
+            enc, cache = model.conve_encode(E[hs], model.R[rs], mask)
+            s = (enc @ E.T).astype(F32)
+            p = (1.0 / (1.0 + np.exp(-s.astype(np.float64)))).astype(F32)
+            # BCELoss + sigmoid backward (torch): (p-y)/max(p(1-p),1e-12) * p(1-p) / (b*N)
+            w = (p * (F32(1.0) - p)).astype(np.float64)
+            G = (p.astype(np.float64) - y) / np.maximum(w, 1e-12) * w / (b * N)
+            g = (G[:, k:k + 1] * enc).sum(0)
+            hk = hs == k
+            if hk.any():
+                denc = (G[hk] @ E.astype(np.float64)).astype(F32)
+                sub = (cache[0][hk], cache[1][hk], None if mask is None else mask[hk])
+                g += model.conve_backward_lhs(denc, sub).sum(0)
+            x = opt.step(x, g.astype(F32))
+            start += bs
+    return x
+
+
+POSTTRAIN = {"ComplEx": posttrain_complex, "TransE": posttrain_transe, "ConvE": posttrain_conve}
+
+
+def triple_results(model: OracleModel, x, kelpie_triple, filt):
+    """``PostTrainingEngine.get_triple_results`` (post_training_engine.py:101-125)."""
+    s, p, o = kelpie_triple
+    scores = model.all_scores([kelpie_triple], kelpie_row=x)[0].copy()
+    target = float(scores[o])
+    F = filter_list(filt, s, p)
+    if model.is_minimizer():
+        scores[F] = 1e6
+        scores[o] = target
+        rank = int((scores <= F32(target)).sum())
+    else:
+        scores[F] = -1e6
+        rank = int((scores >= F32(target)).sum())
+    return {"target_score": target, "target_rank": rank}
+
+
+# =============================================================================
+# RNG protocol: which generator draws what, in reference order
+# =============================================================================
+class TorchNumpyRNG:
+    """Draws from torch's CPU default generator and numpy's global RandomState,
+    exactly as the reference calls them."""
+
+    def rand_init(self, D):
+        return torch.rand(1, D).numpy()[0].astype(F32)  # post_training_engine.py:52
+
+    def xavier_row(self, init, d):
+        # transe.py:93-95: xavier_normal_ on a (1,d) Parameter: std = sqrt(2/(d+1))
+        t = torch.from_numpy(init.reshape(1, -1).copy())
+        torch.nn.init.xavier_normal_(t)
+        return t.numpy()[0].astype(F32)
+
+    def randperm(self, n):
+        return torch.randperm(n).numpy()  # multiclass_nll_optimizer.py:148
+
+    def np_shuffle(self, arr):
+        np.random.shuffle(arr)  # pairwise_ranking_optimizer.py:166
+
+    def randint(self, high, size):
+        return torch.randint(high=high, size=(size,)).numpy()
+
+    def conve_ctor(self, hidden, dim):
+        # KelpieConvE.__init__ builds a fresh ConvE(init_random=False) (conve.py:193-205),
+        # whose Conv2d(1,32,3) and Linear(hidden, dim) reset_parameters() draw from the
+        # CPU generator (conve.py:46-52) before being replaced by frozen copies.
+        torch.nn.Conv2d(1, 32, (3, 3), 1, 0, bias=True)
+        torch.nn.Linear(hidden, dim)
+
+    def dropout_mask(self, shape, p):
+        # ATen CPU dropout: empty_like(x).bernoulli_(1-p).div_(1-p)
+        m = torch.empty(shape).bernoulli_(1 - p)
+        m.div_(1 - p)
+        return m.numpy().astype(F32)
+
+
+# =============================================================================
+# engines
+# =============================================================================
+def _sigmoid(x):
+    return 1 / (1 + math.exp(-x))  # post_training_engine.py:19-20
+
+
+class OracleEngine:
+    """Post-training relevance engine (post_training_engine.py:17-125)."""
+
+    def __init__(self, model: OracleModel, ds: OracleDataset, hp: dict, rng=None):
+        self.model, self.ds, self.hp = model, ds, hp
+        self.rng = rng or TorchNumpyRNG()
+        self.o_to_training = defaultdict(list)
+        for h, r, t in ds.training_triples.tolist():
+            self.o_to_training[t].append((h, r, t))
+        self.set_cache()
+
+    def set_cache(self):
+        self.base_results = {}
+        self.views = {}
+
+    def view(self, s):
+        if s not in self.views:
+            self.views[s] = OracleKelpieView(self.ds, s)
+        return self.views[s]
+
+    def _init_row(self, init):
+        if self.model.name == "ConvE":
+            d = self.model.dimension
+            self.rng.conve_ctor(32 * 38 * (d // 20 - 2), d)
+        if self.model.name == "ComplEx":
+            return (init * F32(self.model.init_scale)).astype(F32)
+        if self.model.name == "TransE":
+            return self.rng.xavier_row(init, self.model.dimension)
+        return init.copy()
+
+    def _post_train(self, rows, x0):
+        return POSTTRAIN[self.model.name](self.model, self.ds, rows, x0, self.hp, self.rng)
+
+    def _pair(self, pred, triples, mode):
+        """Returns (pt_results, base_results) -- PostTrainingEngine.compute_relevance (:46-62)."""
+        s = pred[0]
+        v = self.view(s)
+        init = self.rng.rand_init(self.model.dimension)
+        x_base0 = self._init_row(init)
+        kp = v.as_kelpie(pred)
+        key = tuple(pred)
+        if key not in self.base_results:
+            xb = self._post_train(v.base_training, x_base0)
+            self.base_results[key] = triple_results(self.model, xb, kp, v.filter)
+        base = self.base_results[key]
+        x_pt0 = self._init_row(init)
+        rows, filt = (v.removed(triples) if mode == "necessary" else v.added(triples))
+        xp = self._post_train(rows, x_pt0)
+        pt = triple_results(self.model, xp, kp, filt)
+        return pt, base
+
+    def necessary_relevance(self, pred, triples):
+        pt, base = self._pair(pred, triples, "necessary")
+        rank_d = pt["target_rank"] - base["target_rank"]
+        if self.model.is_minimizer():
+            sd = pt["target_score"] - base["target_score"]
+        else:
+            sd = base["target_score"] - pt["target_score"]
+        return float(F32(F32(rank_d) + F32(_sigmoid(sd)))), pt, base  # float32 tensor add (App. A-Q5)
+
+    def individual_sufficient_relevance(self, pred, triples):
+        pt, base = self._pair(pred, triples, "sufficient")
+        rank_i = base["target_rank"] - pt["target_rank"]
+        if self.model.is_minimizer():
+            si = base["target_score"] - pt["target_score"]
+        else:
+            si = pt["target_score"] - base["target_score"]
+        rel = float(F32(F32(rank_i) + F32(_sigmoid(si))))
+        rel /= float(base["target_rank"])
+        return rel, pt, base
+
+    def sufficient_relevance(self, pred, rule, entities):
+        s = pred[0]
+        rels, details = [], []
+        for e in entities:
+            crule = [replace_entity(tuple(t), s, e) for t in rule]
+            cpred = replace_entity(tuple(pred), s, e)
+            r, pt, base = self.individual_sufficient_relevance(cpred, crule)
+            rels.append(r)
+            details.append((pt, base))
+        return sum(rels) / len(rels), details
+
+    def select_entities_to_convert(self, pred, k, degree_cap=None, criage=False):
+        """engine.py:22-126."""
+        ds = self.ds
+        s, p, o = pred
+        ents = []
+        for e in range(ds.num_entities):
+            if e == s:
+                continue
+            deg = ds.entity_to_degree.get(e, 0)
+            if deg < 1:
+                continue
+            if degree_cap and deg > degree_cap:
+                continue
+            if criage and e not in self.o_to_training:
+                continue
+            if (e, p) in ds.to_filter:
+                if ds.relation_to_type[p] in (ONE_TO_ONE, MANY_TO_ONE):
+                    continue
+                if o in ds.to_filter[(e, p)]:
+                    continue
+            ents.append(e)
+        if not ents:
+            return []
+        out = []
+        for i0 in range(0, len(ents), 4):
+            chunk = ents[i0:i0 + 4]
+            sc = self.model.all_scores([(e, p, o) for e in chunk])
+            for j, e in enumerate(chunk):
+                row = sc[j].copy()
+                F = ds.to_filter.get((e, p), [])
+                t = row[o]
+                if self.model.is_minimizer():
+                    row[F] = 1e6
+                    if 1e6 > t > row.min():
+                        out.append(e)
+                else:
+                    row[F] = -1e6
+                    if -1e6 < t < row.max():
+                        out.append(e)
+        return random.sample(out, k=min(k, len(out)))
+
+
+# =============================================================================
+# builder
+# =============================================================================
+def build_explanations(relevance_fn, pred, candidates, xsi, k=10, length_cap=4, window=10):
+    """StochasticBuilder.build_explanations (stochastic_builder.py:33-107, 110-192),
+    without summarisation; returns (rule_to_relevance top-k, #relevances)."""
+    t2r = {}
+    for t in candidates:
+        t2r[t] = relevance_fn(pred, [t])
+    srt = sorted(t2r.items(), key=lambda x: x[1], reverse=True)
+    rule_to_rel = [((t,), r) for t, r in srt]
+    n = len(t2r)
+    nrel = n
+    best = rule_to_rel[0][1]
+    if not best > xsi:
+        for L in range(2, min(n, length_cap) + 1):
+            rules = list(combinations(candidates, L))
+            rules = [(r, sum(t2r[t] for t in r)) for r in rules]
+            rules = sorted(rules, key=lambda x: x[1], reverse=True)
+            terminate = False
+            cbest = -1e6
+            win = [None] * window
+            cur = {}
+            cnt = 0
+            for i, (rule, _) in enumerate(rules):
+                if terminate:
+                    break
+                rel = relevance_fn(pred, list(rule))
+                cur[rule] = rel
+                cnt += 1
+                win[i % window] = rel
+                if rel > xsi:
+                    break
+                elif rel >= cbest:
+                    cbest = rel
+                elif i >= window:
+                    avg = sum(win) / window
+                    thr = avg / cbest
+                    terminate = random.random() > thr
+            nrel += cnt
+            cs = sorted(cur.items(), key=lambda x: x[1], reverse=True)
+            rule_to_rel += cs
+            if cs[0][1] > best:
+                best = cs[0][1]
+            if best > xsi:
+                break
+    rule_to_rel = sorted(rule_to_rel, key=lambda x: (x[1], 1 / len(x[0])), reverse=True)
+    return rule_to_rel[:k], nrel
+
+
+def topology_prefilter(ds: OracleDataset, pred, k):
+    """TopologyPreFilter.select_triples (topology_prefilter.py:18-37): BFS hop
+    distance from the other endpoint to the pred's object over the undirected
+    training multigraph; stable sort; first k."""
+    s, _, o = pred
+    adj = defaultdict(set)
+    for h, _, t in ds.training_triples.tolist():
+        adj[h].add(t)
+        adj[t].add(h)
+
+    def dist(a):
+        if a == o:
+            return 0
+        seen = {a}
+        frontier = [a]
+        d = 0
+        while frontier:
+            d += 1
+            nxt = []
+            for u in frontier:
+                for w in adj[u]:
+                    if w == o:
+                        return d
+                    if w not in seen:
+                        seen.add(w)
+                        nxt.append(w)
+            frontier = nxt
+        return 1e6
+
+    triples = sorted(ds.entity_to_training_triples[s])
+    res = {t: dist(t[2] if t[0] == s else t[0]) for t in triples}
+    res = sorted(res.items(), key=lambda x: x[1])
+    return [t for t, _ in res][:k]

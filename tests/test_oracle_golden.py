@@ -1,0 +1,118 @@
+"""Pin the CPU oracle against golden vectors captured from the reference.
+
+The fixtures were produced by ``tests/golden/make_golden.py`` (reference run on
+CPU in the development container).  Ranks must match exactly; scores and
+relevances within the 1e-4 tolerance of the north star.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from golden_io import CASES, load_case, seed_all
+from oracle import kelpie_oracle as ko
+
+TOL = 1e-4
+
+
+def _setup(name):
+    rec, arrays, weights = load_case(name)
+    ds = ko.OracleDataset(rec["num_entities"], rec["num_relations"], arrays["train"], arrays["valid"], arrays["test"])
+    dim = rec["model_params"]["dimension"]
+    model = ko.OracleModel(rec["model"], weights, dim, rec["model_params"])
+    return rec, ds, model
+
+
+def _check_results(got_pt, got_base, results, first_call):
+    exp = results
+    # order of get_triple_results calls inside one compute_relevance: base (if first), pt
+    if first_call:
+        assert len(exp) == 2
+        eb, ep = exp
+        assert got_base["target_rank"] == eb["target_rank"]
+        assert abs(got_base["target_score"] - eb["target_score"]) <= TOL * max(1.0, abs(eb["target_score"]))
+    else:
+        ep = exp[-1]
+    assert got_pt["target_rank"] == ep["target_rank"]
+    assert abs(got_pt["target_score"] - ep["target_score"]) <= TOL * max(1.0, abs(ep["target_score"]))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_necessary(name):
+    rec, ds, model = _setup(name)
+    seed_all(rec["seed"])
+    eng = ko.OracleEngine(model, ds, rec["hp"])
+    for block in rec["necessary"]:
+        eng.set_cache()
+        pred = tuple(block["pred"])
+        for ci, call in enumerate(block["calls"]):
+            rule = [tuple(t) for t in call["rule"]]
+            rel, pt, base = eng.necessary_relevance(pred, rule)
+            _check_results(pt, base, call["results"], ci == 0)
+            assert abs(rel - call["relevance"]) <= TOL, (name, pred, rule, rel, call["relevance"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_sufficient(name):
+    rec, ds, model = _setup(name)
+    seed_all(rec["seed"])
+    eng = ko.OracleEngine(model, ds, rec["hp"])
+    for block in rec["sufficient"]:
+        eng.set_cache()
+        pred = tuple(block["pred"])
+        ents = eng.select_entities_to_convert(pred, block["k"], block["degree_cap"])
+        assert ents == block["entities_to_convert"]
+        seen = set()
+        for call in block["calls"]:
+            rule = [tuple(t) for t in call["rule"]]
+            rel, details = eng.sufficient_relevance(pred, rule, ents)
+            assert abs(rel - call["relevance"]) <= TOL, (name, rule, rel, call["relevance"])
+            _check_sufficient_details(details, call["results"], seen, ents, pred)
+
+
+def _check_sufficient_details(details, results, seen, ents, pred):
+    idx = 0
+    for (pt, base), e in zip(details, ents):
+        cp = ko.replace_entity(pred, pred[0], e)
+        if cp not in seen:
+            eb = results[idx]
+            assert base["target_rank"] == eb["target_rank"]
+            assert abs(base["target_score"] - eb["target_score"]) <= TOL * max(1, abs(eb["target_score"]))
+            idx += 1
+            seen.add(cp)
+        ep = results[idx]
+        idx += 1
+        assert pt["target_rank"] == ep["target_rank"]
+        assert abs(pt["target_score"] - ep["target_score"]) <= TOL * max(1, abs(ep["target_score"]))
+    assert idx == len(results)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_prefilter(name):
+    rec, ds, model = _setup(name)
+    for pf in rec["prefilter"]:
+        got = ko.topology_prefilter(ds, tuple(pf["pred"]), pf["k"])
+        assert [list(t) for t in got] == pf["triples"]
+
+
+@pytest.mark.parametrize("name", [c for c in CASES if c != "complex_adam_tiny"])
+def test_oracle_builder(name):
+    rec, ds, model = _setup(name)
+    for key in ("builder", "builder_window"):
+        b = rec.get(key)
+        if not b:
+            continue
+        seed_all(rec["seed"])
+        eng = ko.OracleEngine(model, ds, rec["hp"])
+        eng.set_cache()
+        pred = tuple(b["pred"])
+        cands = [tuple(t) for t in b["candidates"]]
+        fn = lambda p, rule: eng.necessary_relevance(p, rule)[0]
+        out, nrel = ko.build_explanations(fn, pred, cands, b["xsi"])
+        assert nrel == b["n_relevances"]
+        exp = b["rule_to_relevance"]
+        assert len(out) == len(exp)
+        for (rule, rel), (erule_labels, erel) in zip(out, exp):
+            erule = [(int(a[1:]), int(b[1:]), int(c[1:])) for a, b, c in erule_labels]
+            assert list(rule) == erule
+            assert abs(rel - erel) <= TOL
