@@ -1,0 +1,26 @@
+# Builds the gfx950 HIP library kelpie_amd/libkelpie_hip.so (C ABI: include/kelpie_hip.h)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+SRC := $(wildcard kelpie_amd/csrc/*.hip)
+OBJ := $(patsubst kelpie_amd/csrc/%.hip,build/%.o,$(SRC))
+FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+         -Wno-unused-result -Iinclude
+LIB := kelpie_amd/libkelpie_hip.so
+
+all: $(LIB)
+
+build/%.o: kelpie_amd/csrc/%.hip kelpie_amd/csrc/kp_common.hpp include/kelpie_hip.h
+	@mkdir -p build
+	$(HIPCC) $(FLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+
+resources: $(SRC)
+	@mkdir -p build
+	for f in $(SRC); do $(HIPCC) $(FLAGS) -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Spill|Occupancy|LDS" ; done
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean resources

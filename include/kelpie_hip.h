@@ -1,0 +1,183 @@
+/*
+ * kelpie_hip.h -- C ABI of the MI355X-native Kelpie relevance engine.
+ *
+ * The reference has no FFI: its relevance engine is the Python class API of
+ * src/relevance_engines/post_training_engine.py.  This library replaces the
+ * arithmetic below that API (KelpieModel construction, the Kelpie optimizers'
+ * post-training loop and get_triple_results' all-entity filtered rank); the
+ * Python package kelpie_amd binds it with ctypes and re-exposes the
+ * reference's class interface (NecessaryPostTrainingEngine, ...).  Each entry
+ * point names the reference code it replaces.
+ *
+ * Conventions
+ *   - every function returns 0 on success, a negative KP_E* code otherwise;
+ *     kp_last_error(ctx) describes the last failure (thread-local when ctx is
+ *     NULL, e.g. for a failed kp_ctx_create);
+ *   - all pointers are HOST pointers owned by the caller; the context copies
+ *     what it needs to device memory and owns that copy;
+ *   - calls are synchronous at return; a context is not re-entrant (one host
+ *     thread per context);
+ *   - entity ids: frozen entities are [0, n_ent); the kelpie ("mimic") entity
+ *     of a slot has id n_ent, like KelpieDataset.kelpie_entity
+ *     (src/data/kelpie_dataset.py:20-25);
+ *   - relation ids: [0, n_rel2) with n_rel2 = 2|R|; inverse of p is p+|R|
+ *     (src/data/dataset.py:319-331).
+ */
+#ifndef KELPIE_HIP_H
+#define KELPIE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KP_OK 0
+#define KP_EINVAL (-22)
+#define KP_ENOMEM (-12)
+#define KP_EDEVICE (-5)
+#define KP_ENOTSUP (-95)
+
+/* model families (src/link_prediction/__init__.py:5-9, MODEL_REGISTRY) */
+#define KP_MODEL_TRANSE 0
+#define KP_MODEL_COMPLEX 1
+#define KP_MODEL_CONVE 2
+
+/* optimizers (multiclass_nll_optimizer.py:41-48; Kelpie TransE / ConvE use Adam) */
+#define KP_OPT_ADAGRAD 0
+#define KP_OPT_ADAM 1
+#define KP_OPT_SGD 2
+
+typedef struct kp_ctx kp_ctx;
+
+/* Frozen model tables.  Replaces the E/R clones every KelpieModel makes per
+ * candidate (transe.py:86-87, complex.py:146-147, conve.py:206-207): the
+ * tables are uploaded ONCE per context and shared by every slot. */
+typedef struct {
+  int32_t model;      /* KP_MODEL_* */
+  int32_t n_ent;      /* |E| */
+  int32_t n_rel2;     /* 2|R| */
+  int32_t dim;        /* row width: TransE/ConvE d, ComplEx 2d ([Re | Im], complex.py:24-25) */
+  const float* entity;   /* [n_ent][dim] */
+  const float* relation; /* [n_rel2][dim] */
+  /* ConvE frozen layers (conve.py:40-52, frozen copies at :214-237); NULL otherwise */
+  const float* conv_w;   /* [32][3][3] (Conv2d(1,32,3) weight) */
+  const float* conv_b;   /* [32] */
+  const float* fc_w;     /* [dim][hidden], hidden = 32*38*(dim/20-2) */
+  const float* fc_b;     /* [dim] */
+  const float* bn_alpha; /* [1 + 32 + dim]: eval-mode BN1|BN2|BN3 scale  w/sqrt(var+eps) */
+  const float* bn_beta;  /* [1 + 32 + dim]: eval-mode BN1|BN2|BN3 shift  b - mean*scale  */
+} kp_model_desc;
+
+/* Post-training hyper-parameters (the *_explanation.json "training" block,
+ * validated by the optimizers' HyperParams classes). */
+typedef struct {
+  int32_t optimizer;     /* KP_OPT_*; TransE and ConvE: KP_OPT_ADAM */
+  int32_t epochs;
+  int32_t batch_size;
+  float lr;              /* ConvE: 1e-3 (KelpieBCEOptimizer ignores hp lr, bce_optimizer.py:165) */
+  float beta1, beta2;    /* Adam betas */
+  float eps;             /* Adagrad 1e-10, Adam 1e-8 */
+  float reg_weight;      /* ComplEx N3 weight / TransE L2 weight */
+  float margin;          /* TransE */
+  int32_t neg_ratio;     /* TransE negative_triples_ratio */
+  float label_smoothing; /* ConvE */
+  float hidden_dropout;  /* ConvE hidden dropout rate (masks are inputs) */
+} kp_hp;
+
+/* One batch of post-training slots.  A slot is one KelpieModel post-training
+ * (PostTrainingEngine.post_train, post_training_engine.py:64-76) followed by
+ * get_triple_results (:101-125).  Base and post-trained models are both just
+ * slots.
+ *
+ *   x0          [n_slots][dim]   initial kelpie row (after the model's init:
+ *                                ComplEx init*init_scale, TransE xavier, ConvE raw)
+ *   row_off     [n_slots+1]      CSR offsets into rows
+ *   rows        [total][3]       training rows of each slot: the kelpie triples
+ *                                followed by their inverses, in reference order
+ *                                (optimizer.train's vstack(triples, inverse))
+ *   rng_off     [n_slots+1]      CSR offsets (in int32 words) into rng
+ *   rng         [...]            per-slot random draws, generated on the host in
+ *                                reference order (RNG-as-input):
+ *       ComplEx: epochs x R permutation (torch.randperm, multiclass_nll_optimizer.py:148)
+ *       TransE:  epochs x [R row order | R negative entities | R head_or_tail]
+ *                (pairwise_ranking_optimizer.py:166-181; only rows [0,R) are stepped)
+ *       ConvE:   per step: ceil(b*dim/32) words of hidden-dropout keep bits
+ *   pred        [n_slots][3]     kelpie-form triple to rank (s = n_ent)
+ *   filt_off    [n_slots+1]      CSR offsets into filt
+ *   filt        [...]            entities filtered out of the rank (to_filter[(s,p)]
+ *                                of the slot's KelpieDataset after the edit)
+ * outputs:
+ *   out_x       [n_slots][dim]   final kelpie rows (may be NULL)
+ *   out_score   [n_slots]        target score  (all_scores[o])
+ *   out_rank    [n_slots]        filtered rank (minimizer: <=, o restored before
+ *                                counting; maximizer: >=, o excluded if filtered)
+ */
+typedef struct {
+  int32_t n_slots;
+  const float* x0;
+  const int32_t* row_off;
+  const int32_t* rows;
+  const int64_t* rng_off;
+  const int32_t* rng;
+  const int32_t* pred;
+  const int32_t* filt_off;
+  const int32_t* filt;
+  float* out_x;
+  float* out_score;
+  int64_t* out_rank;
+} kp_batch;
+
+/* Create a context on HIP device `device` and upload the frozen tables. */
+int kp_ctx_create(int device, const kp_model_desc* model, kp_ctx** out);
+int kp_ctx_destroy(kp_ctx* ctx);
+const char* kp_last_error(const kp_ctx* ctx);
+
+/* Post-train every slot of the batch and rank its target triple.
+ * Replaces, per slot: KelpieX(...) construction, Kelpie*Optimizer.train
+ * (pairwise_ranking_optimizer.py:160-203, multiclass_nll_optimizer.py:138-164,
+ * bce_optimizer.py:161-208) and PostTrainingEngine.get_triple_results
+ * (post_training_engine.py:101-125). */
+int kp_posttrain_rank(kp_ctx* ctx, const kp_hp* hp, const kp_batch* batch);
+
+/* Model.all_scores (model.py:19; transe.py:48-65, complex.py:88-112,
+ * conve.py:133-158) for n (head, relation) pairs over the frozen entities:
+ * out[n][n_ent].  The RelevanceEngine.select_entities_to_convert sweep
+ * (engine.py:94-101) is built on it. */
+int kp_all_scores(kp_ctx* ctx, int32_t n, const int32_t* heads, const int32_t* rels, float* out);
+
+/* Filtered-rank sweep of engine.py:89-120 for n candidate heads e with
+ * relation p and object o: keep[i] = 1 iff o is not the model's top-1 for
+ * (e,p,.) once to_filter[(e,p)] is masked to +-1e6.  filt CSR as in kp_batch. */
+int kp_convertible(kp_ctx* ctx, int32_t n, const int32_t* heads, int32_t rel, int32_t obj,
+                   const int32_t* filt_off, const int32_t* filt, uint8_t* keep);
+
+/* Advance a torch CPU generator state (the 5056-byte torch.get_rng_state()
+ * blob) by n 32-bit mt19937 outputs, in place.  Used by the host RNG protocol
+ * to replay the draws of reset_parameters() that each KelpieConvE
+ * construction makes (conve.py:46-52 via :202) without materialising them. */
+int kp_mt19937_discard(uint8_t* state, size_t state_len, uint64_t n);
+
+/* Keep-mask of torch.empty(n).bernoulli_(p) on the CPU generator (ATen draws
+ * one random64 = (hi << 32) | lo per element; keep iff u53 * 2^-53 < p), written
+ * as packed bits (bit i of word i/32) and advancing the state blob in place.
+ * Replaces the per-step hidden-dropout mask draw of KelpieConvE training
+ * (conve.py:151 via model.py:114-125, Dropout stays in train mode). */
+int kp_rng_bernoulli_bits(uint8_t* state, size_t state_len, uint64_t n, double p, uint32_t* out_bits);
+
+/* Device time of the last kp_posttrain_rank (HIP events on the context's
+ * stream): the whole call, the summed durations of its dominant kernel's
+ * launches, their count, and the work units those launches processed
+ * (ComplEx: query rows x frozen entities; TransE: slot-epochs; ConvE:
+ * encoder rows x frozen entities).  bench.py derives the roofline from it. */
+int kp_last_timing(const kp_ctx* ctx, double* device_seconds, double* hot_kernel_seconds,
+                   int64_t* hot_kernel_launches, double* hot_work_units);
+
+/* Library version string. */
+const char* kp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KELPIE_HIP_H */

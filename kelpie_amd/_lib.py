@@ -1,0 +1,169 @@
+"""ctypes binding of ``libkelpie_hip.so`` (C ABI: ``include/kelpie_hip.h``).
+
+The library is built in-tree (``make`` / ``__graft_entry__.build()``) for gfx950.
+There is no CPU fallback: if the library is missing every engine call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("KELPIE_HIP_LIB", os.path.join(_HERE, "libkelpie_hip.so"))
+
+KP_MODEL = {"TransE": 0, "ComplEx": 1, "ConvE": 2}
+KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
+
+# symbols declared by include/kelpie_hip.h
+EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_rank", "kp_all_scores",
+           "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits"]
+
+
+class ModelDesc(C.Structure):
+    _fields_ = [("model", C.c_int32), ("n_ent", C.c_int32), ("n_rel2", C.c_int32), ("dim", C.c_int32),
+                ("entity", C.c_void_p), ("relation", C.c_void_p), ("conv_w", C.c_void_p), ("conv_b", C.c_void_p),
+                ("fc_w", C.c_void_p), ("fc_b", C.c_void_p), ("bn_alpha", C.c_void_p), ("bn_beta", C.c_void_p)]
+
+
+class HP(C.Structure):
+    _fields_ = [("optimizer", C.c_int32), ("epochs", C.c_int32), ("batch_size", C.c_int32), ("lr", C.c_float),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("reg_weight", C.c_float),
+                ("margin", C.c_float), ("neg_ratio", C.c_int32), ("label_smoothing", C.c_float),
+                ("hidden_dropout", C.c_float)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("n_slots", C.c_int32), ("x0", C.c_void_p), ("row_off", C.c_void_p), ("rows", C.c_void_p),
+                ("rng_off", C.c_void_p), ("rng", C.c_void_p), ("pred", C.c_void_p), ("filt_off", C.c_void_p),
+                ("filt", C.c_void_p), ("out_x", C.c_void_p), ("out_score", C.c_void_p), ("out_rank", C.c_void_p)]
+
+
+class KelpieHipError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def lib():
+    """Load the HIP library (raises if it is absent: no silent fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise KelpieHipError(f"{LIB_PATH} not found: build it with `make` (hipcc --offload-arch=gfx950)")
+        L = C.CDLL(LIB_PATH)
+        L.kp_ctx_create.argtypes = [C.c_int, C.POINTER(ModelDesc), C.POINTER(C.c_void_p)]
+        L.kp_ctx_destroy.argtypes = [C.c_void_p]
+        L.kp_last_error.argtypes = [C.c_void_p]
+        L.kp_last_error.restype = C.c_char_p
+        L.kp_posttrain_rank.argtypes = [C.c_void_p, C.POINTER(HP), C.POINTER(Batch)]
+        L.kp_all_scores.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.kp_convertible.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]
+        L.kp_mt19937_discard.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.kp_rng_bernoulli_bits.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_double, C.c_void_p]
+        L.kp_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+        L.kp_version.restype = C.c_char_p
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def check(rc, ctx=None):
+    if rc != 0:
+        msg = lib().kp_last_error(ctx).decode(errors="replace")
+        raise KelpieHipError(f"libkelpie_hip error {rc}: {msg}")
+
+
+def mt19937_discard(state: np.ndarray, n: int):
+    """Advance a torch CPU-generator state blob (uint8[5056]) by n 32-bit draws, in place."""
+    assert state.dtype == np.uint8 and state.flags.c_contiguous
+    check(lib().kp_mt19937_discard(_ptr(state), state.size, int(n)))
+
+
+def bernoulli_bits(state: np.ndarray, n: int, p: float) -> np.ndarray:
+    """Keep-mask of ``torch.empty(n).bernoulli_(p)`` as packed little-endian bits
+    (uint32 words), advancing the state blob in place like torch does."""
+    words = np.zeros((n + 31) // 32, dtype=np.uint32)
+    check(lib().kp_rng_bernoulli_bits(_ptr(state), state.size, int(n), float(p), _ptr(words)))
+    return words
+
+
+class Context:
+    """One device context holding the frozen model tables (kp_ctx)."""
+
+    def __init__(self, model_name, entity, relation, conve=None, device=0):
+        L = lib()
+        self._keep = []
+        E = np.ascontiguousarray(entity, dtype=np.float32)
+        R = np.ascontiguousarray(relation, dtype=np.float32)
+        d = ModelDesc(KP_MODEL[model_name], E.shape[0], R.shape[0], E.shape[1], _ptr(E), _ptr(R))
+        self._keep += [E, R]
+        if conve is not None:
+            for k in ("conv_w", "conv_b", "fc_w", "fc_b", "bn_alpha", "bn_beta"):
+                a = np.ascontiguousarray(conve[k], dtype=np.float32)
+                self._keep.append(a)
+                setattr(d, k, _ptr(a))
+        h = C.c_void_p()
+        rc = L.kp_ctx_create(int(device), C.byref(d), C.byref(h))
+        if rc != 0:
+            raise KelpieHipError(f"kp_ctx_create failed ({rc}): {L.kp_last_error(None).decode()}")
+        self.h = h
+        self.n_ent, self.dim = E.shape
+        self._keep = []  # tables are copied to the device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kp_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def posttrain_rank(self, hp: HP, x0, row_off, rows, rng_off, rng, pred, filt_off, filt, want_x=False):
+        n = len(row_off) - 1
+        x0 = np.ascontiguousarray(x0, dtype=np.float32)
+        row_off = np.ascontiguousarray(row_off, dtype=np.int32)
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        rng_off = np.ascontiguousarray(rng_off, dtype=np.int64)
+        rng = np.ascontiguousarray(rng, dtype=np.int32)
+        pred = np.ascontiguousarray(pred, dtype=np.int32)
+        filt_off = np.ascontiguousarray(filt_off, dtype=np.int32)
+        filt = np.ascontiguousarray(filt, dtype=np.int32)
+        out_x = np.zeros((n, self.dim), np.float32) if want_x else None
+        out_s = np.zeros(n, np.float32)
+        out_r = np.zeros(n, np.int64)
+        b = Batch(n, _ptr(x0), _ptr(row_off), _ptr(rows), _ptr(rng_off), _ptr(rng), _ptr(pred), _ptr(filt_off),
+                  _ptr(filt), _ptr(out_x), _ptr(out_s), _ptr(out_r))
+        check(lib().kp_posttrain_rank(self.h, C.byref(hp), C.byref(b)), self.h)
+        return out_s, out_r, out_x
+
+    def all_scores(self, heads, rels):
+        heads = np.ascontiguousarray(heads, dtype=np.int32)
+        rels = np.ascontiguousarray(rels, dtype=np.int32)
+        out = np.zeros((len(heads), self.n_ent), np.float32)
+        check(lib().kp_all_scores(self.h, len(heads), _ptr(heads), _ptr(rels), _ptr(out)), self.h)
+        return out
+
+    def convertible(self, heads, rel, obj, filt_off, filt):
+        heads = np.ascontiguousarray(heads, dtype=np.int32)
+        filt_off = np.ascontiguousarray(filt_off, dtype=np.int32)
+        filt = np.ascontiguousarray(filt, dtype=np.int32)
+        keep = np.zeros(len(heads), np.uint8)
+        check(lib().kp_convertible(self.h, len(heads), _ptr(heads), int(rel), int(obj), _ptr(filt_off),
+                                   _ptr(filt), _ptr(keep)), self.h)
+        return keep
+
+    def last_timing(self):
+        a, b, n, w = C.c_double(), C.c_double(), C.c_int64(), C.c_double()
+        check(lib().kp_last_timing(self.h, C.byref(a), C.byref(b), C.byref(n), C.byref(w)), self.h)
+        return {"device_s": a.value, "hot_s": b.value, "hot_launches": n.value, "hot_work": w.value}

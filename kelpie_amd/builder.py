@@ -1,0 +1,111 @@
+"""Stochastic explanation builder driving the batched engine.
+
+Same algorithm, output and RNG use as the reference
+``src/explanation_builders/stochastic_builder.py:13-192`` (without
+summarisation), restructured for a batched engine:
+
+* all singleton rules of a prediction are evaluated in ONE engine batch
+  (the reference's hot loop A, ``:110-124``);
+* compound rules are evaluated in speculative windows of ``window`` rules in
+  prescore order (hot loop B, ``:126-175``).  The accept / early-return /
+  ``random.random()`` termination logic is then replayed sequentially over the
+  window's relevances; if the search stops inside the window, the torch /
+  numpy generators are rewound to the state right after the last rule the
+  reference would have evaluated, so every later draw is unchanged.
+"""
+from __future__ import annotations
+
+import itertools
+import random
+import time
+
+
+class StochasticBuilder:
+    def __init__(self, xsi, engine, summarization: str = None, max_explanation_length: int = 4, window: int = 32):
+        if summarization is not None:
+            raise NotImplementedError("summarisation (simulation / bisimulation) is out of scope")
+        self.xsi = xsi
+        self.engine = engine
+        self.dataset = engine.dataset
+        self.length_cap = max_explanation_length
+        self.window_size = 10  # the reference's sliding window (stochastic_builder.py:24)
+        self.spec_window = max(1, int(window))
+        self.summarization = None
+        self.stats = {"batches": 0, "evaluated": 0, "wasted": 0}
+
+    def build_explanations(self, pred, candidate_triples: list, k: int = 10):
+        start = time.time()
+        candidate_triples = [tuple(int(v) for v in t) for t in candidate_triples]
+        triple_to_rel = self.explore_singleton_rules(pred, candidate_triples)
+        srt = sorted(triple_to_rel.items(), key=lambda x: x[1], reverse=True)
+        rule_to_rel = [((t,), rel) for (t, rel) in srt]
+        triples_number = len(triple_to_rel)
+        rels_num = triples_number
+        _, best = rule_to_rel[0]
+        if not best > self.xsi:
+            for rule_length in range(2, min(triples_number, self.length_cap) + 1):
+                cur, cur_n = self.explore_compound_rules(pred, candidate_triples, rule_length, triple_to_rel)
+                rels_num += cur_n
+                cur = sorted(cur.items(), key=lambda x: x[1], reverse=True)
+                rule_to_rel += cur
+                _, current_best = cur[0]
+                if current_best > best:
+                    best = current_best
+                if best > self.xsi:
+                    break
+        rule_to_rel = sorted(rule_to_rel, key=lambda x: (x[1], 1 / len(x[0])), reverse=True)[:k]
+        mapped = [(self.dataset.labels_triples(rule), rel) for rule, rel in rule_to_rel]
+        return {"triple": self.dataset.labels_triple(tuple(pred)), "rule_to_relevance": mapped,
+                "#relevances": rels_num, "execution_time": time.time() - start,
+                "rules": rule_to_rel}
+
+    def explore_singleton_rules(self, pred, triples: list):
+        # one engine batch for every singleton; a duplicated candidate is evaluated
+        # once per occurrence and the last value wins, like the dict of :113-123
+        rels = self.engine.compute_relevance_batch(pred, [[t] for t in triples])
+        self.stats["batches"] += 1
+        self.stats["evaluated"] += len(triples)
+        out = {}
+        for t, r in zip(triples, rels):
+            out[t] = r
+        return out
+
+    def explore_compound_rules(self, pred, triples, length, triple_to_relevance):
+        rules = itertools.combinations(triples, length)
+        rules = [(r, sum(triple_to_relevance[t] for t in r)) for r in rules]
+        rules = sorted(rules, key=lambda x: x[1], reverse=True)
+        terminate = False
+        best = -1e6
+        window = [None] * self.window_size
+        rule_to_relevance = {}
+        computed = 0
+        i = 0
+        while i < len(rules) and not terminate:
+            chunk = [r for r, _ in rules[i:i + self.spec_window]]
+            cps = []
+            rels = self.engine.compute_relevance_batch(pred, [list(r) for r in chunk], checkpoints=cps)
+            self.stats["batches"] += 1
+            self.stats["evaluated"] += len(chunk)
+            stop_at = None
+            for j, rel in enumerate(rels):
+                ii = i + j
+                rule = chunk[j]
+                rule_to_relevance[rule] = rel
+                computed += 1
+                window[ii % self.window_size] = rel
+                if rel > self.xsi:
+                    stop_at, terminate = j, True
+                    break
+                elif rel >= best:
+                    best = rel
+                elif ii >= self.window_size:
+                    avg = sum(window) / self.window_size
+                    thr = avg / best
+                    if random.random() > thr:
+                        stop_at, terminate = j, True
+                        break
+            if stop_at is not None and stop_at + 1 < len(chunk):
+                cps[stop_at].restore()  # rewind the speculative draws
+                self.stats["wasted"] += len(chunk) - stop_at - 1
+            i += len(chunk)
+        return rule_to_relevance, computed

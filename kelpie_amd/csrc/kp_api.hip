@@ -1,0 +1,285 @@
+// kp_api.hip -- C ABI entry points of libkelpie_hip.so (include/kelpie_hip.h).
+#include <cmath>
+#include <cstdio>
+
+#include "kp_common.hpp"
+
+int cx_pick_db(int dim);
+
+static thread_local std::string g_tls_err;
+
+template <class F>
+static int guarded(kp_ctx* c, F&& f) {
+  try {
+    f();
+    if (c) c->err.clear();
+    return KP_OK;
+  } catch (const KpError& e) {
+    if (c) c->err = e.msg;
+    g_tls_err = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    if (c) c->err = "host out of memory";
+    g_tls_err = "host out of memory";
+    return KP_ENOMEM;
+  } catch (...) {
+    if (c) c->err = "unknown error";
+    g_tls_err = "unknown error";
+    return KP_EINVAL;
+  }
+}
+
+static void upload_padded(kp_ctx* c, float** dst, const float* src, int rows, int dim, int dp) {
+  std::vector<float> tmp((size_t)rows * dp, 0.f);
+  for (int r = 0; r < rows; ++r) std::memcpy(&tmp[(size_t)r * dp], src + (size_t)r * dim, sizeof(float) * dim);
+  KP_HIP(hipMalloc(dst, sizeof(float) * tmp.size() + 64));
+  KP_HIP(hipMemcpy(*dst, tmp.data(), sizeof(float) * tmp.size(), hipMemcpyHostToDevice));
+}
+
+static void upload_plain(float** dst, const float* src, size_t n) {
+  KP_HIP(hipMalloc(dst, sizeof(float) * n + 64));
+  KP_HIP(hipMemcpy(*dst, src, sizeof(float) * n, hipMemcpyHostToDevice));
+}
+
+extern "C" {
+
+const char* kp_version(void) { return "kelpie_hip 0.1 (gfx950)"; }
+
+const char* kp_last_error(const kp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_tls_err.c_str(); }
+
+int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
+  if (!out || !m) return KP_EINVAL;
+  *out = nullptr;
+  kp_ctx* c = new kp_ctx();
+  int rc = guarded(nullptr, [&] {
+    KP_REQUIRE(m->n_ent > 0 && m->n_rel2 > 0 && m->dim > 0, "kp_ctx_create: empty model");
+    KP_REQUIRE(m->entity && m->relation, "kp_ctx_create: missing tables");
+    KP_REQUIRE(m->model >= KP_MODEL_TRANSE && m->model <= KP_MODEL_CONVE, "kp_ctx_create: unknown model");
+    c->device = device;
+    c->model = m->model;
+    c->n_ent = m->n_ent;
+    c->n_rel2 = m->n_rel2;
+    c->dim = m->dim;
+    KP_HIP(hipSetDevice(device));
+    if (m->model == KP_MODEL_COMPLEX) {
+      KP_REQUIRE(m->dim % 2 == 0, "ComplEx: row width must be even ([Re | Im])");
+      int db = cx_pick_db(m->dim);
+      KP_REQUIRE(db > 0, "ComplEx: row width > 400 not supported yet");
+      c->dp = 16 * db;
+    } else {
+      c->dp = round_up(m->dim, 16);
+    }
+    KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    KP_HIP(hipEventCreate(&c->ev0));
+    KP_HIP(hipEventCreate(&c->ev1));
+    upload_padded(c, &c->dE, m->entity, m->n_ent, m->dim, c->dp);
+    upload_padded(c, &c->dR, m->relation, m->n_rel2, m->dim, c->dp);
+    if (m->model == KP_MODEL_CONVE) {
+      KP_REQUIRE(m->conv_w && m->conv_b && m->fc_w && m->fc_b && m->bn_alpha && m->bn_beta,
+                 "ConvE: missing frozen layers");
+      KP_REQUIRE(m->dim % 20 == 0 && m->dim / 20 >= 3, "ConvE: dim must be 20*h with h >= 3");
+      c->hidden = 32 * 38 * (m->dim / 20 - 2);
+      upload_plain(&c->d_conv_w, m->conv_w, 32 * 9);
+      upload_plain(&c->d_conv_b, m->conv_b, 32);
+      upload_plain(&c->d_fc_w, m->fc_w, (size_t)m->dim * c->hidden);
+      upload_plain(&c->d_fc_b, m->fc_b, m->dim);
+      upload_plain(&c->d_bn_a, m->bn_alpha, 1 + 32 + m->dim);
+      upload_plain(&c->d_bn_b, m->bn_beta, 1 + 32 + m->dim);
+    }
+  });
+  if (rc != KP_OK) {
+    kp_ctx_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return KP_OK;
+}
+
+int kp_ctx_destroy(kp_ctx* c) {
+  if (!c) return KP_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (float* p : {c->dE, c->dR, c->dEt, c->d_conv_w, c->d_conv_b, c->d_fc_w, c->d_fc_b, c->d_bn_a, c->d_bn_b})
+    if (p) (void)hipFree(p);
+  for (auto& b : c->ws) b.release();
+  for (auto e : c->evpool) (void)hipEventDestroy(e);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return KP_OK;
+}
+
+int kp_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* b) {
+  if (!c || !hp || !b) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_REQUIRE(b->n_slots >= 0, "kp_posttrain_rank: negative n_slots");
+    if (b->n_slots == 0) return;
+    KP_REQUIRE(b->x0 && b->row_off && b->pred && b->filt_off && b->out_score && b->out_rank,
+               "kp_posttrain_rank: missing buffer");
+    KP_HIP(hipSetDevice(c->device));
+    switch (c->model) {
+      case KP_MODEL_COMPLEX: complex_posttrain_rank(c, hp, b); break;
+      case KP_MODEL_TRANSE: transe_posttrain_rank(c, hp, b); break;
+      case KP_MODEL_CONVE: conve_posttrain_rank(c, hp, b); break;
+    }
+  });
+}
+
+int kp_all_scores(kp_ctx* c, int32_t n, const int32_t* heads, const int32_t* rels, float* out) {
+  if (!c || n < 0 || (n > 0 && (!heads || !rels || !out))) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_HIP(hipSetDevice(c->device));
+    for (int i = 0; i < n; ++i) {
+      KP_REQUIRE(heads[i] >= 0 && heads[i] < c->n_ent, "kp_all_scores: head out of range");
+      KP_REQUIRE(rels[i] >= 0 && rels[i] < c->n_rel2, "kp_all_scores: relation out of range");
+    }
+    switch (c->model) {
+      case KP_MODEL_COMPLEX: complex_all_scores(c, n, heads, rels, out); break;
+      case KP_MODEL_TRANSE: transe_all_scores(c, n, heads, rels, out); break;
+      case KP_MODEL_CONVE: conve_all_scores(c, n, heads, rels, out); break;
+    }
+  });
+}
+
+int kp_convertible(kp_ctx* c, int32_t n, const int32_t* heads, int32_t rel, int32_t obj, const int32_t* filt_off,
+                   const int32_t* filt, uint8_t* keep) {
+  if (!c || n < 0 || (n > 0 && (!heads || !filt_off || !keep))) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_REQUIRE(obj >= 0 && obj < c->n_ent, "kp_convertible: object out of range");
+    KP_REQUIRE(rel >= 0 && rel < c->n_rel2, "kp_convertible: relation out of range");
+    if (n == 0) return;
+    KP_HIP(hipSetDevice(c->device));
+    for (int i = 0; i < n; ++i) KP_REQUIRE(heads[i] >= 0 && heads[i] < c->n_ent, "kp_convertible: head out of range");
+    // engine.py:94-120 -- score chunks of heads on the device, mask the filter, compare with the extreme
+    const size_t budget = (size_t)256 << 20;
+    const int chunk = (int)std::max<size_t>(64, std::min<size_t>(4096, budget / ((size_t)c->n_ent * 4)));
+    const int ld = c->n_ent;
+    std::vector<int32_t> rels(chunk, rel), fo(chunk + 1);
+    DevBuf bS, bH, bR, bFo, bF, bK;
+    float* dS = reinterpret_cast<float*>(bS.ensure(sizeof(float) * (size_t)chunk * ld));
+    const bool minimizer = (c->model == KP_MODEL_TRANSE);
+    for (int i0 = 0; i0 < n; i0 += chunk) {
+      const int m = std::min(chunk, n - i0);
+      int32_t* dH = upload(c, bH, heads + i0, (size_t)m);
+      int32_t* dR = upload(c, bR, rels.data(), (size_t)m);
+      for (int j = 0; j <= m; ++j) fo[j] = filt_off[i0 + j] - filt_off[i0];
+      int32_t* dFo = upload(c, bFo, fo.data(), (size_t)m + 1);
+      int32_t* dF = upload(c, bF, filt + filt_off[i0], (size_t)std::max(1, fo[m]));
+      uint8_t* dK = reinterpret_cast<uint8_t*>(bK.ensure((size_t)m));
+      switch (c->model) {
+        case KP_MODEL_COMPLEX: complex_scores_dev(c, m, dH, dR, dS, ld); break;
+        case KP_MODEL_TRANSE: transe_scores_dev(c, m, dH, dR, dS, ld); break;
+        case KP_MODEL_CONVE: conve_scores_dev(c, m, dH, dR, dS, ld); break;
+      }
+      launch_convertible_reduce(c, m, dS, ld, obj, dFo, dF, minimizer ? 1 : 0, dK);
+      KP_HIP(hipMemcpyAsync(keep + i0, dK, (size_t)m, hipMemcpyDeviceToHost, c->stream));
+      KP_HIP(hipStreamSynchronize(c->stream));
+    }
+    for (DevBuf* b : {&bS, &bH, &bR, &bFo, &bF, &bK}) b->release();
+  });
+}
+
+// MT19937 of ATen (aten/src/ATen/core/MT19937RNGEngine.h) over the legacy
+// CPU-generator state blob returned by torch.get_rng_state():
+//   { u64 seed; i32 left; i32 seeded; u64 next; u64 state[624]; ... }.
+namespace {
+struct Mt {
+  int32_t left;
+  uint64_t next;
+  uint32_t s[624];
+  void load(const uint8_t* st) {
+    std::memcpy(&left, st + 8, 4);
+    std::memcpy(&next, st + 16, 8);
+    for (int i = 0; i < 624; ++i) {
+      uint64_t v;
+      std::memcpy(&v, st + 24 + 8 * i, 8);
+      s[i] = (uint32_t)v;
+    }
+  }
+  void store(uint8_t* st) const {
+    std::memcpy(st + 8, &left, 4);
+    std::memcpy(st + 16, &next, 8);
+    for (int i = 0; i < 624; ++i) {
+      uint64_t v = s[i];
+      std::memcpy(st + 24 + 8 * i, &v, 8);
+    }
+  }
+  void twist() {
+    constexpr int N = 624, M = 397;
+    int i = 0;
+    for (; i < N - M; ++i) {
+      uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
+      s[i] = s[i + M] ^ (y >> 1) ^ ((s[i + 1] & 1u) ? 0x9908b0dfu : 0u);
+    }
+    for (; i < N - 1; ++i) {
+      uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
+      s[i] = s[i + M - N] ^ (y >> 1) ^ ((s[i + 1] & 1u) ? 0x9908b0dfu : 0u);
+    }
+    uint32_t y = (s[N - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
+    s[N - 1] = s[M - 1] ^ (y >> 1) ^ ((s[0] & 1u) ? 0x9908b0dfu : 0u);
+  }
+  uint32_t operator()() {
+    if (--left == 0) {
+      twist();
+      left = 624;
+      next = 0;
+    }
+    uint32_t y = s[next++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+};
+}  // namespace
+
+int kp_rng_bernoulli_bits(uint8_t* st, size_t len, uint64_t n, double p, uint32_t* out) {
+  if (!st || len < 24 + 624 * 8 || (n > 0 && !out)) return KP_EINVAL;
+  Mt mt;
+  mt.load(st);
+  const uint64_t mask53 = (1ULL << 53) - 1;
+  const double scale = std::ldexp(1.0, -53);
+  for (uint64_t w = 0; w < (n + 31) / 32; ++w) out[w] = 0u;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t hi = mt(), lo = mt();
+    uint64_t x = (hi << 32) | lo;
+    double u = (double)(x & mask53) * scale;
+    if (u < p) out[i >> 5] |= 1u << (i & 31);
+  }
+  mt.store(st);
+  return KP_OK;
+}
+
+int kp_mt19937_discard(uint8_t* st, size_t len, uint64_t n) {
+  if (!st || len < 24 + 624 * 8) return KP_EINVAL;
+  Mt mt;
+  mt.load(st);
+  // operator() semantics: --left == 0 -> twist, left = 624, next = 0; then next++
+  while (n > 0) {
+    uint64_t k = std::min<uint64_t>(n, (uint64_t)(mt.left - 1));
+    mt.left -= (int32_t)k;
+    mt.next += k;
+    n -= k;
+    if (n > 0) {
+      mt.twist();
+      mt.left = 624;
+      mt.next = 1;
+      n -= 1;
+    }
+  }
+  mt.store(st);
+  return KP_OK;
+}
+
+int kp_last_timing(const kp_ctx* c, double* dev_s, double* hot_s, int64_t* hot_n, double* hot_w) {
+  if (!c) return KP_EINVAL;
+  if (hot_w) *hot_w = c->timing.hot_work;
+  if (dev_s) *dev_s = c->timing.device_s;
+  if (hot_s) *hot_s = c->timing.hot_s;
+  if (hot_n) *hot_n = c->timing.hot_launches;
+  return KP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,148 @@
+// kp_common.hpp -- shared host/device helpers of the Kelpie HIP library (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kelpie_hip.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define KP_WAVE 64
+
+// ----------------------------------------------------------------------------
+// error plumbing
+// ----------------------------------------------------------------------------
+struct KpError {
+  int code;
+  std::string msg;
+};
+
+#define KP_HIP(expr)                                                              \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess)                                                         \
+      throw KpError{KP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)}; \
+  } while (0)
+
+#define KP_REQUIRE(cond, msg)                         \
+  do {                                                \
+    if (!(cond)) throw KpError{KP_EINVAL, (msg)};     \
+  } while (0)
+
+// grow-only device buffer
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void* ensure(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes > cap) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      size_t want = bytes + bytes / 4;
+      KP_HIP(hipMalloc(&p, want));
+      cap = want;
+    }
+    return p;
+  }
+  template <class T>
+  T* as() { return reinterpret_cast<T*>(p); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Timing {
+  double device_s = 0.0;  // whole call on the device (first upload .. last kernel)
+  double loop_s = 0.0;    // post-training loop
+  double hot_s = 0.0;     // sum of the dominant kernel's launch durations
+  int64_t hot_launches = 0;
+  double hot_work = 0.0;  // work units of the dominant kernel (see kp_last_timing)
+};
+
+struct kp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int model = 0;
+  int n_ent = 0, n_rel2 = 0, dim = 0, dp = 0;  // dp: padded row stride (multiple of 16)
+  int hidden = 0;                              // ConvE
+  float* dE = nullptr;                         // [n_ent][dp] zero-padded
+  float* dR = nullptr;                         // [n_rel2][dp]
+  float* dEt = nullptr;                        // TransE: ||E_e||^2 etc (unused for others)
+  // ConvE frozen layers
+  float* d_conv_w = nullptr;
+  float* d_conv_b = nullptr;
+  float* d_fc_w = nullptr;   // [dim][hidden]
+  float* d_fc_b = nullptr;
+  float* d_bn_a = nullptr;
+  float* d_bn_b = nullptr;
+  std::vector<float> hE;     // host copy (ConvE/TransE helpers)
+  DevBuf ws[24];             // workspace slots (see each model file)
+  std::string err;
+  Timing timing;
+  bool time_hot = true;
+  std::vector<hipEvent_t> evpool;
+  std::vector<std::pair<double, double>> hot_pairs;  // (work units, seconds) per hot launch
+  hipEvent_t event(size_t i) {
+    while (evpool.size() <= i) {
+      hipEvent_t e;
+      KP_HIP(hipEventCreate(&e));
+      evpool.push_back(e);
+    }
+    return evpool[i];
+  }
+};
+
+static inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// upload helper
+template <class T>
+static inline T* upload(kp_ctx* c, DevBuf& b, const T* src, size_t n) {
+  T* d = reinterpret_cast<T*>(b.ensure(n * sizeof(T)));
+  if (n) KP_HIP(hipMemcpyAsync(d, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return d;
+}
+
+// ----------------------------------------------------------------------------
+// device helpers
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ----------------------------------------------------------------------------
+// entry points implemented per model family
+// ----------------------------------------------------------------------------
+void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* b);
+void complex_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rels, float* out);
+// scores of n (head, rel) pairs over the frozen entities into a device buffer [n][ld]
+void complex_scores_dev(kp_ctx* c, int n, const int32_t* d_heads, const int32_t* d_rels, float* d_out, int ld);
+void transe_scores_dev(kp_ctx* c, int n, const int32_t* d_heads, const int32_t* d_rels, float* d_out, int ld);
+void conve_scores_dev(kp_ctx* c, int n, const int32_t* d_heads, const int32_t* d_rels, float* d_out, int ld);
+void launch_convertible_reduce(kp_ctx* c, int n, const float* d_scores, int ld, int obj, const int32_t* d_fo,
+                               const int32_t* d_f, int minimizer, uint8_t* d_keep);
+void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* b);
+void transe_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rels, float* out);
+void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* b);
+void conve_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rels, float* out);
+
+// shared rank kernel launcher (kp_rank.hip): scores [n][ld] already on device,
+// column `kcol` = kelpie score (or -1 when absent)
+void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld, int act);
+void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
+                       const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
+                       int minimizer, float* d_target, int64_t* d_rank);

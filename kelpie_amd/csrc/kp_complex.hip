@@ -1,0 +1,866 @@
+// kp_complex.hip -- ComplEx batched post-training (KelpieComplEx +
+// KelpieMultiClassNLLOptimizer) and ranking, for gfx950.
+//
+// Reference semantics (src/link_prediction/models/complex.py:59-112,144-159,
+// src/link_prediction/optimization/multiclass_nll_optimizer.py:57-164):
+//   rows   = kelpie triples + inverses; per epoch torch.randperm; minibatches of
+//            min(batch_size, R) rows stepping by batch_size;
+//   loss   = CrossEntropy(q_i . E_all^T, t_i) (mean) + N3;  E_all = [E ; x]
+//   step   = Adagrad / Adam / SGD on the single kelpie row x.
+//
+// Decomposition used here (ComplEx), per minibatch of b rows:
+//   * rows whose head is the kelpie ("queries"): q = x o r changes every step.
+//     Rows sharing a relation share q and the softmax, so they are merged
+//     into one query with count c, kelpie-target count ck and frozen-target
+//     sum Tsum.  Each query needs, over the FROZEN entities, the softmax
+//     statistics (m, l) and O = sum_e exp(s_e - m) E_e -> kp_cx_attn, a
+//     flash-attention-shaped pass with K = V = E on fp32 MFMA.
+//   * rows whose head is frozen ("tails"; their target is always the kelpie):
+//     q is fixed, so the frozen log-sum-exp is computed once per batch
+//     (kp_cx_attn in pair mode) and each step only needs q . x.
+//   * the kelpie column (entity |E|) is merged analytically in kp_cx_update,
+//     which assembles the single-row gradient and applies the optimizer.
+//   When R <= batch_size (one step per epoch) the permutation only reorders
+//   the batch, so every epoch reuses one plan; otherwise each (epoch, step)
+//   gets its own plan from the permutation.
+#include <algorithm>
+#include <cmath>
+#include <unordered_map>
+
+#include "kp_common.hpp"
+
+namespace {
+
+struct CxPlan {
+  int b, q_begin, q_count, t_begin, t_count, cnt_l, cnt_r, pad;
+};
+struct CxQuery {
+  int rel, c, ck, tg_begin, tg_count, pad0, pad1, pad2;
+};
+struct CxTail {
+  int pair, c;
+};
+
+constexpr float kNegInf = -__builtin_huge_valf();
+
+// ----------------------------------------------------------------------------
+// q = lhs o rel  (complex.py:65-72): [a c - b e | a e + b c], no fp contraction
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float cx_q(const float* __restrict__ lhs, const float* __restrict__ rel, int d,
+                                      int half) {
+  if (d < half) {
+    float ac = __fmul_rn(lhs[d], rel[d]);
+    float be = __fmul_rn(lhs[d + half], rel[d + half]);
+    return __fsub_rn(ac, be);
+  } else if (d < 2 * half) {
+    int i = d - half;
+    float ae = __fmul_rn(lhs[i], rel[d]);
+    float bc = __fmul_rn(lhs[d], rel[i]);
+    return __fadd_rn(ae, bc);
+  }
+  return 0.f;
+}
+
+// qpair[p] = E[h] o R[r] for the frozen-head rows
+__global__ void kp_cx_qpair(const float* __restrict__ E, const float* __restrict__ R, int dp, int half,
+                            const int2* __restrict__ pairs, int n_pairs, float* __restrict__ out) {
+  int p = blockIdx.x;
+  if (p >= n_pairs) return;
+  int2 hr = pairs[p];
+  const float* lhs = E + (size_t)hr.x * dp;
+  const float* rel = R + (size_t)hr.y * dp;
+  for (int d = threadIdx.x; d < dp; d += blockDim.x) out[(size_t)p * dp + d] = cx_q(lhs, rel, d, half);
+}
+
+// Tsum[q] = sum of frozen target rows of a plan query
+__global__ void kp_cx_tsum(const float* __restrict__ E, int dp, const CxQuery* __restrict__ pq, int nq,
+                           const int32_t* __restrict__ targets, float* __restrict__ tsum) {
+  int q = blockIdx.x;
+  if (q >= nq) return;
+  CxQuery Q = pq[q];
+  for (int d = threadIdx.x; d < dp; d += blockDim.x) {
+    float acc = 0.f;
+    for (int i = 0; i < Q.tg_count; ++i) acc += E[(size_t)targets[Q.tg_begin + i] * dp + d];
+    tsum[(size_t)q * dp + d] = acc;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// kp_cx_attn: per query q, over frozen entities [key_begin, key_end):
+//   m = max_e s_e,  l = sum_e exp(s_e - m),  O = sum_e exp(s_e - m) E_e
+// with s_e = q . E_e.  4 waves x 16 queries per workgroup share a 16-entity
+// E tile in LDS (double buffered, register prefetch).  fp32 MFMA 16x16x4 in the
+// swapped form: S^T = E . Q^T (key on the C row), so P already sits in the
+// B-operand layout of O^T += E^T . P (no LDS round trip for P).
+//   lane l: g = l>>4, c = l&15.  Q fragment qv[j][i] = Q[c][16j+4g+i] stays in
+//   VGPRs; O^T accumulators O[j][r] = O[d = 16j+4g+r][q = c].
+// WITH_O = false: pair mode (queries read from Qpre, only m and l).
+// ----------------------------------------------------------------------------
+template <int DB, bool WITH_O>
+__global__ __launch_bounds__(256, 1) void kp_cx_attn(const float* __restrict__ E, int n_ent, int half,
+                                                     const int2* __restrict__ qdesc,
+                                                     const float* __restrict__ X,
+                                                     const float* __restrict__ R,
+                                                     const float* __restrict__ Qpre, int nq,
+                                                     int keys_per_split, float* __restrict__ out_m,
+                                                     float* __restrict__ out_l, float* __restrict__ out_O) {
+  constexpr int DP = 16 * DB;
+  constexpr int S = DP + 4;  // LDS row stride: 2-way b128 / conflict-free b32
+  constexpr int KT = 16;
+  constexpr int F4_ROW = DP / 4;
+  constexpr int NF4 = KT * F4_ROW;
+  constexpr int PF = (NF4 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][KT][S]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int q = blockIdx.x * 64 + 16 * w + c;
+  const bool valid = q < nq;
+  const int split = blockIdx.y;
+  const int key_begin = split * keys_per_split;
+  const int key_end = min(n_ent, key_begin + keys_per_split);
+
+  // ---- Q fragment -> registers
+  float qv[DB][4];
+  if (WITH_O) {
+    int2 sr = valid ? qdesc[q] : make_int2(0, 0);
+    const float* x = X + (size_t)sr.x * DP;
+    const float* r = R + (size_t)sr.y * DP;
+#pragma unroll
+    for (int j = 0; j < DB; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qv[j][i] = valid ? cx_q(x, r, 16 * j + 4 * g + i, half) : 0.f;
+  } else {
+    const float* qp = Qpre + (size_t)(valid ? q : 0) * DP;
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      float4 v = *reinterpret_cast<const float4*>(qp + 16 * j + 4 * g);
+      qv[j][0] = valid ? v.x : 0.f;
+      qv[j][1] = valid ? v.y : 0.f;
+      qv[j][2] = valid ? v.z : 0.f;
+      qv[j][3] = valid ? v.w : 0.f;
+    }
+  }
+
+  f32x4 O[WITH_O ? DB : 1];
+#pragma unroll
+  for (int j = 0; j < (WITH_O ? DB : 1); ++j) O[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m_run = kNegInf, l_run = 0.f;
+
+  const int nkeys = max(0, key_end - key_begin);
+  const int ntiles = (nkeys + KT - 1) / KT;
+  float4 pf[PF];
+
+  auto gload = [&](int tile) {
+    const int k0 = key_begin + tile * KT;
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      int f = tid + 256 * u;
+      int row = f / F4_ROW, c4 = f - row * F4_ROW;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (f < NF4 && k0 + row < key_end) v = *reinterpret_cast<const float4*>(E + (size_t)(k0 + row) * DP + 4 * c4);
+      pf[u] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+    float* base = lds + buf * (KT * S);
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      int f = tid + 256 * u;
+      if (f < NF4) {
+        int row = f / F4_ROW, c4 = f - row * F4_ROW;
+        *reinterpret_cast<float4*>(base + row * S + 4 * c4) = pf[u];
+      }
+    }
+  };
+
+  if (ntiles > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    const float* Es = lds + (t & 1) * (KT * S);
+    const int k0 = key_begin + t * KT;
+    // ---- S^T tile: s[r] = q_c . E[k0 + 4g + r]
+    f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      float4 a = *reinterpret_cast<const float4*>(Es + c * S + 16 * j + 4 * g);
+      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, qv[j][0], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, qv[j][1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, qv[j][2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, qv[j][3], s, 0, 0, 0);
+    }
+    float sv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sv[r] = (k0 + 4 * g + r < key_end) ? s[r] : kNegInf;
+    float tmax = fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float scale = __expf(m_run - m_new);
+    float p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = __expf(sv[r] - m_new);
+    l_run = l_run * scale + ((p[0] + p[1]) + (p[2] + p[3]));
+    m_run = m_new;
+    if (WITH_O) {
+      if (__any(scale != 1.0f)) {
+#pragma unroll
+        for (int j = 0; j < DB; ++j) O[j] *= scale;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int j = 0; j < DB; ++j) {
+          float a = Es[(4 * g + r) * S + 16 * j + c];
+          O[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, p[r], O[j], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < ntiles) lstore((t + 1) & 1);
+    __syncthreads();
+  }
+
+  float l_tot = l_run + __shfl_xor(l_run, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  if (valid) {
+    const size_t o = (size_t)split * nq + q;
+    if (g == 0) {
+      out_m[o] = m_run;
+      out_l[o] = l_tot;
+    }
+    if (WITH_O) {
+      float* dst = out_O + o * DP;
+#pragma unroll
+      for (int j = 0; j < DB; ++j)
+        *reinterpret_cast<float4*>(dst + 16 * j + 4 * g) = make_float4(O[j][0], O[j][1], O[j][2], O[j][3]);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// kp_cx_update: one workgroup per active slot at this step.  Assembles the
+// single-row gradient of the minibatch loss and applies the
+// optimizer with torch's op order (optim/adagrad.py, optim/adam.py).
+// ----------------------------------------------------------------------------
+struct CxOpt {
+  int kind;
+  float lr, b1, b2, eps;
+  float one_minus_b1, one_minus_b2;
+  float step_size;  // Adam: lr / (1 - b1^t)
+  float bc2_sqrt;   // Adam: sqrt(1 - b2^t)
+  float reg_w;
+};
+
+#define UPD_CHUNK 64
+#define UPD_MAXSPLIT 16
+
+template <int DP>
+__global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __restrict__ act,
+                                                    const CxPlan* __restrict__ plans,
+                                                    const CxQuery* __restrict__ pq,
+                                                    const CxTail* __restrict__ pt,
+                                                    const float* __restrict__ R,
+                                                    const float* __restrict__ Tsum,
+                                                    const float* __restrict__ Qpair,
+                                                    const float* __restrict__ lsef,
+                                                    const float* __restrict__ att_m,
+                                                    const float* __restrict__ att_l,
+                                                    const float* __restrict__ att_O, int nq_step,
+                                                    int n_split, float* __restrict__ X,
+                                                    float* __restrict__ S1, float* __restrict__ S2,
+                                                    CxOpt opt) {
+  __shared__ __attribute__((aligned(16))) float xs[DP];
+  __shared__ float s_pk[UPD_CHUNK];
+  __shared__ float s_cf[UPD_CHUNK];
+  __shared__ float s_w[UPD_CHUNK][UPD_MAXSPLIT];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int4 a4 = act[blockIdx.x];
+  const int slot = a4.x;
+  const CxPlan P = plans[a4.y];
+  const int qoff = a4.z;
+  float* x = X + (size_t)slot * DP;
+  for (int d = tid; d < DP; d += 256) xs[d] = x[d];
+  __syncthreads();
+
+  constexpr int PER = (DP / 2 + 255) / 256 > 0 ? (DP / 2 + 255) / 256 : 1;
+  float gre[PER], gim[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) gre[u] = gim[u] = 0.f;
+
+  // ---------------- kelpie-head queries
+  for (int c0 = 0; c0 < P.q_count; c0 += UPD_CHUNK) {
+    const int cn = min(UPD_CHUNK, P.q_count - c0);
+    for (int j = w; j < cn; j += 4) {
+      const CxQuery Q = pq[P.q_begin + c0 + j];
+      const float* rel = R + (size_t)Q.rel * DP;
+      float z = 0.f;
+      for (int d = lane; d < 2 * half; d += 64) z += cx_q(xs, rel, d, half) * xs[d];
+      z = wave_sum(z);
+      const int qi = qoff + c0 + j;
+      float mm = kNegInf;
+      for (int sp = 0; sp < n_split; ++sp) mm = fmaxf(mm, att_m[(size_t)sp * nq_step + qi]);
+      float ll = 0.f;
+      for (int sp = 0; sp < n_split; ++sp) {
+        float ms = att_m[(size_t)sp * nq_step + qi];
+        ll += (ms == kNegInf) ? 0.f : att_l[(size_t)sp * nq_step + qi] * __expf(ms - mm);
+      }
+      const float lse_f = mm + __logf(ll);
+      const float hi = fmaxf(lse_f, z), lo = fminf(lse_f, z);
+      const float lse = hi + log1pf(__expf(lo - hi));
+      if (lane == 0) {
+        const float pk = __expf(z - lse);
+        s_pk[j] = pk;
+        s_cf[j] = (float)Q.c * pk - (float)Q.ck;
+      }
+      if (lane < n_split) {
+        float ms = att_m[(size_t)lane * nq_step + qi];
+        s_w[j][lane] = (ms == kNegInf) ? 0.f : __expf(ms - lse);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int i = tid + 256 * u;
+      if (i < half) {
+        const float a = xs[i], b = xs[i + half];
+        float accr = gre[u], acci = gim[u];
+        for (int j = 0; j < cn; ++j) {
+          const CxQuery Q = pq[P.q_begin + c0 + j];
+          const int qi = qoff + c0 + j;
+          const float cc = R[(size_t)Q.rel * DP + i], ee = R[(size_t)Q.rel * DP + i + half];
+          float ore = 0.f, oim = 0.f;
+          for (int sp = 0; sp < n_split; ++sp) {
+            const float* Op = att_O + ((size_t)sp * nq_step + qi) * DP;
+            ore += s_w[j][sp] * Op[i];
+            oim += s_w[j][sp] * Op[i + half];
+          }
+          const float pk = s_pk[j];
+          const float ere = ore + pk * a, eim = oim + pk * b;
+          const float* ts = Tsum + (size_t)(P.q_begin + c0 + j) * DP;
+          const float fc = (float)Q.c, fck = (float)Q.ck;
+          const float dre = fc * ere - ts[i] - fck * a;
+          const float dim_ = fc * eim - ts[i + half] - fck * b;
+          const float qre = a * cc - b * ee, qim = a * ee + b * cc;
+          const float cf = s_cf[j];
+          accr += dre * cc + dim_ * ee + cf * qre;
+          acci += -dre * ee + dim_ * cc + cf * qim;
+        }
+        gre[u] = accr;
+        gim[u] = acci;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---------------- frozen-head rows (target = kelpie)
+  for (int c0 = 0; c0 < P.t_count; c0 += UPD_CHUNK) {
+    const int cn = min(UPD_CHUNK, P.t_count - c0);
+    for (int j = w; j < cn; j += 4) {
+      const CxTail T = pt[P.t_begin + c0 + j];
+      const float* qp = Qpair + (size_t)T.pair * DP;
+      float z = 0.f;
+      for (int d = lane; d < 2 * half; d += 64) z += qp[d] * xs[d];
+      z = wave_sum(z);
+      const float lf = lsef[T.pair];
+      const float hi = fmaxf(lf, z), lo = fminf(lf, z);
+      const float lse = hi + log1pf(__expf(lo - hi));
+      if (lane == 0) s_cf[j] = (float)T.c * (__expf(z - lse) - 1.0f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int i = tid + 256 * u;
+      if (i < half) {
+        float accr = gre[u], acci = gim[u];
+        for (int j = 0; j < cn; ++j) {
+          const CxTail T = pt[P.t_begin + c0 + j];
+          const float* qp = Qpair + (size_t)T.pair * DP;
+          accr += s_cf[j] * qp[i];
+          acci += s_cf[j] * qp[i + half];
+        }
+        gre[u] = accr;
+        gim[u] = acci;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---------------- regulariser, optimizer
+  const float inv_b = 1.0f / (float)P.b;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = tid + 256 * u;
+    if (i >= half) continue;
+    float gv[2] = {gre[u] * inv_b, gim[u] * inv_b};
+    const float a = xs[i], b = xs[i + half];
+    if (opt.reg_w != 0.f) {
+      const float mod = sqrtf(a * a + b * b);
+      const float k3 = 3.0f * opt.reg_w * inv_b * (float)(P.cnt_l + P.cnt_r) * mod;
+      gv[0] += k3 * a;
+      gv[1] += k3 * b;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int d = i + h * half;
+      const float gd = gv[h];
+      float xd = xs[d];
+      if (opt.kind == KP_OPT_ADAGRAD) {
+        float s1 = S1[(size_t)slot * DP + d];
+        s1 = s1 + gd * gd;
+        const float stdv = sqrtf(s1) + opt.eps;
+        xd = xd + (-opt.lr * gd) / stdv;
+        S1[(size_t)slot * DP + d] = s1;
+      } else if (opt.kind == KP_OPT_ADAM) {
+        float m1 = S1[(size_t)slot * DP + d], v2 = S2[(size_t)slot * DP + d];
+        m1 = m1 + opt.one_minus_b1 * (gd - m1);
+        v2 = v2 * opt.b2;
+        v2 = v2 + (opt.one_minus_b2 * gd) * gd;
+        const float den = sqrtf(v2) / opt.bc2_sqrt + opt.eps;
+        xd = xd + (-opt.step_size * m1) / den;
+        S1[(size_t)slot * DP + d] = m1;
+        S2[(size_t)slot * DP + d] = v2;
+      } else {
+        xd = xd + (-opt.lr) * gd;
+      }
+      x[d] = xd;
+    }
+  }
+}
+
+// ranking queries: q_s = x_s o R[p_s]; kelpie column score q_s . x_s
+template <int DP>
+__global__ void kp_cx_rankq(const float* __restrict__ X, const float* __restrict__ R, int half,
+                            const int32_t* __restrict__ pred, int n_slots, float* __restrict__ Q,
+                            float* __restrict__ scores, int ld, int kcol) {
+  const int s = blockIdx.x;
+  if (s >= n_slots) return;
+  const float* x = X + (size_t)s * DP;
+  const float* rel = R + (size_t)pred[3 * s + 1] * DP;
+  float z = 0.f;
+  for (int d = threadIdx.x; d < DP; d += 64) {
+    float q = cx_q(x, rel, d, half);
+    Q[(size_t)s * DP + d] = q;
+    z += q * x[d];
+  }
+  z = wave_sum(z);
+  if (threadIdx.x == 0) scores[(size_t)s * ld + kcol] = z;
+}
+
+__global__ void kp_cx_scoreq(const float* __restrict__ E, const float* __restrict__ R, int dp, int half,
+                             const int32_t* __restrict__ heads, const int32_t* __restrict__ rels, int n,
+                             float* __restrict__ Q) {
+  int s = blockIdx.x;
+  if (s >= n) return;
+  const float* lhs = E + (size_t)heads[s] * dp;
+  const float* rel = R + (size_t)rels[s] * dp;
+  for (int d = threadIdx.x; d < dp; d += blockDim.x) Q[(size_t)s * dp + d] = cx_q(lhs, rel, d, half);
+}
+
+// ----------------------------------------------------------------------------
+// host side
+// ----------------------------------------------------------------------------
+template <int DB>
+void launch_attn(kp_ctx* c, bool with_o, const int2* qdesc, const float* X, const float* Qpre, int nq,
+                 int n_split, float* m, float* l, float* O) {
+  if (nq <= 0) return;
+  const int keys_per_split = (c->n_ent + n_split - 1) / n_split;
+  dim3 grid((nq + 63) / 64, n_split);
+  const size_t shm = 2 * 16 * (16 * DB + 4) * sizeof(float);
+  const int half = c->dim / 2;
+  if (with_o)
+    hipLaunchKernelGGL((kp_cx_attn<DB, true>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, half, qdesc, X,
+                       c->dR, Qpre, nq, keys_per_split, m, l, O);
+  else
+    hipLaunchKernelGGL((kp_cx_attn<DB, false>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, half, qdesc, X,
+                       c->dR, Qpre, nq, keys_per_split, m, l, O);
+  KP_HIP(hipGetLastError());
+}
+
+template <int DB>
+void launch_update(kp_ctx* c, int n_act, const int4* act, const CxPlan* plans, const CxQuery* pq,
+                   const CxTail* pt, const float* tsum, const float* qpair, const float* lsef, const float* am,
+                   const float* al, const float* aO, int nq_step, int n_split, float* X, float* S1, float* S2,
+                   const CxOpt& opt) {
+  if (n_act <= 0) return;
+  hipLaunchKernelGGL((kp_cx_update<16 * DB>), dim3(n_act), dim3(256), 0, c->stream, c->dim / 2, act, plans, pq, pt,
+                     c->dR, tsum, qpair, lsef, am, al, aO, nq_step, n_split, X, S1, S2, opt);
+  KP_HIP(hipGetLastError());
+}
+
+template <int DB>
+void launch_rankq(kp_ctx* c, const float* X, const int32_t* pred, int n, float* Q, float* scores, int ld) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL((kp_cx_rankq<16 * DB>), dim3(n), dim3(64), 0, c->stream, X, c->dR, c->dim / 2, pred, n, Q,
+                     scores, ld, c->n_ent);
+  KP_HIP(hipGetLastError());
+}
+
+#define CX_DISPATCH(DBV, ...)   \
+  switch (DBV) {                 \
+    case 1: { constexpr int DB = 1; __VA_ARGS__; } break;   \
+    case 2: { constexpr int DB = 2; __VA_ARGS__; } break;   \
+    case 4: { constexpr int DB = 4; __VA_ARGS__; } break;   \
+    case 8: { constexpr int DB = 8; __VA_ARGS__; } break;   \
+    case 13: { constexpr int DB = 13; __VA_ARGS__; } break; \
+    case 16: { constexpr int DB = 16; __VA_ARGS__; } break; \
+    case 25: { constexpr int DB = 25; __VA_ARGS__; } break; \
+    default: throw KpError{KP_ENOTSUP, "ComplEx: unsupported padded dimension"}; \
+  }
+
+static int choose_split(int nq, int n_ent) {
+  // enough workgroups to fill 256 CUs (1 workgroup/CU), limited by keys per split
+  const int tiles = (nq + 63) / 64;
+  int best = 1;
+  double best_eff = 0;
+  for (int s = 1; s <= UPD_MAXSPLIT; ++s) {
+    if (n_ent / s < 256 && s > 1) break;
+    const int wgs = tiles * s;
+    const int rounds = (wgs + 255) / 256;
+    // time ~ rounds * (keys per split) + combine overhead per split
+    const double t = rounds * ((double)n_ent / s) + 0.02 * n_ent * (s - 1) * tiles / 256.0;
+    const double eff = 1.0 / t;
+    if (eff > best_eff) {
+      best_eff = eff;
+      best = s;
+    }
+  }
+  return best;
+}
+
+}  // namespace
+
+int cx_pick_db(int dim) {
+  static const int dbs[] = {1, 2, 4, 8, 13, 16, 25};
+  for (int db : dbs)
+    if (16 * db >= dim) return db;
+  return -1;
+}
+
+void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
+  const int DBV = c->dp / 16;
+  const int K = c->n_ent;  // kelpie id
+  const int ns = bt->n_slots;
+  const int hpbs = hp->batch_size;
+  KP_REQUIRE(hpbs > 0 && hp->epochs >= 0, "ComplEx: bad batch_size/epochs");
+  const int E = hp->epochs;
+
+  std::vector<CxPlan> plans;
+  std::vector<CxQuery> pqs;
+  std::vector<CxTail> pts;
+  std::vector<int32_t> targets;
+  std::vector<int2> pairs;
+  std::unordered_map<int64_t, int> pair_id;
+  std::vector<int> plan_base(ns, 0), nsteps(ns, 0);
+
+  std::vector<int> rel_slot(c->n_rel2, -1);
+  std::vector<int> rel_cnt, rel_ck, rel_first;
+  std::unordered_map<int, int> tail_slot;
+  auto make_plan = [&](const int32_t* rows, const int32_t* idx, int n) {
+    CxPlan P{};
+    P.b = n;
+    P.q_begin = (int)pqs.size();
+    P.t_begin = (int)pts.size();
+    std::vector<int> rels;
+    tail_slot.clear();
+    // pass 1: group
+    std::vector<int> qtg_count;
+    for (int k = 0; k < n; ++k) {
+      const int32_t* rw = rows + 3 * (size_t)(idx ? idx[k] : k);
+      const int h = rw[0], r = rw[1], t = rw[2];
+      if (h == K) {
+        if (rel_slot[r] < 0) {
+          rel_slot[r] = (int)rels.size();
+          rels.push_back(r);
+          qtg_count.push_back(0);
+          pqs.push_back(CxQuery{r, 0, 0, 0, 0, 0, 0, 0});
+        }
+        CxQuery& Q = pqs[P.q_begin + rel_slot[r]];
+        Q.c += 1;
+        P.cnt_l += 1;
+        if (t == K) {
+          Q.ck += 1;
+          P.cnt_r += 1;
+        } else {
+          qtg_count[rel_slot[r]] += 1;
+        }
+      } else {
+        KP_REQUIRE(t == K, "ComplEx: a training row does not involve the kelpie entity");
+        P.cnt_r += 1;
+        const int64_t key = (int64_t)h * c->n_rel2 + r;
+        auto it = pair_id.find(key);
+        int pid;
+        if (it == pair_id.end()) {
+          pid = (int)pairs.size();
+          pair_id.emplace(key, pid);
+          pairs.push_back(make_int2(h, r));
+        } else {
+          pid = it->second;
+        }
+        auto jt = tail_slot.find(pid);
+        if (jt == tail_slot.end()) {
+          tail_slot.emplace(pid, (int)pts.size());
+          pts.push_back(CxTail{pid, 1});
+        } else {
+          pts[jt->second].c += 1;
+        }
+      }
+    }
+    // pass 2: frozen targets grouped per query
+    int base = (int)targets.size();
+    for (size_t j = 0; j < rels.size(); ++j) {
+      pqs[P.q_begin + j].tg_begin = base;
+      pqs[P.q_begin + j].tg_count = 0;
+      base += qtg_count[j];
+    }
+    targets.resize(base);
+    for (int k = 0; k < n; ++k) {
+      const int32_t* rw = rows + 3 * (size_t)(idx ? idx[k] : k);
+      if (rw[0] == K && rw[2] != K) {
+        CxQuery& Q = pqs[P.q_begin + rel_slot[rw[1]]];
+        targets[Q.tg_begin + Q.tg_count++] = rw[2];
+      }
+    }
+    for (int r : rels) rel_slot[r] = -1;
+    P.q_count = (int)rels.size();
+    P.t_count = (int)pts.size() - P.t_begin;
+    plans.push_back(P);
+  };
+
+  int T = 0;
+  for (int s = 0; s < ns; ++s) {
+    const int r0 = bt->row_off[s], r1 = bt->row_off[s + 1];
+    const int R = r1 - r0;
+    KP_REQUIRE(R >= 0, "ComplEx: bad row_off");
+    const int32_t* rows = bt->rows + 3 * (size_t)r0;
+    plan_base[s] = (int)plans.size();
+    if (R == 0 || E == 0) {
+      nsteps[s] = 0;
+      continue;
+    }
+    const int nst = (R + hpbs - 1) / hpbs;
+    const int bs = std::min(hpbs, R);
+    nsteps[s] = nst;
+    if (nst == 1) {
+      make_plan(rows, nullptr, R);
+    } else {
+      const int64_t g0 = bt->rng_off[s], g1 = bt->rng_off[s + 1];
+      KP_REQUIRE(g1 - g0 >= (int64_t)E * R, "ComplEx: missing randperm draws for a multi-step slot");
+      for (int e = 0; e < E; ++e) {
+        const int32_t* perm = bt->rng + g0 + (int64_t)e * R;
+        for (int j = 0; j < nst; ++j) {
+          const int st = j * hpbs;
+          const int n = std::min(bs, R - st);
+          make_plan(rows, perm + st, n);
+        }
+      }
+    }
+    T = std::max(T, E * nst);
+  }
+
+  // per-step active lists
+  std::vector<int> act_off(T + 1, 0), q_off(T + 1, 0);
+  std::vector<int4> acts;
+  std::vector<int2> stepq;
+  int max_nq = 0;
+  for (int t = 0; t < T; ++t) {
+    act_off[t] = (int)acts.size();
+    q_off[t] = (int)stepq.size();
+    int qo = 0;
+    for (int s = 0; s < ns; ++s) {
+      const int nst = nsteps[s];
+      if (nst == 0 || t >= E * nst) continue;
+      const int plan = plan_base[s] + (nst == 1 ? 0 : t);
+      acts.push_back(make_int4(s, plan, qo, 0));
+      const CxPlan& P = plans[plan];
+      for (int j = 0; j < P.q_count; ++j) stepq.push_back(make_int2(s, pqs[P.q_begin + j].rel));
+      qo += P.q_count;
+    }
+    max_nq = std::max(max_nq, qo);
+  }
+  act_off[T] = (int)acts.size();
+  q_off[T] = (int)stepq.size();
+
+  const int DP = c->dp;
+  // ---- uploads
+  float* dX = nullptr;
+  {
+    std::vector<float> xp((size_t)ns * DP, 0.f);
+    for (int s = 0; s < ns; ++s)
+      std::memcpy(&xp[(size_t)s * DP], bt->x0 + (size_t)s * c->dim, sizeof(float) * c->dim);
+    dX = upload(c, c->ws[0], xp.data(), xp.size());
+  }
+  float* dS1 = reinterpret_cast<float*>(c->ws[1].ensure(sizeof(float) * (size_t)ns * DP));
+  float* dS2 = reinterpret_cast<float*>(c->ws[2].ensure(sizeof(float) * (size_t)ns * DP));
+  KP_HIP(hipMemsetAsync(dS1, 0, sizeof(float) * (size_t)ns * DP, c->stream));
+  KP_HIP(hipMemsetAsync(dS2, 0, sizeof(float) * (size_t)ns * DP, c->stream));
+  CxPlan* dPlans = upload(c, c->ws[3], plans.data(), plans.size());
+  CxQuery* dPq = upload(c, c->ws[4], pqs.data(), pqs.size());
+  CxTail* dPt = upload(c, c->ws[5], pts.data(), pts.size());
+  int32_t* dTg = upload(c, c->ws[6], targets.data(), targets.size());
+  int2* dPairs = upload(c, c->ws[7], pairs.data(), pairs.size());
+  int4* dActs = upload(c, c->ws[8], acts.data(), acts.size());
+  int2* dStepQ = upload(c, c->ws[9], stepq.data(), stepq.size());
+  const int npq = (int)pqs.size(), npairs = (int)pairs.size();
+  float* dTsum = reinterpret_cast<float*>(c->ws[10].ensure(sizeof(float) * (size_t)std::max(npq, 1) * DP));
+  float* dQpair = reinterpret_cast<float*>(c->ws[11].ensure(sizeof(float) * (size_t)std::max(npairs, 1) * DP));
+  float* dLsef = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)std::max(npairs, 1)));
+
+  const int half = c->dim / 2;
+  KP_HIP(hipEventRecord(c->ev0, c->stream));
+  if (npq > 0) {
+    hipLaunchKernelGGL(kp_cx_tsum, dim3(npq), dim3(128), 0, c->stream, c->dE, DP, dPq, npq, dTg, dTsum);
+    KP_HIP(hipGetLastError());
+  }
+  // frozen-head pairs: q and frozen log-sum-exp
+  const int n_split_max = UPD_MAXSPLIT;
+  const int split_pairs = choose_split(npairs, c->n_ent);
+  const int split_step = choose_split(max_nq, c->n_ent);
+  size_t att_rows = (size_t)std::max(npairs, 1) * split_pairs;
+  for (int t = 0; t < T; ++t) {
+    const int nq = q_off[t + 1] - q_off[t];
+    att_rows = std::max(att_rows, (size_t)nq * choose_split(nq, c->n_ent));
+  }
+  (void)split_step;
+  float* dAm = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * att_rows));
+  float* dAl = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * att_rows));
+  float* dAO = reinterpret_cast<float*>(c->ws[15].ensure(sizeof(float) * att_rows * DP));
+  (void)n_split_max;
+  if (npairs > 0) {
+    hipLaunchKernelGGL(kp_cx_qpair, dim3(npairs), dim3(128), 0, c->stream, c->dE, c->dR, DP, half, dPairs, npairs,
+                       dQpair);
+    KP_HIP(hipGetLastError());
+    CX_DISPATCH(DBV, launch_attn<DB>(c, false, nullptr, nullptr, dQpair, npairs, split_pairs, dAm, dAl, nullptr));
+    // combine splits into lsef (host-free: small kernel via update-style math on host is avoided)
+    std::vector<float> hm((size_t)npairs * split_pairs), hl((size_t)npairs * split_pairs);
+    KP_HIP(hipMemcpyAsync(hm.data(), dAm, sizeof(float) * hm.size(), hipMemcpyDeviceToHost, c->stream));
+    KP_HIP(hipMemcpyAsync(hl.data(), dAl, sizeof(float) * hl.size(), hipMemcpyDeviceToHost, c->stream));
+    KP_HIP(hipStreamSynchronize(c->stream));
+    std::vector<float> lse(npairs);
+    for (int p = 0; p < npairs; ++p) {
+      float mm = -INFINITY;
+      for (int s = 0; s < split_pairs; ++s) mm = std::max(mm, hm[(size_t)s * npairs + p]);
+      double ll = 0;
+      for (int s = 0; s < split_pairs; ++s) {
+        float ms = hm[(size_t)s * npairs + p];
+        if (ms != -INFINITY) ll += (double)hl[(size_t)s * npairs + p] * std::exp((double)ms - mm);
+      }
+      lse[p] = (float)(mm + std::log(ll));
+    }
+    KP_HIP(hipMemcpyAsync(dLsef, lse.data(), sizeof(float) * npairs, hipMemcpyHostToDevice, c->stream));
+  }
+
+  // ---- the epoch/step loop
+  CxOpt opt{};
+  opt.kind = hp->optimizer;
+  opt.lr = hp->lr;
+  opt.b1 = hp->beta1;
+  opt.b2 = hp->beta2;
+  opt.eps = hp->eps;
+  opt.one_minus_b1 = (float)(1.0 - (double)hp->beta1);
+  opt.one_minus_b2 = (float)(1.0 - (double)hp->beta2);
+  opt.reg_w = hp->reg_weight;
+  hipEvent_t h0, h1;
+  KP_HIP(hipEventCreate(&h0));
+  KP_HIP(hipEventCreate(&h1));
+  KP_HIP(hipEventRecord(h0, c->stream));
+  int64_t hot_launches = 0;
+  c->hot_pairs.clear();
+  for (int t = 0; t < T; ++t) {
+    const int nq = q_off[t + 1] - q_off[t];
+    const int na = act_off[t + 1] - act_off[t];
+    const int sp = choose_split(nq, c->n_ent);
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (nq > 0 && c->time_hot) {
+      ea = c->event(2 * hot_launches);
+      eb = c->event(2 * hot_launches + 1);
+      KP_HIP(hipEventRecord(ea, c->stream));
+    }
+    CX_DISPATCH(DBV, launch_attn<DB>(c, true, dStepQ + q_off[t], dX, nullptr, nq, sp, dAm, dAl, dAO));
+    if (nq > 0) {
+      if (c->time_hot) {
+        KP_HIP(hipEventRecord(eb, c->stream));
+        c->hot_pairs.push_back({(double)nq, 0.0});
+      }
+      ++hot_launches;
+    }
+    const double step = (double)(t + 1);
+    opt.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, step)));
+    opt.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)hp->beta2, step));
+    CX_DISPATCH(DBV, launch_update<DB>(c, na, dActs + act_off[t], dPlans, dPq, dPt, dTsum, dQpair, dLsef, dAm, dAl,
+                                       dAO, nq, sp, dX, dS1, dS2, opt));
+  }
+  KP_HIP(hipEventRecord(h1, c->stream));
+
+  // ---- ranking: scores of (kelpie, p, .) over E plus the kelpie column
+  const int ld = round_up(c->n_ent + 1, 4);
+  float* dScores = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)ns * ld));
+  float* dQr = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * (size_t)ns * DP));
+  int32_t* dPred = upload(c, c->ws[18], bt->pred, (size_t)ns * 3);
+  std::vector<int32_t> po(ns);
+  for (int s = 0; s < ns; ++s) po[s] = bt->pred[3 * s + 2];
+  int32_t* dPo = upload(c, c->ws[19], po.data(), po.size());
+  int32_t* dFo = upload(c, c->ws[20], bt->filt_off, (size_t)ns + 1);
+  int32_t* dF = upload(c, c->ws[21], bt->filt, (size_t)bt->filt_off[ns]);
+  float* dTarget = reinterpret_cast<float*>(c->ws[22].ensure(sizeof(float) * (size_t)ns));
+  int64_t* dRank = reinterpret_cast<int64_t*>(c->ws[23].ensure(sizeof(int64_t) * (size_t)ns));
+  CX_DISPATCH(DBV, launch_rankq<DB>(c, dX, dPred, ns, dQr, dScores, ld));
+  launch_score_gemm(c, dQr, ns, dScores, ld, 0);
+  launch_rank_count(c, ns, dScores, ld, c->n_ent + 1, dPo, dFo, dF, 0, dTarget, dRank);
+  KP_HIP(hipEventRecord(c->ev1, c->stream));
+
+  if (bt->out_x) {
+    std::vector<float> xp((size_t)ns * DP);
+    KP_HIP(hipMemcpyAsync(xp.data(), dX, sizeof(float) * xp.size(), hipMemcpyDeviceToHost, c->stream));
+    KP_HIP(hipStreamSynchronize(c->stream));
+    for (int s = 0; s < ns; ++s)
+      std::memcpy(bt->out_x + (size_t)s * c->dim, &xp[(size_t)s * DP], sizeof(float) * c->dim);
+  }
+  KP_HIP(hipMemcpyAsync(bt->out_score, dTarget, sizeof(float) * ns, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipMemcpyAsync(bt->out_rank, dRank, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  float ms_all = 0.f, ms_loop = 0.f;
+  KP_HIP(hipEventElapsedTime(&ms_all, c->ev0, c->ev1));
+  KP_HIP(hipEventElapsedTime(&ms_loop, h0, h1));
+  (void)hipEventDestroy(h0);
+  (void)hipEventDestroy(h1);
+  double hot = 0.0;
+  for (size_t i = 0; i < c->hot_pairs.size(); ++i) {
+    float ms = 0.f;
+    KP_HIP(hipEventElapsedTime(&ms, c->event(2 * i), c->event(2 * i + 1)));
+    c->hot_pairs[i].second = ms * 1e-3;
+    hot += ms * 1e-3;
+  }
+  c->timing.device_s = ms_all * 1e-3;
+  c->timing.loop_s = ms_loop * 1e-3;
+  c->timing.hot_s = hot;
+  c->timing.hot_launches = hot_launches;
+  double work = 0.0;
+  for (auto& pr : c->hot_pairs) work += pr.first * (double)c->n_ent;
+  c->timing.hot_work = work;
+}
+
+void complex_scores_dev(kp_ctx* c, int n, const int32_t* dh, const int32_t* dr, float* dS, int ld) {
+  if (n <= 0) return;
+  const int DP = c->dp;
+  float* dQ = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * (size_t)n * DP));
+  hipLaunchKernelGGL(kp_cx_scoreq, dim3(n), dim3(128), 0, c->stream, c->dE, c->dR, DP, c->dim / 2, dh, dr, n, dQ);
+  KP_HIP(hipGetLastError());
+  launch_score_gemm(c, dQ, n, dS, ld, 0);
+}
+
+void complex_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rels, float* out) {
+  if (n <= 0) return;
+  int32_t* dh = upload(c, c->ws[18], heads, (size_t)n);
+  int32_t* dr = upload(c, c->ws[19], rels, (size_t)n);
+  float* dS = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)n * c->n_ent));
+  complex_scores_dev(c, n, dh, dr, dS, c->n_ent);
+  KP_HIP(hipMemcpyAsync(out, dS, sizeof(float) * (size_t)n * c->n_ent, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+}

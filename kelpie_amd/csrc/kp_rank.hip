@@ -1,0 +1,199 @@
+// kp_rank.hip -- all-entity scoring (fp32 MFMA) and the filtered rank of
+// PostTrainingEngine.get_triple_results (post_training_engine.py:101-125).
+#include "kp_common.hpp"
+
+// ----------------------------------------------------------------------------
+// score GEMM:  out[q][e] = act( Q[q] . E[e] )  for e < n_ent
+//   Q [nq][dp], E [n_ent][dp] (dp multiple of 16, zero padded), out row stride ld.
+//   fp32 MFMA v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain).  Block tile
+//   64 queries x 64 entities x BK 32, 4 waves; wave w owns queries [16w,16w+16)
+//   x 64 entities (4 accumulators).  C layout: row (query) = 4*(l>>4)+r,
+//   col (entity) = l&15 -> lanes store consecutive entities (coalesced).
+//   act: 0 identity (ComplEx), 1 sigmoid (ConvE, conve.py:156).
+// ----------------------------------------------------------------------------
+#define SG_BM 64
+#define SG_BN 64
+#define SG_BK 32
+#define SG_LD (SG_BK + 4)
+
+__global__ __launch_bounds__(256) void kp_score_gemm(const float* __restrict__ Q, int nq,
+                                                     const float* __restrict__ E, int n_ent, int dp,
+                                                     float* __restrict__ out, int ld, int act) {
+  __shared__ __attribute__((aligned(16))) float Qs[SG_BM * SG_LD];
+  __shared__ __attribute__((aligned(16))) float Es[SG_BN * SG_LD];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int q0 = blockIdx.y * SG_BM;
+  const int e0 = blockIdx.x * SG_BN;
+  f32x4 acc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < dp; k0 += SG_BK) {
+    // stage: 64 rows x 32 floats for Q and E (8 float4 per row) -> 512 float4 each, 2 per thread
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      int f = tid + 256 * u;
+      int row = f >> 3, c4 = (f & 7) * 4;
+      float4 vq = make_float4(0.f, 0.f, 0.f, 0.f), ve = vq;
+      int kk = k0 + c4;
+      if (q0 + row < nq && kk < dp) vq = *reinterpret_cast<const float4*>(Q + (size_t)(q0 + row) * dp + kk);
+      if (e0 + row < n_ent && kk < dp) ve = *reinterpret_cast<const float4*>(E + (size_t)(e0 + row) * dp + kk);
+      *reinterpret_cast<float4*>(&Qs[row * SG_LD + c4]) = vq;
+      *reinterpret_cast<float4*>(&Es[row * SG_LD + c4]) = ve;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < SG_BK; kk += 4) {
+      float a = Qs[(16 * w + c) * SG_LD + kk + g];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        float b = Es[(16 * n + c) * SG_LD + kk + g];
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[n], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    int e = e0 + 16 * n + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int q = q0 + 16 * w + 4 * g + r;
+      if (q < nq && e < n_ent) {
+        float v = acc[n][r];
+        if (act == 1) v = 1.0f / (1.0f + __expf(-v));
+        out[(size_t)q * ld + e] = v;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// filtered rank, one workgroup per slot.
+//   scores[s][0..n_cols) (column n_cols-1 is the kelpie entity when present)
+//   minimizer: v_e = 1e6 for e in F, v_o = target, rank = #{v_e <= target}
+//   maximizer: v_e = -1e6 for e in F,             rank = #{v_e >= target}
+//   (post_training_engine.py:110-119; an o in F is excluded for maximizers)
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void kp_rank_count(int n_slots, const float* __restrict__ scores, int ld,
+                                                     int n_cols, const int32_t* __restrict__ pred_o,
+                                                     const int32_t* __restrict__ filt_off,
+                                                     const int32_t* __restrict__ filt, int minimizer,
+                                                     float* __restrict__ target_out,
+                                                     int64_t* __restrict__ rank_out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
+  __shared__ int partial[4];
+  const int s = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nwords = (n_cols + 31) >> 5;
+  for (int i = tid; i < nwords; i += blockDim.x) bits[i] = 0u;
+  __syncthreads();
+  const int f0 = filt_off[s], f1 = filt_off[s + 1];
+  for (int i = f0 + tid; i < f1; i += blockDim.x) {
+    int e = filt[i];
+    if (e >= 0 && e < n_cols) atomicOr(&bits[e >> 5], 1u << (e & 31));
+  }
+  __syncthreads();
+  const float* row = scores + (size_t)s * ld;
+  const int o = pred_o[s];
+  const float target = row[o];
+  int cnt = 0;
+  if (minimizer) {
+    for (int e = tid; e < n_cols; e += blockDim.x) {
+      float v = row[e];
+      if ((bits[e >> 5] >> (e & 31)) & 1u) v = 1e6f;
+      if (e == o) v = target;
+      cnt += (v <= target) ? 1 : 0;
+    }
+  } else {
+    for (int e = tid; e < n_cols; e += blockDim.x) {
+      float v = row[e];
+      if ((bits[e >> 5] >> (e & 31)) & 1u) v = -1e6f;
+      cnt += (v >= target) ? 1 : 0;
+    }
+  }
+  // block reduce
+  for (int o2 = 32; o2 > 0; o2 >>= 1) cnt += __shfl_xor(cnt, o2, 64);
+  if ((tid & 63) == 0) partial[tid >> 6] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += partial[w];
+    rank_out[s] = tot;
+    target_out[s] = target;
+  }
+}
+
+void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
+                       const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
+                       int minimizer, float* d_target, int64_t* d_rank) {
+  if (n_slots <= 0) return;
+  size_t shm = (size_t)((n_cols + 31) / 32) * 4;
+  KP_REQUIRE(shm <= 150 * 1024, "rank: too many entities for the LDS filter bitmap");
+  hipLaunchKernelGGL(kp_rank_count, dim3(n_slots), dim3(256), shm, c->stream, n_slots, d_scores, ld, n_cols,
+                     d_pred_o, d_filt_off, d_filt, minimizer, d_target, d_rank);
+  KP_HIP(hipGetLastError());
+}
+
+void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld, int act) {
+  if (nq <= 0) return;
+  dim3 grid((c->n_ent + SG_BN - 1) / SG_BN, (nq + SG_BM - 1) / SG_BM);
+  hipLaunchKernelGGL(kp_score_gemm, grid, dim3(256), 0, c->stream, dQ, nq, c->dE, c->n_ent, c->dp, d_out, ld, act);
+  KP_HIP(hipGetLastError());
+}
+
+// ----------------------------------------------------------------------------
+// conversion-entity test of RelevanceEngine.select_entities_to_convert
+// (engine.py:103-120), one workgroup per candidate head: keep iff the target's
+// raw score lies strictly inside (-1e6, max of the filter-masked row) for
+// maximizers, or inside (min, 1e6) for minimizers.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void kp_convertible_reduce(int n, const float* __restrict__ scores, int ld,
+                                                             int n_ent, int obj,
+                                                             const int32_t* __restrict__ filt_off,
+                                                             const int32_t* __restrict__ filt, int minimizer,
+                                                             uint8_t* __restrict__ keep) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
+  __shared__ float part[4];
+  const int i = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nwords = (n_ent + 31) >> 5;
+  for (int k = tid; k < nwords; k += blockDim.x) bits[k] = 0u;
+  __syncthreads();
+  for (int k = filt_off[i] + tid; k < filt_off[i + 1]; k += blockDim.x) {
+    int e = filt[k];
+    if (e >= 0 && e < n_ent) atomicOr(&bits[e >> 5], 1u << (e & 31));
+  }
+  __syncthreads();
+  const float* row = scores + (size_t)i * ld;
+  const float t = row[obj];
+  float ext = minimizer ? 3.0e38f : -3.0e38f;
+  for (int e = tid; e < n_ent; e += blockDim.x) {
+    float v = row[e];
+    if ((bits[e >> 5] >> (e & 31)) & 1u) v = minimizer ? 1e6f : -1e6f;
+    ext = minimizer ? fminf(ext, v) : fmaxf(ext, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    float other = __shfl_xor(ext, o, 64);
+    ext = minimizer ? fminf(ext, other) : fmaxf(ext, other);
+  }
+  if ((tid & 63) == 0) part[tid >> 6] = ext;
+  __syncthreads();
+  if (tid == 0) {
+    float e2 = part[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) e2 = minimizer ? fminf(e2, part[w]) : fmaxf(e2, part[w]);
+    keep[i] = minimizer ? ((1e6f > t && t > e2) ? 1 : 0) : ((-1e6f < t && t < e2) ? 1 : 0);
+  }
+}
+
+void launch_convertible_reduce(kp_ctx* c, int n, const float* d_scores, int ld, int obj, const int32_t* d_fo,
+                               const int32_t* d_f, int minimizer, uint8_t* d_keep) {
+  if (n <= 0) return;
+  size_t shm = (size_t)((c->n_ent + 31) / 32) * 4;
+  KP_REQUIRE(shm <= 150 * 1024, "convertible: too many entities for the LDS filter bitmap");
+  hipLaunchKernelGGL(kp_convertible_reduce, dim3(n), dim3(256), shm, c->stream, n, d_scores, ld, c->n_ent, obj, d_fo,
+                     d_f, minimizer, d_keep);
+  KP_HIP(hipGetLastError());
+}

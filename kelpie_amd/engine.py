@@ -1,0 +1,255 @@
+"""MI355X-native post-training relevance engines.
+
+Drop-in for the reference's ``src/relevance_engines/post_training_engine.py``:
+same class names, constructor ``(model, dataset, hp)``, ``set_cache()``,
+``compute_relevance(pred, triples) -> float``, ``select_entities_to_convert``
+and the same errors.  Underneath, every ``compute_relevance`` call becomes one
+or more *slots* of a batched HIP launch (``kp_posttrain_rank``), and
+``compute_relevance_batch(pred, rules)`` evaluates many candidates in one
+launch while consuming the reference's random draws in the reference's order
+(``kelpie_amd.rng``), so a batch returns exactly what the sequential calls
+would.
+"""
+from __future__ import annotations
+
+import math
+import random
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .data import MANY_TO_ONE, ONE_TO_ONE, Dataset, KelpieView
+from .models import FrozenModel
+from .rng import ReferenceRNG, StateCheckpoint
+
+
+def _sigmoid(x):
+    # post_training_engine.py:19-20 (math.exp overflows below -709 like the reference)
+    return 1 / (1 + math.exp(-x))
+
+
+@dataclass
+class _Slot:
+    x0: np.ndarray
+    rows: np.ndarray
+    rng: np.ndarray
+    pred: tuple
+    filt: list
+    result: dict = field(default=None)
+
+
+class RelevanceEngine:
+    """engine.py:13-20 + select_entities_to_convert (engine.py:22-126)."""
+
+    def __init__(self, model: FrozenModel, dataset: Dataset):
+        self.model = model
+        self.dataset = dataset
+        self._o_to_training = None
+
+    @property
+    def o_to_training_triples(self):
+        if self._o_to_training is None:
+            d = {}
+            for h, r, t in self.dataset.training_triples.tolist():
+                d.setdefault(t, []).append((h, r, t))
+            self._o_to_training = d
+        return self._o_to_training
+
+    def select_entities_to_convert(self, pred, k: int, degree_cap=None, criage=False):
+        ds = self.dataset
+        s, p, o = (int(v) for v in pred)
+        ents = []
+        for e in range(ds.num_entities):
+            if e == s:
+                continue
+            deg = ds.entity_to_degree.get(e, 0)
+            if deg < 1:
+                continue
+            if degree_cap and deg > degree_cap:
+                continue
+            if criage and e not in self.o_to_training_triples:
+                continue
+            if (e, p) in ds.to_filter:
+                if ds.relation_to_type[p] in (ONE_TO_ONE, MANY_TO_ONE):
+                    continue
+                if o in ds.to_filter[(e, p)]:
+                    continue
+            ents.append(e)
+        if not ents:
+            self.entities_to_convert = []
+            return []
+        fo, fl = [0], []
+        for e in ents:
+            F = ds.to_filter.get((e, p), [])
+            fl.extend(F)
+            fo.append(len(fl))
+        keep = self.model.ctx.convertible(np.array(ents), p, o, np.array(fo), np.array(fl, dtype=np.int64))
+        overall = [e for e, kflag in zip(ents, keep) if kflag]
+        chosen = random.sample(overall, k=min(k, len(overall)))  # engine.py:125 (python RNG)
+        self.entities_to_convert = chosen
+        return chosen
+
+
+class PostTrainingEngine(RelevanceEngine):
+    """post_training_engine.py:17-125."""
+
+    def __init__(self, model: FrozenModel, dataset: Dataset, hp: dict, rng: ReferenceRNG | None = None):
+        RelevanceEngine.__init__(self, model=model, dataset=dataset)
+        self.hp = hp
+        self.rng = rng or ReferenceRNG()
+        self._kp_hp = model.kp_hp(hp)
+        if getattr(model, "is_kelpie", False):
+            raise Exception("Already a post-trainable KelpieModel.")
+        self.set_cache()
+        self.last_batch_stats = {}
+
+    def set_cache(self):
+        self.base_pt_results = {}
+        self.kelpie_dataset_cache_size = 20
+        self.kelpie_dataset_cache = OrderedDict()
+
+    def _get_kelpie_dataset(self, original_entity: int) -> KelpieView:
+        e = int(original_entity)
+        if e not in self.kelpie_dataset_cache:
+            self.kelpie_dataset_cache[e] = KelpieView(self.dataset, e)
+            self.kelpie_dataset_cache.move_to_end(e)
+            if len(self.kelpie_dataset_cache) > self.kelpie_dataset_cache_size:
+                self.kelpie_dataset_cache.popitem(last=False)
+        return self.kelpie_dataset_cache[e]
+
+    # ------------------------------------------------------------------ slot assembly
+    def _slot(self, x0, rows, kelpie_pred, filt):
+        draws = self.model.posttrain_draws(rows, self.hp, self.rng)
+        return _Slot(x0=x0, rows=rows, rng=draws, pred=tuple(int(v) for v in kelpie_pred), filt=list(filt))
+
+    def _schedule(self, pred, triples, mode, slots, pending_base):
+        """Consume the draws of one reference compute_relevance call (post_training_engine.py:46-62)
+        and append its slots.  Returns (pt_slot, base_key)."""
+        pred = tuple(int(v) for v in pred)
+        view = self._get_kelpie_dataset(pred[0])
+        init = self.rng.rand_init(self.model.dimension)
+        x_base = self.model.kelpie_init(init, self.rng)  # base KelpieModel is built every call (A-Q6)
+        kp = view.as_kelpie_triple(pred)
+        if pred not in self.base_pt_results and pred not in pending_base:
+            pending_base[pred] = len(slots)
+            slots.append(self._slot(x_base, view.base_rows, kp, view.filter_for(kp[1])))
+        x_pt = self.model.kelpie_init(init, self.rng)
+        rows, delta = view.removed(triples) if mode == "necessary" else view.added(triples)
+        filt = view.filter_for(kp[1], delta.get(kp[1]))
+        slots.append(self._slot(x_pt, rows, kp, filt))
+        return len(slots) - 1, pred
+
+    def _run(self, slots):
+        if not slots:
+            return
+        n = len(slots)
+        D = self.model.dimension
+        x0 = np.stack([s.x0 for s in slots]).astype(np.float32)
+        row_off = np.zeros(n + 1, np.int32)
+        row_off[1:] = np.cumsum([len(s.rows) for s in slots])
+        rows = np.concatenate([s.rows.reshape(-1, 3) for s in slots]).astype(np.int32) if row_off[-1] \
+            else np.zeros((0, 3), np.int32)
+        rng_off = np.zeros(n + 1, np.int64)
+        rng_off[1:] = np.cumsum([s.rng.size for s in slots])
+        rng = np.concatenate([s.rng.reshape(-1) for s in slots]).astype(np.int32) if rng_off[-1] \
+            else np.zeros(1, np.int32)
+        pred = np.array([s.pred for s in slots], np.int32)
+        filt_off = np.zeros(n + 1, np.int32)
+        filt_off[1:] = np.cumsum([len(s.filt) for s in slots])
+        filt = np.array([e for s in slots for e in s.filt], np.int32) if filt_off[-1] else np.zeros(1, np.int32)
+        assert x0.shape == (n, D)
+        score, rank, _ = self.model.ctx.posttrain_rank(self._kp_hp, x0, row_off, rows, rng_off, rng, pred,
+                                                       filt_off, filt)
+        for i, s in enumerate(slots):
+            s.result = {"target_score": float(score[i]), "target_rank": int(rank[i])}
+        self.last_batch_stats = {"slots": n, "rows": int(row_off[-1]), **self.model.ctx.last_timing()}
+
+    def _base_result(self, key, slots, pending_base):
+        if key in self.base_pt_results:
+            return self.base_pt_results[key]
+        res = slots[pending_base[key]].result
+        self.base_pt_results[key] = res
+        return res
+
+    # ------------------------------------------------------------------ reference API
+    def compute_relevance(self, pred, triples: list):
+        return self.compute_relevance_batch(pred, [triples])[0]
+
+    def compute_relevance_batch(self, pred, rules, checkpoints: list | None = None):
+        raise NotImplementedError
+
+
+class NecessaryPostTrainingEngine(PostTrainingEngine):
+    """post_training_engine.py:128-157."""
+
+    def compute_relevance_batch(self, pred, rules, checkpoints: list | None = None):
+        """Relevances of ``rules`` for ``pred``, identical to calling
+        ``compute_relevance`` on each rule in order.  When ``checkpoints`` is a
+        list, the generator state after each rule's draws is appended to it."""
+        slots, pending, jobs = [], {}, []
+        for rule in rules:
+            pt_idx, key = self._schedule(pred, [tuple(t) for t in rule], "necessary", slots, pending)
+            jobs.append((pt_idx, key))
+            if checkpoints is not None:
+                checkpoints.append(StateCheckpoint())
+        self._run(slots)
+        out = []
+        minimizer = self.model.is_minimizer()
+        for pt_idx, key in jobs:
+            base = self._base_result(key, slots, pending)
+            pt = slots[pt_idx].result
+            rank_worsening = pt["target_rank"] - base["target_rank"]
+            if minimizer:
+                score_worsening = pt["target_score"] - base["target_score"]
+            else:
+                score_worsening = base["target_score"] - pt["target_score"]
+            # int64 tensor + python float -> float32 tensor (A-Q5)
+            out.append(float(np.float32(np.float32(rank_worsening) + np.float32(_sigmoid(score_worsening)))))
+        self.last_results = [(slots[i].result, self.base_pt_results[k]) for i, k in jobs]
+        return out
+
+
+class SufficientPostTrainingEngine(PostTrainingEngine):
+    """post_training_engine.py:160-207."""
+
+    def __init__(self, model, dataset, hp, rng=None):
+        super().__init__(model, dataset, hp, rng)
+        self.entities_to_convert = []
+
+    def compute_relevance_batch(self, pred, rules, checkpoints: list | None = None):
+        pred = tuple(int(v) for v in pred)
+        s = pred[0]
+        if not self.entities_to_convert:
+            raise ZeroDivisionError("division by zero")  # sum([]) / len([]) in the reference
+        slots, pending, jobs = [], {}, []
+        for rule in rules:
+            rj = []
+            for e in self.entities_to_convert:
+                crule = Dataset.replace_entity_in_triples([tuple(t) for t in rule], s, e)
+                cpred = Dataset.replace_entity_in_triple(pred, s, e)
+                rj.append(self._schedule(cpred, crule, "sufficient", slots, pending))
+            jobs.append(rj)
+            if checkpoints is not None:
+                checkpoints.append(StateCheckpoint())
+        self._run(slots)
+        minimizer = self.model.is_minimizer()
+        out = []
+        self.last_results = []
+        for rj in jobs:
+            rels = []
+            self.last_results.append([(slots[i].result, self.base_pt_results.get(k) or slots[pending[k]].result)
+                                      for i, k in rj])
+            for pt_idx, key in rj:
+                base = self._base_result(key, slots, pending)
+                pt = slots[pt_idx].result
+                rank_improvement = base["target_rank"] - pt["target_rank"]
+                if minimizer:
+                    score_improvement = base["target_score"] - pt["target_score"]
+                else:
+                    score_improvement = pt["target_score"] - base["target_score"]
+                rel = float(np.float32(np.float32(rank_improvement) + np.float32(_sigmoid(score_improvement))))
+                rel /= float(base["target_rank"])
+                rels.append(rel)
+            out.append(sum(rels) / len(rels))
+        return out

@@ -1,0 +1,215 @@
+"""Frozen link-prediction models as seen by the relevance engine.
+
+These classes keep the reference ``Model`` surface the engine uses
+(``name``, ``dimension``, ``is_minimizer()``, ``all_scores(triples)``,
+``MODEL_REGISTRY``; src/link_prediction/models/model.py:8-78,
+src/link_prediction/__init__.py:5-9) and hold the HIP context with the
+frozen tables.  The per-candidate ``Kelpie*`` model construction of the
+reference (transe.py:84-99, complex.py:144-159, conve.py:193-237) is reduced
+to the kelpie-row initialisation below plus the RNG it consumes; the tables
+themselves are never cloned.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _lib
+from .rng import ReferenceRNG
+
+
+class FrozenModel:
+    name = "?"
+
+    def __init__(self, dataset, entity_embeddings, relation_embeddings, device=0):
+        self.dataset = dataset
+        self.entity_embeddings = np.ascontiguousarray(entity_embeddings, dtype=np.float32)
+        self.relation_embeddings = np.ascontiguousarray(relation_embeddings, dtype=np.float32)
+        assert self.entity_embeddings.shape[0] == dataset.num_entities
+        assert self.relation_embeddings.shape[0] == 2 * dataset.num_relations
+        self.device = device
+        self._ctx = None
+
+    # ------------------------------------------------------------ reference surface
+    @property
+    def dimension(self):
+        return self.entity_embeddings.shape[1]
+
+    def is_minimizer(self):
+        return False
+
+    def eval(self):
+        return self
+
+    @property
+    def ctx(self) -> _lib.Context:
+        if self._ctx is None:
+            self._ctx = self._make_ctx()
+        return self._ctx
+
+    def _make_ctx(self):
+        return _lib.Context(self.name, self.entity_embeddings, self.relation_embeddings, device=self.device)
+
+    def all_scores(self, triples):
+        """``Model.all_scores`` over the frozen entities (model.py:19): float32 [B, |E|]."""
+        t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        return self.ctx.all_scores(t[:, 0], t[:, 1])
+
+    # ------------------------------------------------------------ kelpie hooks
+    def kelpie_init(self, init: np.ndarray, rng: ReferenceRNG) -> np.ndarray:
+        raise NotImplementedError
+
+    def kp_hp(self, hp: dict) -> _lib.HP:
+        raise NotImplementedError
+
+    def posttrain_draws(self, rows: np.ndarray, hp: dict, rng: ReferenceRNG) -> np.ndarray:
+        """Random draws of one post-training over ``rows`` (kelpie rows + inverses)."""
+        raise NotImplementedError
+
+
+class ComplEx(FrozenModel):
+    """ComplEx (complex.py:17-142): rows [Re | Im], maximizer."""
+
+    name = "ComplEx"
+
+    def __init__(self, dataset, entity_embeddings, relation_embeddings, init_scale=1e-3, device=0):
+        super().__init__(dataset, entity_embeddings, relation_embeddings, device)
+        assert self.dimension % 2 == 0
+        self.real_dimension = self.dimension // 2
+        self.init_scale = float(init_scale)
+
+    def kelpie_init(self, init, rng):
+        # KelpieComplEx: Parameter(init.cuda()) *= init_scale (complex.py:155-157), float32
+        return (init.astype(np.float32) * np.float32(self.init_scale)).astype(np.float32)
+
+    def kp_hp(self, hp):
+        name = hp["optimizer_name"]
+        if name not in _lib.KP_OPT:
+            raise ValueError(f"unknown optimizer {name}")
+        if float(hp.get("regularizer_weight", 0.0)) != 0.0 and hp.get("regularizer_name", "N3") != "N3":
+            raise NotImplementedError("only the N3 regulariser is supported with a non-zero weight")
+        return _lib.HP(optimizer=_lib.KP_OPT[name], epochs=int(hp["epochs"]), batch_size=int(hp["batch_size"]),
+                       lr=float(hp["lr"]), beta1=float(hp.get("decay1", 0.9)), beta2=float(hp.get("decay2", 0.999)),
+                       eps=1e-10 if name == "Adagrad" else 1e-8, reg_weight=float(hp.get("regularizer_weight", 0.0)))
+
+    def posttrain_draws(self, rows, hp, rng):
+        return rng.complex_epochs(len(rows), int(hp["epochs"]), int(hp["batch_size"]))
+
+
+class TransE(FrozenModel):
+    """TransE (transe.py:17-82): L2 distance, minimizer."""
+
+    name = "TransE"
+
+    def __init__(self, dataset, entity_embeddings, relation_embeddings, norm=2, device=0):
+        super().__init__(dataset, entity_embeddings, relation_embeddings, device)
+        if norm != 2:
+            raise NotImplementedError("TransE: only the L2 norm (all reference configs) is supported")
+        self.norm = norm
+
+    def is_minimizer(self):
+        return True
+
+    def kelpie_init(self, init, rng):
+        # KelpieTransE: xavier_normal_ overwrites the init copy (transe.py:93-95)
+        return rng.xavier_row(self.dimension)
+
+    def kp_hp(self, hp):
+        return _lib.HP(optimizer=_lib.KP_OPT["Adam"], epochs=int(hp["epochs"]), batch_size=int(hp["batch_size"]),
+                       lr=float(hp["lr"]), beta1=0.9, beta2=0.999, eps=1e-8,
+                       reg_weight=float(hp["regularizer_weight"]), margin=float(hp["margin"]),
+                       neg_ratio=int(hp["negative_triples_ratio"]))
+
+    def posttrain_draws(self, rows, hp, rng):
+        return rng.transe_epochs(len(rows), int(hp["epochs"]), int(hp["negative_triples_ratio"]),
+                                 self.dataset.num_entities + 1)
+
+
+class ConvE(FrozenModel):
+    """ConvE (conve.py:23-191): 20 x (d/20) images, 32 3x3 filters, sigmoid scores."""
+
+    name = "ConvE"
+
+    def __init__(self, dataset, entity_embeddings, relation_embeddings, conv_weight, conv_bias, fc_weight, fc_bias,
+                 bn=None, input_dropout_rate=0.0, feature_map_dropout_rate=0.0, hidden_dropout_rate=0.0, device=0):
+        super().__init__(dataset, entity_embeddings, relation_embeddings, device)
+        d = self.dimension
+        if d % 20 or d // 20 < 3:
+            raise ValueError("ConvE dimension must be 20*h with h >= 3")
+        if input_dropout_rate or feature_map_dropout_rate:
+            raise NotImplementedError("ConvE input / feature-map dropout > 0 during post-training")
+        self.hidden_layer_size = 32 * 38 * (d // 20 - 2)
+        self.conv_weight = np.asarray(conv_weight, np.float32).reshape(32, 3, 3)
+        self.conv_bias = np.asarray(conv_bias, np.float32).reshape(32)
+        self.fc_weight = np.asarray(fc_weight, np.float32).reshape(d, self.hidden_layer_size)
+        self.fc_bias = np.asarray(fc_bias, np.float32).reshape(d)
+        self.hidden_dropout_rate = float(hidden_dropout_rate)
+        alpha, beta = [], []
+        for i, c in ((1, 1), (2, 32), (3, d)):
+            b = (bn or {}).get(i, {})
+            w = np.asarray(b.get("weight", np.ones(c)), np.float32)
+            bias = np.asarray(b.get("bias", np.zeros(c)), np.float32)
+            mean = np.asarray(b.get("running_mean", np.zeros(c)), np.float32)
+            var = np.asarray(b.get("running_var", np.ones(c)), np.float32)
+            inv = (1.0 / np.sqrt(var.astype(np.float64) + 1e-5)).astype(np.float32)
+            a = (inv * w).astype(np.float32)
+            alpha.append(a)
+            beta.append((bias - mean * a).astype(np.float32))
+        self.bn_alpha = np.concatenate(alpha)
+        self.bn_beta = np.concatenate(beta)
+
+    def _make_ctx(self):
+        return _lib.Context("ConvE", self.entity_embeddings, self.relation_embeddings, device=self.device,
+                            conve={"conv_w": self.conv_weight, "conv_b": self.conv_bias, "fc_w": self.fc_weight,
+                                   "fc_b": self.fc_bias, "bn_alpha": self.bn_alpha, "bn_beta": self.bn_beta})
+
+    def kelpie_init(self, init, rng):
+        rng.conve_construction(self.hidden_layer_size, self.dimension)
+        return init.astype(np.float32).copy()
+
+    def kp_hp(self, hp):
+        return _lib.HP(optimizer=_lib.KP_OPT["Adam"], epochs=int(hp["epochs"]), batch_size=int(hp["batch_size"]),
+                       lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, label_smoothing=float(hp["label_smoothing"]),
+                       hidden_dropout=self.hidden_dropout_rate)
+
+    def er_vocab_sizes(self, rows: np.ndarray, batch_size: int, epochs: int):
+        pairs = {}
+        for h, r, _ in rows.tolist():
+            pairs.setdefault((h, r), None)
+        P = len(pairs)
+        per_epoch = [min(batch_size, P - s) for s in range(0, P, batch_size)]
+        return per_epoch * epochs
+
+    def posttrain_draws(self, rows, hp, rng):
+        steps = self.er_vocab_sizes(rows, int(hp["batch_size"]), int(hp["epochs"]))
+        return rng.conve_masks(steps, self.dimension, self.hidden_dropout_rate)
+
+
+MODEL_REGISTRY = {"ComplEx": ComplEx, "TransE": TransE, "ConvE": ConvE}
+
+
+def from_state_dict(name, dataset, state, model_params, device=0):
+    """Build a frozen model from a reference checkpoint state dict (``torch.save(
+    model.state_dict())``, pairwise_ranking_optimizer.py:96-98 etc.), loaded by
+    the caller with ``torch.load(path, weights_only=True)``."""
+
+    def arr(k):
+        v = state[k]
+        return v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
+
+    E, R = arr("entity_embeddings"), arr("relation_embeddings")
+    if name == "ComplEx":
+        return ComplEx(dataset, E, R, init_scale=model_params.get("init_scale", 1e-3), device=device)
+    if name == "TransE":
+        return TransE(dataset, E, R, norm=model_params.get("norm", 2), device=device)
+    if name == "ConvE":
+        bn = {}
+        for i in (1, 2, 3):
+            bn[i] = {k: arr(f"batch_norm_{i}.{k}") for k in ("weight", "bias", "running_mean", "running_var")}
+        return ConvE(dataset, E, R, arr("convolutional_layer.weight"), arr("convolutional_layer.bias"),
+                     arr("hidden_layer.weight"), arr("hidden_layer.bias"), bn=bn,
+                     input_dropout_rate=model_params.get("input_dropout_rate", 0.0),
+                     feature_map_dropout_rate=model_params.get("feature_map_dropout_rate", 0.0),
+                     hidden_dropout_rate=model_params.get("hidden_dropout_rate", 0.0), device=device)
+    raise ValueError(name)

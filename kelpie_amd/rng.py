@@ -1,0 +1,114 @@
+"""Host RNG protocol: the reference's random draws, in the reference's order.
+
+Post-training is stochastic.  The reference draws from
+three process-global generators while it runs candidate after candidate:
+
+* torch CPU generator: the kelpie init ``torch.rand(1, D)``
+  (post_training_engine.py:52), TransE's ``xavier_normal_`` on the kelpie row
+  (transe.py:93-95), the ``reset_parameters()`` of the throw-away Conv2d /
+  Linear every ``KelpieConvE`` builds (conve.py:46-52 via :202),
+  ``torch.randperm`` per ComplEx epoch (multiclass_nll_optimizer.py:148),
+  ``torch.randint`` negatives per TransE epoch (pairwise_ranking_optimizer.py:171-172)
+  and ConvE's hidden-dropout masks (Dropout left in train mode, model.py:114-125);
+* numpy global ``RandomState``: ``np.random.shuffle`` of the TransE rows
+  (pairwise_ranking_optimizer.py:166);
+* python ``random``: builder termination and conversion-entity sampling.
+
+The batched GPU engine evaluates many candidates at once, so the host draws
+every candidate's numbers up front, in exactly the reference's sequence, from
+the same generators, and ships them to the kernels (RNG-as-input).  Seeded
+identically, the engine therefore sees bit-identical draws to the reference.
+
+Draws whose VALUES the kernels never need are skipped by advancing the
+generator state (:func:`kelpie_amd._lib.mt19937_discard`): a ComplEx epoch
+whose rows fit one minibatch only reorders the batch, and a ConvE model
+construction only burns ``32*9 + 32 + hidden*dim + dim`` outputs.
+Consumption counts (randperm(n): n-1 outputs, randint: one per element,
+bernoulli_: two per element) are pinned by ``tests/test_rng_protocol.py``.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _get_state():
+    return torch.get_rng_state().numpy().copy()
+
+
+def _set_state(st):
+    torch.set_rng_state(torch.from_numpy(st))
+
+
+class ReferenceRNG:
+    """Draws from the process-global torch / numpy generators (reference order)."""
+
+    # ---------------------------------------------------------------- model construction
+    def rand_init(self, D: int) -> np.ndarray:
+        return torch.rand(1, D).numpy()[0].astype(np.float32)
+
+    def xavier_row(self, d: int) -> np.ndarray:
+        # xavier_normal_ on a (1, d) parameter: normal_(0, sqrt(2 / (d + 1)))
+        return torch.empty(1, d).normal_(0.0, math.sqrt(2.0 / float(d + 1))).numpy()[0].astype(np.float32)
+
+    def discard(self, n: int):
+        if n <= 0:
+            return
+        st = _get_state()
+        _lib.mt19937_discard(st, n)
+        _set_state(st)
+
+    def conve_construction(self, hidden: int, dim: int):
+        self.discard(32 * 9 + 32 + hidden * dim + dim)
+
+    # ---------------------------------------------------------------- per-optimizer draws
+    def complex_epochs(self, R: int, epochs: int, batch_size: int) -> np.ndarray:
+        """Per-epoch ``torch.randperm(R)``; values are only needed when an epoch
+        has more than one minibatch."""
+        if R > batch_size:
+            return np.concatenate([torch.randperm(R).numpy().astype(np.int32) for _ in range(epochs)]) \
+                if epochs else np.zeros(0, np.int32)
+        self.discard(epochs * max(R - 1, 0))
+        return np.zeros(0, np.int32)
+
+    def transe_epochs(self, R: int, epochs: int, ratio: int, n_entities: int) -> np.ndarray:
+        """Per epoch [row order (R) | negative entity (R) | head_or_tail (R)].
+
+        The row order composes the in-place ``np.random.shuffle`` of every epoch;
+        of the ``ratio*R`` randint draws only the first R are stepped (SURVEY A-Q2)."""
+        out = np.zeros((epochs, 3, R), np.int32)
+        idx = np.arange(R, dtype=np.int64)
+        n = ratio * R
+        for e in range(epochs):
+            np.random.shuffle(idx)
+            ents = torch.randint(high=n_entities, size=(n,))
+            hot = torch.randint(high=2, size=(n,))
+            out[e, 0] = idx
+            out[e, 1] = ents[:R].numpy()
+            out[e, 2] = hot[:R].numpy()
+        return out.reshape(-1)
+
+    def conve_masks(self, n_rows_per_step, dim: int, p_drop: float) -> np.ndarray:
+        """Hidden-dropout keep bits for every step, packed per step in uint32 words."""
+        if p_drop <= 0.0:
+            return np.zeros(0, np.int32)
+        st = _get_state()
+        chunks = [_lib.bernoulli_bits(st, int(b) * dim, 1.0 - p_drop) for b in n_rows_per_step]
+        _set_state(st)
+        return np.concatenate(chunks).view(np.int32) if chunks else np.zeros(0, np.int32)
+
+
+class StateCheckpoint:
+    """Snapshot of the torch / numpy generators (to rewind speculative draws)."""
+
+    def __init__(self):
+        self.torch_state = torch.get_rng_state()
+        self.np_state = np.random.get_state()
+
+    def restore(self):
+        torch.set_rng_state(self.torch_state)
+        np.random.set_state(self.np_state)

@@ -413,10 +413,10 @@ def posttrain_transe(model: OracleModel, ds, triples, x0, hp, rng):
     d = model.dimension
     opt = AdamState(d, hp["lr"])
     for _ in range(int(hp["epochs"])):
-        rng.np_shuffle(rows)  # in place, compounding across epochs
-        rep = np.repeat(rows, ratio, axis=0)
-        ents = rng.randint(N, rep.shape[0])
-        hot = rng.randint(2, rep.shape[0])
+        # in-place shuffle (compounding across epochs) + ratio*R negatives
+        rows_e, ents, hot = rng.transe_epoch(rows, N, ratio)
+        rep = np.repeat(rows_e, ratio, axis=0)[:n]
+        ents, hot = ents[:n], hot[:n]
         neg = rep.copy()
         neg[:, 0] = np.where(hot == 1, ents, rep[:, 0])
         neg[:, 2] = np.where(hot == 1, rep[:, 2], ents)
@@ -532,11 +532,14 @@ class TorchNumpyRNG:
     def randperm(self, n):
         return torch.randperm(n).numpy()  # multiclass_nll_optimizer.py:148
 
-    def np_shuffle(self, arr):
-        np.random.shuffle(arr)  # pairwise_ranking_optimizer.py:166
-
-    def randint(self, high, size):
-        return torch.randint(high=high, size=(size,)).numpy()
+    def transe_epoch(self, rows, n_entities, ratio):
+        # pairwise_ranking_optimizer.py:166-172: shuffle in place, then
+        # randint(N) and randint(2) over the ratio-times repeated rows
+        np.random.shuffle(rows)
+        n = ratio * rows.shape[0]
+        ents = torch.randint(high=n_entities, size=(n,)).numpy()
+        hot = torch.randint(high=2, size=(n,)).numpy()
+        return rows, ents, hot
 
     def conve_ctor(self, hidden, dim):
         # KelpieConvE.__init__ builds a fresh ConvE(init_random=False) (conve.py:193-205),

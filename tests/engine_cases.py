@@ -1,0 +1,107 @@
+"""Shared checks of the product engine against the reference golden vectors.
+
+Used by test_engine_cpu.py (oracle-backed context: host protocol only) and
+test_gpu_parity.py (the HIP library on an MI355X)."""
+from __future__ import annotations
+
+import numpy as np
+
+from golden_io import load_case, seed_all
+
+import kelpie_amd as ka
+
+TOL = 1e-4
+
+
+def build_product(name, backend):
+    rec, arrays, w = load_case(name)
+    ds = ka.Dataset(rec["num_entities"], rec["num_relations"], arrays["train"], arrays["valid"], arrays["test"])
+    mp = rec["model_params"]
+    if rec["model"] == "ComplEx":
+        model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"], init_scale=mp["init_scale"])
+    elif rec["model"] == "TransE":
+        model = ka.TransE(ds, w["entity_embeddings"], w["relation_embeddings"], norm=mp["norm"])
+    else:
+        bn = {i: {"weight": w[f"bn{i}_weight"], "bias": w[f"bn{i}_bias"], "running_mean": w[f"bn{i}_mean"],
+                  "running_var": w[f"bn{i}_var"]} for i in (1, 2, 3)}
+        model = ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
+                         w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn,
+                         input_dropout_rate=mp["input_dropout_rate"],
+                         feature_map_dropout_rate=mp["feature_map_dropout_rate"],
+                         hidden_dropout_rate=mp["hidden_dropout_rate"])
+    if backend == "cpu":
+        from cpu_backend import OracleBackedContext
+        model._ctx = OracleBackedContext(model)
+    return rec, ds, model
+
+
+def _close(a, b, tol=TOL):
+    return abs(a - b) <= tol * max(1.0, abs(b))
+
+
+def check_necessary(name, backend, batched):
+    """Every recorded compute_relevance call; batched=True evaluates all rules of
+    a prediction in one engine batch (must equal the sequential reference)."""
+    rec, ds, model = build_product(name, backend)
+    seed_all(rec["seed"])
+    eng = ka.NecessaryPostTrainingEngine(model, ds, rec["hp"])
+    stats = {"rank_match": 0, "n": 0, "max_rel_err": 0.0, "max_score_err": 0.0}
+    for block in rec["necessary"]:
+        eng.set_cache()
+        pred = tuple(block["pred"])
+        rules = [[tuple(t) for t in c["rule"]] for c in block["calls"]]
+        if batched:
+            rels = eng.compute_relevance_batch(pred, rules)
+            results = list(eng.last_results)
+        else:
+            rels, results = [], []
+            for r in rules:
+                rels.append(eng.compute_relevance(pred, r))
+                results.append(eng.last_results[0])
+        for ci, (call, rel, (pt, base)) in enumerate(zip(block["calls"], rels, results)):
+            exp_pt = call["results"][-1]
+            stats["n"] += 1
+            stats["rank_match"] += int(pt["target_rank"] == exp_pt["target_rank"])
+            stats["max_rel_err"] = max(stats["max_rel_err"], abs(rel - call["relevance"]))
+            stats["max_score_err"] = max(stats["max_score_err"], abs(pt["target_score"] - exp_pt["target_score"]))
+            if ci == 0:
+                eb = call["results"][0]
+                assert base["target_rank"] == eb["target_rank"], (name, pred, "base rank")
+                assert _close(base["target_score"], eb["target_score"]), (name, pred, "base score")
+            assert pt["target_rank"] == exp_pt["target_rank"], (name, pred, call["rule"], pt, exp_pt)
+            assert _close(pt["target_score"], exp_pt["target_score"]), (name, pred, call["rule"], pt, exp_pt)
+            assert abs(rel - call["relevance"]) <= TOL, (name, pred, call["rule"], rel, call["relevance"])
+    return stats
+
+
+def check_sufficient(name, backend, batched):
+    rec, ds, model = build_product(name, backend)
+    seed_all(rec["seed"])
+    eng = ka.SufficientPostTrainingEngine(model, ds, rec["hp"])
+    for block in rec["sufficient"]:
+        eng.set_cache()
+        pred = tuple(block["pred"])
+        ents = eng.select_entities_to_convert(pred, block["k"], block["degree_cap"])
+        assert ents == block["entities_to_convert"], (ents, block["entities_to_convert"])
+        rules = [[tuple(t) for t in c["rule"]] for c in block["calls"]]
+        rels = eng.compute_relevance_batch(pred, rules) if batched else [eng.compute_relevance(pred, r) for r in rules]
+        for call, rel in zip(block["calls"], rels):
+            assert abs(rel - call["relevance"]) <= TOL, (name, call["rule"], rel, call["relevance"])
+
+
+def check_builder(name, backend, window=32):
+    rec, ds, model = build_product(name, backend)
+    for key in ("builder", "builder_window"):
+        b = rec.get(key)
+        if not b:
+            continue
+        seed_all(rec["seed"])
+        eng = ka.NecessaryPostTrainingEngine(model, ds, rec["hp"])
+        builder = ka.StochasticBuilder(b["xsi"], eng, window=window)
+        eng.set_cache()
+        out = builder.build_explanations(tuple(b["pred"]), [tuple(t) for t in b["candidates"]])
+        assert out["#relevances"] == b["n_relevances"], (key, out["#relevances"], b["n_relevances"])
+        assert len(out["rule_to_relevance"]) == len(b["rule_to_relevance"])
+        for (rule, rel), (erule, erel) in zip(out["rule_to_relevance"], b["rule_to_relevance"]):
+            assert [list(t) for t in rule] == [list(t) for t in erule]
+            assert abs(rel - erel) <= TOL

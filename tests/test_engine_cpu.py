@@ -1,0 +1,30 @@
+"""Host layer of the product engine vs the reference golden vectors, on CPU.
+
+The HIP context is replaced by the oracle-backed stand-in (tests/cpu_backend.py),
+so these tests pin everything the product does on the host -- kelpie views and
+filters, the RNG protocol (draw order, skipped draws), slot assembly, relevance
+formulas, batching and the builder's speculative windows with RNG rewind.
+"""
+import pytest
+
+from engine_cases import check_builder, check_necessary, check_sufficient
+from golden_io import CASES
+
+FAST = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve60_tiny"]
+
+
+@pytest.mark.parametrize("name", FAST)
+@pytest.mark.parametrize("batched", [False, True])
+def test_necessary_host_protocol(name, batched):
+    check_necessary(name, "cpu", batched)
+
+
+@pytest.mark.parametrize("name", FAST)
+def test_sufficient_host_protocol(name):
+    check_sufficient(name, "cpu", batched=True)
+
+
+@pytest.mark.parametrize("name", ["transe_tiny", "complex_tiny", "conve60_tiny"])
+@pytest.mark.parametrize("window", [1, 4, 32])
+def test_builder_speculative_windows(name, window):
+    check_builder(name, "cpu", window=window)

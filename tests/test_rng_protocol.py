@@ -1,0 +1,76 @@
+"""The host RNG protocol's shortcuts consume exactly what the reference's calls consume."""
+import numpy as np
+import torch
+
+from kelpie_amd import _lib
+from kelpie_amd.rng import ReferenceRNG
+
+
+def _state():
+    return torch.get_rng_state().numpy().copy()
+
+
+def test_discard_matches_randperm():
+    for n in (1, 2, 7, 72, 600):
+        torch.manual_seed(3)
+        s0 = _state()
+        torch.randperm(n)
+        ref = _state()
+        _lib.mt19937_discard(s0, max(n - 1, 0))
+        assert np.array_equal(s0, ref), n
+
+
+def test_discard_matches_conve_construction():
+    for hidden, dim in ((1216, 60), (9728, 200)):
+        torch.manual_seed(5)
+        torch.rand(3)
+        s0 = _state()
+        torch.nn.Conv2d(1, 32, (3, 3), 1, 0, bias=True)
+        torch.nn.Linear(hidden, dim)
+        ref = _state()
+        torch.set_rng_state(torch.from_numpy(s0))
+        ReferenceRNG().conve_construction(hidden, dim)
+        assert np.array_equal(_state(), ref)
+
+
+def test_bernoulli_bits_match_torch():
+    for shape, p in (((3, 5), 0.8), ((20, 200), 0.8), ((7, 60), 0.5)):
+        torch.manual_seed(11)
+        s0 = _state()
+        m = torch.empty(*shape).bernoulli_(p).numpy().reshape(-1)
+        ref = _state()
+        bits = _lib.bernoulli_bits(s0, m.size, p)
+        got = np.unpackbits(bits.view(np.uint8), bitorder="little")[:m.size]
+        assert np.array_equal(got, m.astype(np.uint8))
+        assert np.array_equal(s0, ref)
+
+
+def test_complex_epochs_skip_is_equivalent():
+    rng = ReferenceRNG()
+    torch.manual_seed(9)
+    rng.complex_epochs(40, 43, 512)  # skipped values
+    a = torch.rand(4)
+    torch.manual_seed(9)
+    for _ in range(43):
+        torch.randperm(40)
+    b = torch.rand(4)
+    assert torch.equal(a, b)
+
+
+def test_transe_epochs_match_reference_calls():
+    R, E, ratio, N = 9, 5, 5, 301
+    torch.manual_seed(2)
+    np.random.seed(2)
+    blob = ReferenceRNG().transe_epochs(R, E, ratio, N).reshape(E, 3, R)
+    after = torch.rand(2)
+    torch.manual_seed(2)
+    np.random.seed(2)
+    rows = np.arange(R * 3).reshape(R, 3)
+    for e in range(E):
+        np.random.shuffle(rows)
+        ents = torch.randint(high=N, size=(ratio * R,))
+        hot = torch.randint(high=2, size=(ratio * R,))
+        assert np.array_equal(rows[:, 0] // 3, blob[e, 0])
+        assert np.array_equal(ents[:R].numpy(), blob[e, 1])
+        assert np.array_equal(hot[:R].numpy(), blob[e, 2])
+    assert torch.equal(torch.rand(2), after)
