@@ -92,7 +92,7 @@ def seed_all(seed=42):
     torch.manual_seed(seed)
 
 
-def cpu_baseline(wl, ds, model, pred, cands, gpu_details):
+def cpu_baseline(wl, ds, model, pred, cands, gpu_details, ents=None):
     """Time the oracle (numpy restatement, tests-only module) on a bounded sample
     of the same workload and compare its relevances with the GPU's."""
     from threadpoolctl import threadpool_info
@@ -107,7 +107,6 @@ def cpu_baseline(wl, ds, model, pred, cands, gpu_details):
     t0 = time.time()
     rels, deltas = [], []
     if wl["mode"] == "sufficient":
-        ents = eng.select_entities_to_convert(pred, wl["convert"], 200)
         t0 = time.time()
         for c in cands:
             r, det = eng.sufficient_relevance(pred, [c], ents)
@@ -169,7 +168,9 @@ def main():
         jobs.append(step)
     log(f"[rank {rank}] setup (conversion entities) {time.time() - t_setup:.1f}s")
 
-    def run_step(step):
+    breakdown = {"schedule_s": 0.0, "pack_s": 0.0, "lib_s": 0.0, "device_s": 0.0}
+
+    def run_step(step, record=False):
         recs = []
         hot = [0.0, 0.0, 0]
         units = 0
@@ -184,6 +185,9 @@ def main():
             hot[0] += st.get("hot_s", 0.0)
             hot[1] += st.get("hot_work", 0.0)
             hot[2] += st.get("hot_launches", 0)
+            if record:
+                for k in breakdown:
+                    breakdown[k] += st.get(k, 0.0)
             units += len(cands)
             for r in rels:
                 recs.append([r, 0, 0, 0, 0])
@@ -197,7 +201,7 @@ def main():
     t0 = time.perf_counter()
     units, recs, hot = 0, [], [0.0, 0.0, 0]
     for i in range(args.warmup, n_steps):
-        u, r, h = run_step(jobs[i])
+        u, r, h = run_step(jobs[i], record=True)
         units += u
         recs += r
         hot = [hot[0] + h[0], hot[1] + h[1], hot[2] + h[2]]
@@ -236,12 +240,15 @@ def main():
         else:
             gpu_deltas = [pt["target_rank"] - b["target_rank"] for pt, b in eng.last_results]
         try:
-            cpu, cpu_rels, match = cpu_baseline(wl, ds, model, pred, sample, gpu_deltas)
+            cpu, cpu_rels, match = cpu_baseline(wl, ds, model, pred, sample, gpu_deltas, ents)
             match_rate = float(np.mean(match)) if match else None
-            log(f"[rank 0] oracle rels {cpu_rels} gpu rels {gpu_rels}")
+            log(f"[rank 0] oracle rels {cpu_rels} gpu rels {gpu_rels} rank-delta matches {match}")
         except Exception as exc:  # the oracle is test infrastructure; report, never fake
             log(f"[rank 0] cpu baseline failed: {exc!r}")
 
+    log(f"[rank {rank}] per-step breakdown (s): " +
+        ", ".join(f"{k}={v / max(args.steps, 1):.4f}" for k, v in breakdown.items()) +
+        f", wall={elapsed / max(args.steps, 1):.4f}")
     if rank == 0:
         ms = elapsed_max / max(args.steps, 1) * 1e3
         line = {"metric": METRIC, "value": total_units / elapsed_max, "unit": "candidates/s", "n_gpus": world,

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import math
 import random
+import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
 
@@ -143,6 +144,7 @@ class PostTrainingEngine(RelevanceEngine):
     def _run(self, slots):
         if not slots:
             return
+        t_run = time.perf_counter()
         n = len(slots)
         D = self.model.dimension
         x0 = np.stack([s.x0 for s in slots]).astype(np.float32)
@@ -159,11 +161,14 @@ class PostTrainingEngine(RelevanceEngine):
         filt_off[1:] = np.cumsum([len(s.filt) for s in slots])
         filt = np.array([e for s in slots for e in s.filt], np.int32) if filt_off[-1] else np.zeros(1, np.int32)
         assert x0.shape == (n, D)
+        t_lib = time.perf_counter()
         score, rank, _ = self.model.ctx.posttrain_rank(self._kp_hp, x0, row_off, rows, rng_off, rng, pred,
                                                        filt_off, filt)
+        t_end = time.perf_counter()
         for i, s in enumerate(slots):
             s.result = {"target_score": float(score[i]), "target_rank": int(rank[i])}
-        self.last_batch_stats = {"slots": n, "rows": int(row_off[-1]), **self.model.ctx.last_timing()}
+        self.last_batch_stats = {"slots": n, "rows": int(row_off[-1]), "pack_s": t_lib - t_run,
+                                 "lib_s": t_end - t_lib, **self.model.ctx.last_timing()}
 
     def _base_result(self, key, slots, pending_base):
         if key in self.base_pt_results:
@@ -188,12 +193,15 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
         ``compute_relevance`` on each rule in order.  When ``checkpoints`` is a
         list, the generator state after each rule's draws is appended to it."""
         slots, pending, jobs = [], {}, []
+        t0 = time.perf_counter()
         for rule in rules:
             pt_idx, key = self._schedule(pred, [tuple(t) for t in rule], "necessary", slots, pending)
             jobs.append((pt_idx, key))
             if checkpoints is not None:
                 checkpoints.append(StateCheckpoint())
+        t_sched = time.perf_counter() - t0
         self._run(slots)
+        self.last_batch_stats["schedule_s"] = t_sched
         out = []
         minimizer = self.model.is_minimizer()
         for pt_idx, key in jobs:
@@ -223,6 +231,7 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
         if not self.entities_to_convert:
             raise ZeroDivisionError("division by zero")  # sum([]) / len([]) in the reference
         slots, pending, jobs = [], {}, []
+        t0 = time.perf_counter()
         for rule in rules:
             rj = []
             for e in self.entities_to_convert:
@@ -232,7 +241,9 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
             jobs.append(rj)
             if checkpoints is not None:
                 checkpoints.append(StateCheckpoint())
+        t_sched = time.perf_counter() - t0
         self._run(slots)
+        self.last_batch_stats["schedule_s"] = t_sched
         minimizer = self.model.is_minimizer()
         out = []
         self.last_results = []
