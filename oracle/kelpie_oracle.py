@@ -432,7 +432,8 @@ def posttrain_transe(model: OracleModel, ds, triples, x0, hp, rng):
                 v = (E[tri[:, 0]] + model.R[tri[:, 1]] - E[tri[:, 2]]).astype(F32)
                 f = np.sqrt((v.astype(np.float64) ** 2).sum(1))
                 vs.append((v, f, tri))
-            act = (vs[0][1] - vs[1][1] + float(margin)) > 0
+            # clamp_min backward passes the gradient where z >= 0
+            act = (vs[0][1] - vs[1][1] + float(margin)) >= 0
             for sign, (v, f, tri) in ((1.0, vs[0]), (-1.0, vs[1])):
                 with np.errstate(invalid="ignore", divide="ignore"):
                     u = np.where(f[:, None] > 0, v / f[:, None], 0.0)

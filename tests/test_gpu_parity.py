@@ -12,7 +12,7 @@ import kelpie_amd as ka
 
 pytestmark = pytest.mark.gpu
 
-GPU_CASES = ["complex_tiny", "complex_adam_tiny"]
+GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny"]
 
 
 @pytest.mark.parametrize("name", GPU_CASES)
@@ -26,7 +26,7 @@ def test_sufficient_vs_reference_goldens(name):
     check_sufficient(name, "gpu", batched=True)
 
 
-@pytest.mark.parametrize("name", ["complex_tiny"])
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
 @pytest.mark.parametrize("window", [1, 32])
 def test_builder_vs_reference_goldens(name, window):
     check_builder(name, "gpu", window=window)
