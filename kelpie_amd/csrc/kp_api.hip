@@ -61,10 +61,10 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     c->n_rel2 = m->n_rel2;
     c->dim = m->dim;
     KP_HIP(hipSetDevice(device));
-    if (m->model == KP_MODEL_COMPLEX) {
-      KP_REQUIRE(m->dim % 2 == 0, "ComplEx: row width must be even ([Re | Im])");
+    if (m->model == KP_MODEL_COMPLEX || m->model == KP_MODEL_CONVE) {
+      KP_REQUIRE(m->model != KP_MODEL_COMPLEX || m->dim % 2 == 0, "ComplEx: row width must be even ([Re | Im])");
       int db = cx_pick_db(m->dim);
-      KP_REQUIRE(db > 0, "ComplEx: row width > 400 not supported yet");
+      KP_REQUIRE(db > 0, "row width > 400 not supported yet for ComplEx / ConvE");
       c->dp = 16 * db;
     } else {
       c->dp = round_up(m->dim, 16);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -143,6 +144,9 @@ void conve_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rel
 // shared rank kernel launcher (kp_rank.hip): scores [n][ld] already on device,
 // column `kcol` = kelpie score (or -1 when absent)
 void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld, int act);
+// out[z][m][n] = act(sum_{k in split z} A[m][k] B[n][k] + (z == 0 ? bias[n] : 0)), fp32 MFMA
+void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
+                     int ldo, const float* bias, int act, int ksplit);
 void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
                        const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
                        int minimizer, float* d_target, int64_t* d_rank);

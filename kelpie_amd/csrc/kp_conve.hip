@@ -1,11 +1,692 @@
-// kp_conve.hip -- ConvE post-training (placeholder until the kernel lands).
-#include "kp_common.hpp"
-void conve_posttrain_rank(kp_ctx*, const kp_hp*, const kp_batch*) {
-  throw KpError{KP_ENOTSUP, "ConvE kernels not built yet"};
+// kp_conve.hip -- ConvE batched post-training (KelpieConvE + KelpieBCEOptimizer)
+// and ranking, for gfx950.
+//
+// Reference semantics (src/link_prediction/models/conve.py:133-158,193-237,
+// src/link_prediction/optimization/bce_optimizer.py:92-112,161-208):
+//   rows = kelpie triples + inverses -> er_vocab (h, r) -> tails, insertion
+//   order, NOT shuffled; minibatches of batch_size pairs; targets one-hot over
+//   N = |E|+1 entities, smoothed (1-ls) y + 1/N; BCELoss(sigmoid(x . E_all^T));
+//   encoder: BN1 -> conv 3x3 (32) -> BN2 -> ReLU -> FC -> dropout -> BN3 -> ReLU,
+//   with every layer frozen and BN in eval mode, but Dropout in TRAIN mode
+//   (model.py:114-125): the hidden-dropout masks are drawn on the host (RNG as
+//   input, packed keep bits); Adam(lr = 1e-3) on the kelpie row.
+//
+// Per step, for the pairs whose head is the kelpie ("kelpie pairs"):
+//   conv forward (kp_cv_conv_fwd) -> FC (fp32 MFMA GEMM, split-K) -> dropout/BN3/ReLU
+//   (kp_cv_post_fc) -> O = sum_e G(x . E_e) E_e over the frozen entities
+//   (kpattn::kp_attn<.., ATT_BCE_O>, the same MFMA pass as ComplEx) -> target and
+//   kelpie-column corrections and the encoder backward (kp_cv_dx, FC^T GEMM,
+//   kp_cv_conv_bwd) -> kp_cv_update (+ the kelpie-column gradient of every pair;
+//   pairs with a frozen head reuse their precomputed FC output) -> Adam.
+#include <cmath>
+#include <unordered_map>
+
+#include "kp_attn.hpp"
+
+int cx_pick_db(int dim);
+
+namespace {
+using namespace kpattn;
+
+struct CvInst {  // one kelpie pair in one step
+  int slot, rel, b, pos;
+  long long mask_off;  // word offset of this step's keep bits (-1: no dropout)
+  int tail_begin, tail_count;
+};
+struct CvFInst {  // one frozen-head pair in one step
+  int slot, fp, b, pos;
+  long long mask_off;
+};
+struct CvAct {
+  int slot, k_begin, k_count, f_begin, f_count, pad0, pad1, pad2;
+};
+struct CvConst {
+  int n_ent, dim, dp, H, hid;
+  float scale;  // 1/(1-p) as float32 (dropout noise value)
+  float ylo, yhi;
+  int has_mask;
+};
+
+__device__ __forceinline__ float bce_g(float s, float y, float gs) {
+  // BCELoss backward (grad = gs) followed by sigmoid backward, torch op order
+  const float p = 1.0f / (1.0f + __expf(-s));
+  const float w = (1.0f - p) * p;
+  return ((p - y) / fmaxf(w, 1e-12f) * gs) * w;
 }
-void conve_all_scores(kp_ctx*, int, const int32_t*, const int32_t*, float*) {
-  throw KpError{KP_ENOTSUP, "ConvE kernels not built yet"};
+
+__device__ __forceinline__ float noise_at(const int32_t* __restrict__ bits, long long off, int bitidx, float scale) {
+  if (off < 0) return 1.0f;
+  const uint32_t w = (uint32_t)bits[off + (bitidx >> 5)];
+  return ((w >> (bitidx & 31)) & 1u) ? scale : 0.0f;
 }
-void conve_scores_dev(kp_ctx*, int, const int32_t*, const int32_t*, float*, int) {
-  throw KpError{KP_ENOTSUP, "conve kernels not built yet"};
+
+// image (BN1) -> conv 3x3 + bias -> BN2 -> ReLU -> flat (conve.py:134-146).
+// src[i] = (lhs, rel): lhs >= 0 a frozen entity row, lhs < 0 the kelpie row X[-lhs-1].
+__global__ __launch_bounds__(256) void kp_cv_conv_fwd(int M, const int2* __restrict__ src,
+                                                      const float* __restrict__ E, const float* __restrict__ X,
+                                                      const float* __restrict__ R, CvConst k,
+                                                      const float* __restrict__ cw, const float* __restrict__ cb,
+                                                      const float* __restrict__ bna, const float* __restrict__ bnb,
+                                                      float* __restrict__ flat) {
+  __shared__ float img[40 * 32];
+  __shared__ float w[288], bias[32], a2[32], b2[32];
+  const int i = blockIdx.x;
+  if (i >= M) return;
+  const int tid = threadIdx.x;
+  const int2 sr = src[i];
+  const float* lhs = sr.x >= 0 ? E + (size_t)sr.x * k.dp : X + (size_t)(-sr.x - 1) * k.dp;
+  const float* rel = R + (size_t)sr.y * k.dp;
+  const float a1 = bna[0], b1 = bnb[0];
+  for (int j = tid; j < 20 * k.H; j += 256) {
+    img[j] = lhs[j] * a1 + b1;
+    img[20 * k.H + j] = rel[j] * a1 + b1;
+  }
+  for (int j = tid; j < 288; j += 256) w[j] = cw[j];
+  if (tid < 32) {
+    bias[tid] = cb[tid];
+    a2[tid] = bna[1 + tid];
+    b2[tid] = bnb[1 + tid];
+  }
+  __syncthreads();
+  const int W2 = k.H - 2;
+  const int per_c = 38 * W2;
+  for (int o = tid; o < k.hid; o += 256) {
+    const int c = o / per_c, rem = o - c * per_c;
+    const int y = rem / W2, xx = rem - y * W2;
+    float acc = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) acc += w[c * 9 + ky * 3 + kx] * img[(y + ky) * k.H + xx + kx];
+    acc += bias[c];
+    const float v = acc * a2[c] + b2[c];
+    flat[(size_t)i * k.hid + o] = fmaxf(v, 0.f);
+  }
+}
+
+// x = ReLU(BN3(dropout(FC))) from the split-K FC slabs; writes dp-padded rows
+__global__ void kp_cv_post_fc(int M, const float* __restrict__ slabs, int ksplit, CvConst k,
+                              const CvInst* __restrict__ inst, const int32_t* __restrict__ bits,
+                              const float* __restrict__ bna, const float* __restrict__ bnb, float* __restrict__ Q) {
+  const int i = blockIdx.x;
+  if (i >= M) return;
+  const float* a3 = bna + 33;
+  const float* b3 = bnb + 33;
+  for (int d = threadIdx.x; d < k.dp; d += blockDim.x) {
+    float v = 0.f;
+    if (d < k.dim) {
+      float fc = 0.f;
+      for (int z = 0; z < ksplit; ++z) fc += slabs[((size_t)z * M + i) * k.dim + d];
+      float nz = 1.0f;
+      if (inst && k.has_mask) nz = noise_at(bits, inst[i].mask_off, inst[i].pos * k.dim + d, k.scale);
+      const float dr = (inst && k.has_mask) ? fc * nz : fc;
+      v = fmaxf(dr * a3[d] + b3[d], 0.f);
+    }
+    Q[(size_t)i * k.dp + d] = v;
+  }
+}
+
+// block-wide sum (256 threads)
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// dL/dx_i (encoder output) -> dL/dfc_i; also G at the kelpie column
+__global__ __launch_bounds__(256) void kp_cv_dx(int M, CvConst k, const CvInst* __restrict__ inst,
+                                                const float* __restrict__ Q, const float* __restrict__ O, int n_split,
+                                                const int32_t* __restrict__ tails, const float* __restrict__ E,
+                                                const float* __restrict__ X, const int32_t* __restrict__ bits,
+                                                const float* __restrict__ bna, float* __restrict__ dfc,
+                                                float* __restrict__ gk) {
+  __shared__ float red[4];
+  __shared__ float xi[640], xk[640];
+  const int i = blockIdx.x;
+  if (i >= M) return;
+  const int tid = threadIdx.x;
+  const CvInst I = inst[i];
+  for (int d = tid; d < k.dp; d += 256) {
+    xi[d] = Q[(size_t)i * k.dp + d];
+    xk[d] = X[(size_t)I.slot * k.dp + d];
+  }
+  __syncthreads();
+  const float gs = 1.0f / (float)((long long)I.b * (long long)(k.n_ent + 1));
+  // kelpie column
+  float part = 0.f;
+  for (int d = tid; d < k.dim; d += 256) part += xi[d] * xk[d];
+  const float sk = block_sum(part, red);
+  bool k_is_tail = false;
+  for (int t = 0; t < I.tail_count; ++t) k_is_tail |= (tails[I.tail_begin + t] == k.n_ent);
+  const float Gk = bce_g(sk, k_is_tail ? k.yhi : k.ylo, gs);
+  if (tid == 0) gk[i] = Gk;
+  const float* a3 = bna + 33;
+  for (int d0 = 0; d0 < k.dim; d0 += 256) {
+    const int d = d0 + tid;
+    float dx = 0.f;
+    if (d < k.dim) {
+      for (int sp = 0; sp < n_split; ++sp) dx += O[((size_t)sp * M + i) * k.dp + d];
+      dx += Gk * xk[d];
+    }
+    // target corrections: G(s, yhi) - G(s, ylo) for the frozen tails
+    for (int t = 0; t < I.tail_count; ++t) {
+      const int e = tails[I.tail_begin + t];
+      if (e == k.n_ent) continue;
+      float pp = 0.f;
+      for (int dd = tid; dd < k.dim; dd += 256) pp += xi[dd] * E[(size_t)e * k.dp + dd];
+      const float st = block_sum(pp, red);
+      const float corr = bce_g(st, k.yhi, gs) - bce_g(st, k.ylo, gs);
+      if (d < k.dim) dx += corr * E[(size_t)e * k.dp + d];
+    }
+    if (d < k.dim) {
+      const float nz = k.has_mask ? noise_at(bits, I.mask_off, I.pos * k.dim + d, k.scale) : 1.0f;
+      const float relu = xi[d] > 0.f ? 1.0f : 0.0f;
+      dfc[(size_t)i * k.dim + d] = dx * relu * a3[d] * nz;
+    }
+  }
+}
+
+// dL/dflat -> ReLU / BN2 -> transposed 3x3 conv -> BN1 -> the lhs half of the image
+__global__ __launch_bounds__(256) void kp_cv_conv_bwd(int M, CvConst k, const float* __restrict__ dflat,
+                                                      const float* __restrict__ flat,
+                                                      const float* __restrict__ cw, const float* __restrict__ bna,
+                                                      float* __restrict__ dl) {
+  extern __shared__ __attribute__((aligned(16))) float dc[];  // [32][20][W2]
+  __shared__ float w[288];
+  const int i = blockIdx.x;
+  if (i >= M) return;
+  const int tid = threadIdx.x;
+  const int W2 = k.H - 2;
+  const int per_c = 38 * W2;
+  for (int j = tid; j < 288; j += 256) w[j] = cw[j];
+  for (int j = tid; j < 32 * 20 * W2; j += 256) {
+    const int c = j / (20 * W2), rem = j - c * 20 * W2;
+    const int o = c * per_c + rem;  // rows 0..19 of channel c
+    const float f = flat[(size_t)i * k.hid + o];
+    dc[j] = (f > 0.f) ? dflat[(size_t)i * k.hid + o] * bna[1 + c] : 0.f;
+  }
+  __syncthreads();
+  const float a1 = bna[0];
+  for (int j = tid; j < 20 * k.H; j += 256) {
+    const int yy = j / k.H, xx = j - yy * k.H;
+    float acc = 0.f;
+    for (int c = 0; c < 32; ++c) {
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int y = yy - ky;
+        if (y < 0 || y >= 20) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int x = xx - kx;
+          if (x < 0 || x >= W2) continue;
+          acc += dc[(c * 20 + y) * W2 + x] * w[c * 9 + ky * 3 + kx];
+        }
+      }
+    }
+    dl[(size_t)i * k.dp + j] = acc * a1;
+  }
+}
+
+struct CvOpt {
+  float lr, b1, b2, eps, one_minus_b1, one_minus_b2, step_size, bc2_sqrt;
+};
+
+// gradient assembly + Adam, one workgroup per active slot
+__global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __restrict__ act,
+                                                    const CvInst* __restrict__ ki, const CvFInst* __restrict__ fi,
+                                                    const float* __restrict__ Q, const float* __restrict__ gk,
+                                                    const float* __restrict__ dl, const float* __restrict__ fcf,
+                                                    const int32_t* __restrict__ bits, const float* __restrict__ bna,
+                                                    const float* __restrict__ bnb, float* __restrict__ X,
+                                                    float* __restrict__ S1, float* __restrict__ S2, CvOpt opt) {
+  __shared__ float xs[640];
+  __shared__ float xf[640];
+  __shared__ float red[4];
+  const CvAct A = act[blockIdx.x];
+  const int tid = threadIdx.x;
+  float* x = X + (size_t)A.slot * k.dp;
+  for (int d = tid; d < k.dp; d += 256) xs[d] = x[d];
+  __syncthreads();
+  float g[3] = {0.f, 0.f, 0.f};
+  for (int j = 0; j < A.k_count; ++j) {
+    const int ii = A.k_begin + j;
+    const float G = gk[ii];
+    for (int u = 0; u < 3; ++u) {
+      const int d = tid + 256 * u;
+      if (d < k.dim) g[u] += G * Q[(size_t)ii * k.dp + d] + dl[(size_t)ii * k.dp + d];
+    }
+  }
+  const float* a3 = bna + 33;
+  const float* b3 = bnb + 33;
+  for (int j = 0; j < A.f_count; ++j) {
+    const CvFInst F = fi[A.f_begin + j];
+    float part = 0.f;
+    for (int u = 0; u < 3; ++u) {
+      const int d = tid + 256 * u;
+      if (d < k.dim) {
+        const float fc = fcf[(size_t)F.fp * k.dim + d];
+        const float nz = k.has_mask ? noise_at(bits, F.mask_off, F.pos * k.dim + d, k.scale) : 1.0f;
+        const float dr = k.has_mask ? fc * nz : fc;
+        const float v = fmaxf(dr * a3[d] + b3[d], 0.f);
+        xf[d] = v;
+        part += v * xs[d];
+      }
+    }
+    const float s = block_sum(part, red);
+    const float gs = 1.0f / (float)((long long)F.b * (long long)(k.n_ent + 1));
+    const float G = bce_g(s, k.yhi, gs);
+    for (int u = 0; u < 3; ++u) {
+      const int d = tid + 256 * u;
+      if (d < k.dim) g[u] += G * xf[d];
+    }
+    __syncthreads();
+  }
+  for (int u = 0; u < 3; ++u) {
+    const int d = tid + 256 * u;
+    if (d >= k.dim) continue;
+    const size_t o = (size_t)A.slot * k.dp + d;
+    float m1 = S1[o], v2 = S2[o];
+    const float gd = g[u];
+    m1 = m1 + opt.one_minus_b1 * (gd - m1);
+    v2 = v2 * opt.b2;
+    v2 = v2 + (opt.one_minus_b2 * gd) * gd;
+    const float den = sqrtf(v2) / opt.bc2_sqrt + opt.eps;
+    x[d] = xs[d] + (-opt.step_size * m1) / den;
+    S1[o] = m1;
+    S2[o] = v2;
+  }
+}
+
+// kelpie column of the rank scores: sigmoid(q_s . x_s)
+__global__ void kp_cv_kcol(int n, CvConst k, const float* __restrict__ Q, const float* __restrict__ X,
+                           float* __restrict__ scores, int ld) {
+  const int s = blockIdx.x;
+  if (s >= n) return;
+  float z = 0.f;
+  for (int d = threadIdx.x; d < k.dim; d += 64) z += Q[(size_t)s * k.dp + d] * X[(size_t)s * k.dp + d];
+  z = wave_sum(z);
+  if (threadIdx.x == 0) scores[(size_t)s * ld + k.n_ent] = 1.0f / (1.0f + __expf(-z));
+}
+
+CvConst make_const(kp_ctx* c, const kp_hp* hp) {
+  CvConst k{};
+  k.n_ent = c->n_ent;
+  k.dim = c->dim;
+  k.dp = c->dp;
+  k.H = c->dim / 20;
+  k.hid = c->hidden;
+  const double p = hp ? hp->hidden_dropout : 0.0;
+  k.has_mask = (p > 0.0) ? 1 : 0;
+  k.scale = (p > 0.0) ? (1.0f / (float)(1.0 - p)) : 1.0f;
+  const double ls = hp ? hp->label_smoothing : 0.0;
+  if (ls != 0.0) {
+    const float inv_n = (float)(1.0 / (double)(c->n_ent + 1));
+    k.ylo = inv_n;
+    k.yhi = (float)(1.0 - ls) * 1.0f + inv_n;
+  } else {
+    k.ylo = 0.f;
+    k.yhi = 1.f;
+  }
+  return k;
+}
+
+// encoder (eval mode) for n (lhs, rel) sources -> Q [n][dp]
+void encode_eval(kp_ctx* c, int n, const int2* dsrc, const float* dX, float* dQ) {
+  if (n <= 0) return;
+  CvConst k = make_const(c, nullptr);
+  float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)n * c->hidden));
+  float* dfc = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * (size_t)n * c->dim));
+  hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(n), dim3(256), 0, c->stream, n, dsrc, c->dE, dX, c->dR, k, c->d_conv_w,
+                     c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
+  KP_HIP(hipGetLastError());
+  launch_gemm_abt(c, dflat, c->hidden, n, c->d_fc_w, c->hidden, c->dim, c->hidden, dfc, c->dim, c->d_fc_b, 0, 1);
+  hipLaunchKernelGGL(kp_cv_post_fc, dim3(n), dim3(256), 0, c->stream, n, dfc, 1, k, nullptr, nullptr, c->d_bn_a,
+                     c->d_bn_b, dQ);
+  KP_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+float* conve_fc_wt(kp_ctx* c);
+
+void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
+  const int ns = bt->n_slots;
+  const int K = c->n_ent;
+  const int DP = c->dp;
+  const int DBV = DP / 16;
+  KP_REQUIRE(hp->batch_size >= 1 && hp->epochs >= 0, "ConvE: bad hyper-parameters");
+  CvConst kc = make_const(c, hp);
+  const int E_ = hp->epochs;
+
+  // ---------------- host planning: er_vocab per slot (bce_optimizer.py:92-96)
+  struct Pair {
+    int h, r;
+    std::vector<int> tails;
+  };
+  std::vector<int2> fpairs;                // frozen (h, r) -> fc precompute
+  std::unordered_map<long long, int> fp_id;
+  std::vector<int32_t> tails;
+  std::vector<CvInst> kinst;
+  std::vector<CvFInst> finst;
+  std::vector<CvAct> acts;
+  // per slot: batches (pair ranges) and mask word offsets per step
+  struct SlotPlan {
+    std::vector<Pair> pairs;
+    int nb = 0;
+  };
+  std::vector<SlotPlan> plan(ns);
+  int T = 0;
+  for (int s = 0; s < ns; ++s) {
+    const int r0 = bt->row_off[s], r1 = bt->row_off[s + 1];
+    KP_REQUIRE(r1 >= r0, "ConvE: bad row_off");
+    std::unordered_map<long long, int> idx;
+    auto& P = plan[s].pairs;
+    for (int j = r0; j < r1; ++j) {
+      const int h = bt->rows[3 * j], r = bt->rows[3 * j + 1], t = bt->rows[3 * j + 2];
+      KP_REQUIRE(h >= 0 && h <= K && t >= 0 && t <= K && r >= 0 && r < c->n_rel2, "ConvE: row id out of range");
+      const long long key = (long long)h * c->n_rel2 + r;
+      auto it = idx.find(key);
+      if (it == idx.end()) {
+        idx.emplace(key, (int)P.size());
+        P.push_back(Pair{h, r, {t}});
+      } else {
+        P[it->second].tails.push_back(t);
+      }
+    }
+    plan[s].nb = P.empty() ? 0 : (int)((P.size() + hp->batch_size - 1) / hp->batch_size);
+    T = std::max(T, E_ * plan[s].nb);
+    for (auto& pr : P)
+      if (pr.h != K) {
+        for (int tt : pr.tails) KP_REQUIRE(tt == K, "ConvE: a training row does not involve the kelpie entity");
+        const long long key = (long long)pr.h * c->n_rel2 + pr.r;
+        if (!fp_id.count(key)) {
+          fp_id.emplace(key, (int)fpairs.size());
+          fpairs.push_back(make_int2(pr.h, pr.r));
+        }
+      }
+  }
+  // mask word offsets: per slot, steps in order, ceil(b*dim/32) words each
+  std::vector<std::vector<long long>> moff(ns);
+  for (int s = 0; s < ns; ++s) {
+    const int nb = plan[s].nb;
+    const int P = (int)plan[s].pairs.size();
+    long long off = bt->rng_off[s];
+    for (int t = 0; t < E_ * nb; ++t) {
+      const int j = t % nb;
+      const int b = std::min(hp->batch_size, P - j * hp->batch_size);
+      moff[s].push_back(kc.has_mask ? off : -1);
+      off += ((long long)b * c->dim + 31) / 32;
+    }
+    if (kc.has_mask) KP_REQUIRE(off <= bt->rng_off[s + 1], "ConvE: missing hidden-dropout keep bits");
+  }
+  // per-step instance lists
+  std::vector<int> kin_off(T + 1, 0), fin_off(T + 1, 0), act_o(T + 1, 0);
+  int max_k = 0;
+  for (int t = 0; t < T; ++t) {
+    kin_off[t] = (int)kinst.size();
+    fin_off[t] = (int)finst.size();
+    act_o[t] = (int)acts.size();
+    int local_k = 0;
+    for (int s = 0; s < ns; ++s) {
+      const int nb = plan[s].nb;
+      if (nb == 0 || t >= E_ * nb) continue;
+      const int j = t % nb;
+      const auto& P = plan[s].pairs;
+      const int p0 = j * hp->batch_size, p1 = std::min((int)P.size(), p0 + hp->batch_size);
+      const int b = p1 - p0;
+      CvAct A{};
+      A.slot = s;
+      A.k_begin = local_k;
+      A.f_begin = (int)finst.size() - fin_off[t];
+      for (int q = p0; q < p1; ++q) {
+        const auto& pr = P[q];
+        if (pr.h == K) {
+          CvInst I{};
+          I.slot = s;
+          I.rel = pr.r;
+          I.b = b;
+          I.pos = q - p0;
+          I.mask_off = moff[s][t];
+          I.tail_begin = (int)tails.size();
+          std::vector<int> uniq;
+          for (int tt : pr.tails)
+            if (std::find(uniq.begin(), uniq.end(), tt) == uniq.end()) uniq.push_back(tt);
+          tails.insert(tails.end(), uniq.begin(), uniq.end());
+          I.tail_count = (int)uniq.size();
+          kinst.push_back(I);
+          ++local_k;
+        } else {
+          CvFInst F{};
+          F.slot = s;
+          F.fp = fp_id.at((long long)pr.h * c->n_rel2 + pr.r);
+          F.b = b;
+          F.pos = q - p0;
+          F.mask_off = moff[s][t];
+          finst.push_back(F);
+        }
+      }
+      A.k_count = local_k - A.k_begin;
+      A.f_count = (int)finst.size() - fin_off[t] - A.f_begin;
+      acts.push_back(A);
+    }
+    max_k = std::max(max_k, local_k);
+  }
+  kin_off[T] = (int)kinst.size();
+  fin_off[T] = (int)finst.size();
+  act_o[T] = (int)acts.size();
+
+  // ---------------- uploads
+  std::vector<float> xp((size_t)ns * DP, 0.f);
+  for (int s = 0; s < ns; ++s) std::memcpy(&xp[(size_t)s * DP], bt->x0 + (size_t)s * c->dim, sizeof(float) * c->dim);
+  float* dX = upload(c, c->ws[0], xp.data(), xp.size());
+  float* dS1 = reinterpret_cast<float*>(c->ws[1].ensure(sizeof(float) * xp.size()));
+  float* dS2 = reinterpret_cast<float*>(c->ws[2].ensure(sizeof(float) * xp.size()));
+  KP_HIP(hipMemsetAsync(dS1, 0, sizeof(float) * xp.size(), c->stream));
+  KP_HIP(hipMemsetAsync(dS2, 0, sizeof(float) * xp.size(), c->stream));
+  CvInst* dKI = upload(c, c->ws[3], kinst.data(), std::max<size_t>(1, kinst.size()));
+  CvFInst* dFI = upload(c, c->ws[4], finst.data(), std::max<size_t>(1, finst.size()));
+  CvAct* dAct = upload(c, c->ws[5], acts.data(), std::max<size_t>(1, acts.size()));
+  int32_t* dTails = upload(c, c->ws[6], tails.data(), std::max<size_t>(1, tails.size()));
+  const int64_t nbits = bt->rng_off[ns];
+  int32_t* dBits = upload(c, c->ws[7], bt->rng, (size_t)std::max<int64_t>(1, nbits));
+  const int nfp = (int)fpairs.size();
+
+  KP_HIP(hipEventRecord(c->ev0, c->stream));
+  // frozen-head pairs: FC output (pre-dropout) once per batch
+  float* dFcf = reinterpret_cast<float*>(c->ws[8].ensure(sizeof(float) * (size_t)std::max(1, nfp) * c->dim));
+  if (nfp > 0) {
+    int2* dFp = upload(c, c->ws[9], fpairs.data(), fpairs.size());
+    float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)nfp * c->hidden));
+    hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(nfp), dim3(256), 0, c->stream, nfp, dFp, c->dE, dX, c->dR, kc,
+                       c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
+    KP_HIP(hipGetLastError());
+    launch_gemm_abt(c, dflat, c->hidden, nfp, c->d_fc_w, c->hidden, c->dim, c->hidden, dFcf, c->dim, c->d_fc_b, 0, 1);
+  }
+  // step workspaces
+  const int KS = 8;  // split-K of the FC forward
+  const int mk = std::max(1, max_k);
+  float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)std::max(mk, nfp) * c->hidden));
+  float* dslab = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * (size_t)KS * mk * c->dim));
+  float* dQ = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)mk * DP));
+  int2* dSrc = reinterpret_cast<int2*>(c->ws[15].ensure(sizeof(int2) * (size_t)std::max<size_t>(1, kinst.size())));
+  float* dgs = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)std::max<size_t>(1, kinst.size())));
+  {
+    std::vector<int2> src(kinst.size());
+    std::vector<float> gsv(kinst.size());
+    for (size_t i = 0; i < kinst.size(); ++i) {
+      src[i] = make_int2(-kinst[i].slot - 1, kinst[i].rel);
+      gsv[i] = 1.0f / (float)((long long)kinst[i].b * (long long)(K + 1));
+    }
+    if (!src.empty()) {
+      KP_HIP(hipMemcpyAsync(dSrc, src.data(), sizeof(int2) * src.size(), hipMemcpyHostToDevice, c->stream));
+      KP_HIP(hipMemcpyAsync(dgs, gsv.data(), sizeof(float) * gsv.size(), hipMemcpyHostToDevice, c->stream));
+    }
+  }
+  const int n_split = 4;
+  float* dO = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * (size_t)n_split * mk * DP));
+  float* ddfc = reinterpret_cast<float*>(c->ws[18].ensure(sizeof(float) * (size_t)mk * c->dim));
+  float* dgk = reinterpret_cast<float*>(c->ws[19].ensure(sizeof(float) * (size_t)mk));
+  float* ddflat = reinterpret_cast<float*>(c->ws[20].ensure(sizeof(float) * (size_t)mk * c->hidden));
+  float* ddl = reinterpret_cast<float*>(c->ws[21].ensure(sizeof(float) * (size_t)mk * DP));
+  float* dWt = conve_fc_wt(c);
+
+  CvOpt opt{};
+  opt.lr = hp->lr;
+  opt.b1 = hp->beta1;
+  opt.b2 = hp->beta2;
+  opt.eps = hp->eps;
+  opt.one_minus_b1 = (float)(1.0 - (double)hp->beta1);
+  opt.one_minus_b2 = (float)(1.0 - (double)hp->beta2);
+  double hot = 0.0, work = 0.0;
+  int64_t launches = 0;
+  c->hot_pairs.clear();
+  const size_t shm_attn = 2 * 16 * (DP + 4) * sizeof(float);
+  const size_t shm_cbwd = sizeof(float) * 32 * 20 * (c->dim / 20 - 2);
+  for (int t = 0; t < T; ++t) {
+    const int nk = kin_off[t + 1] - kin_off[t];
+    const int na = act_o[t + 1] - act_o[t];
+    const CvInst* KI = dKI + kin_off[t];
+    if (nk > 0) {
+      hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
+                         kc, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
+      KP_HIP(hipGetLastError());
+      launch_gemm_abt(c, dflat, c->hidden, nk, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b, 0,
+                      KS);
+      hipLaunchKernelGGL(kp_cv_post_fc, dim3(nk), dim3(256), 0, c->stream, nk, dslab, KS, kc, KI, dBits, c->d_bn_a,
+                         c->d_bn_b, dQ);
+      KP_HIP(hipGetLastError());
+      hipEvent_t ea = nullptr, eb = nullptr;
+      if (c->time_hot) {
+        ea = c->event(2 * launches);
+        eb = c->event(2 * launches + 1);
+        KP_HIP(hipEventRecord(ea, c->stream));
+      }
+      const int kps = (K + n_split - 1) / n_split;
+      dim3 grid((nk + 63) / 64, n_split);
+#define CV_ATT(DBX)                                                                                                  \
+  hipLaunchKernelGGL((kp_attn<DBX, ATT_BCE_O>), grid, dim3(256), shm_attn, c->stream, c->dE, K, 0, nullptr, nullptr, \
+                     nullptr, dQ, nk, kps, nullptr, nullptr, dO, dgs + kin_off[t], kc.ylo)
+      switch (DBV) {
+        case 4: CV_ATT(4); break;
+        case 8: CV_ATT(8); break;
+        case 13: CV_ATT(13); break;
+        case 16: CV_ATT(16); break;
+        case 25: CV_ATT(25); break;
+        default: throw KpError{KP_ENOTSUP, "ConvE: unsupported padded dimension"};
+      }
+#undef CV_ATT
+      KP_HIP(hipGetLastError());
+      if (c->time_hot) {
+        KP_HIP(hipEventRecord(eb, c->stream));
+        c->hot_pairs.push_back({(double)nk, 0.0});
+      }
+      ++launches;
+      hipLaunchKernelGGL(kp_cv_dx, dim3(nk), dim3(256), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE, dX,
+                         dBits, c->d_bn_a, ddfc, dgk);
+      KP_HIP(hipGetLastError());
+      launch_gemm_abt(c, ddfc, c->dim, nk, dWt, c->dim, c->hidden, c->dim, ddflat, c->hidden, nullptr, 0, 1);
+      hipLaunchKernelGGL(kp_cv_conv_bwd, dim3(nk), dim3(256), shm_cbwd, c->stream, nk, kc, ddflat, dflat, c->d_conv_w,
+                         c->d_bn_a, ddl);
+      KP_HIP(hipGetLastError());
+    }
+    const double step = (double)(t + 1);
+    opt.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, step)));
+    opt.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)hp->beta2, step));
+    if (na > 0) {
+      // dAct entries index kinst/finst relative to this step's lists
+      hipLaunchKernelGGL(kp_cv_update, dim3(na), dim3(256), 0, c->stream, kc, dAct + act_o[t], KI, dFI + fin_off[t], dQ,
+                         dgk, ddl, dFcf, dBits, c->d_bn_a, c->d_bn_b, dX, dS1, dS2, opt);
+      KP_HIP(hipGetLastError());
+    }
+  }
+
+  // ---------------- rank: sigmoid(enc(x, R_p) . E_e), kelpie column, maximizer
+  const int ld = round_up(K + 1, 4);
+  float* dScores = reinterpret_cast<float*>(c->ws[10].ensure(sizeof(float) * (size_t)ns * ld));
+  std::vector<int2> rsrc(ns);
+  std::vector<int32_t> po(ns);
+  for (int s = 0; s < ns; ++s) {
+    KP_REQUIRE(bt->pred[3 * s] == K, "ConvE: the ranked triple must start at the kelpie entity");
+    rsrc[s] = make_int2(-s - 1, bt->pred[3 * s + 1]);
+    po[s] = bt->pred[3 * s + 2];
+  }
+  int2* dRsrc = upload(c, c->ws[11], rsrc.data(), rsrc.size());
+  float* dQr = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)std::max(ns, mk) * DP));
+  encode_eval(c, ns, dRsrc, dX, dQr);
+  launch_score_gemm(c, dQr, ns, dScores, ld, 1);
+  hipLaunchKernelGGL(kp_cv_kcol, dim3(ns), dim3(64), 0, c->stream, ns, kc, dQr, dX, dScores, ld);
+  KP_HIP(hipGetLastError());
+  int32_t* dPo = upload(c, c->ws[22], po.data(), po.size());
+  int32_t* dFo = upload(c, c->ws[23], bt->filt_off, (size_t)ns + 1);
+  DevBuf bF, bT, bR;
+  int32_t* dF = upload(c, bF, bt->filt, (size_t)std::max(1, bt->filt_off[ns]));
+  float* dTarget = reinterpret_cast<float*>(bT.ensure(sizeof(float) * ns));
+  int64_t* dRank = reinterpret_cast<int64_t*>(bR.ensure(sizeof(int64_t) * ns));
+  launch_rank_count(c, ns, dScores, ld, K + 1, dPo, dFo, dF, 0, dTarget, dRank);
+  KP_HIP(hipEventRecord(c->ev1, c->stream));
+  if (bt->out_x) KP_HIP(hipMemcpyAsync(xp.data(), dX, sizeof(float) * xp.size(), hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipMemcpyAsync(bt->out_score, dTarget, sizeof(float) * ns, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipMemcpyAsync(bt->out_rank, dRank, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  if (bt->out_x)
+    for (int s = 0; s < ns; ++s) std::memcpy(bt->out_x + (size_t)s * c->dim, &xp[(size_t)s * DP], sizeof(float) * c->dim);
+  float ms_all = 0.f;
+  KP_HIP(hipEventElapsedTime(&ms_all, c->ev0, c->ev1));
+  for (size_t i = 0; i < c->hot_pairs.size(); ++i) {
+    float ms = 0.f;
+    KP_HIP(hipEventElapsedTime(&ms, c->event(2 * i), c->event(2 * i + 1)));
+    hot += ms * 1e-3;
+    work += c->hot_pairs[i].first * (double)K;
+  }
+  for (DevBuf* b : {&bF, &bT, &bR}) b->release();
+  c->timing.device_s = ms_all * 1e-3;
+  c->timing.loop_s = ms_all * 1e-3;
+  c->timing.hot_s = hot;
+  c->timing.hot_launches = launches;
+  c->timing.hot_work = work;
+}
+
+float* conve_fc_wt(kp_ctx* c) {
+  // FC weight transposed [hidden][dim] for the backward GEMM (built once, kept in the context)
+  if (!c->dEt) {
+    std::vector<float> w((size_t)c->dim * c->hidden), wt((size_t)c->dim * c->hidden);
+    KP_HIP(hipMemcpy(w.data(), c->d_fc_w, sizeof(float) * w.size(), hipMemcpyDeviceToHost));
+    for (int o = 0; o < c->dim; ++o)
+      for (int j = 0; j < c->hidden; ++j) wt[(size_t)j * c->dim + o] = w[(size_t)o * c->hidden + j];
+    KP_HIP(hipMalloc(&c->dEt, sizeof(float) * wt.size()));
+    KP_HIP(hipMemcpy(c->dEt, wt.data(), sizeof(float) * wt.size(), hipMemcpyHostToDevice));
+  }
+  return c->dEt;
+}
+
+void conve_scores_dev(kp_ctx* c, int n, const int32_t* d_heads, const int32_t* d_rels, float* d_out, int ld) {
+  if (n <= 0) return;
+  std::vector<int32_t> h(n), r(n);
+  KP_HIP(hipMemcpyAsync(h.data(), d_heads, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipMemcpyAsync(r.data(), d_rels, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  std::vector<int2> src(n);
+  for (int i = 0; i < n; ++i) src[i] = make_int2(h[i], r[i]);
+  DevBuf bs, bq;
+  int2* dsrc = upload(c, bs, src.data(), src.size());
+  float* dQ = reinterpret_cast<float*>(bq.ensure(sizeof(float) * (size_t)n * c->dp));
+  encode_eval(c, n, dsrc, nullptr, dQ);
+  launch_gemm_abt(c, dQ, c->dp, n, c->dE, c->dp, c->n_ent, c->dp, d_out, ld, nullptr, 1, 1);
+  KP_HIP(hipStreamSynchronize(c->stream));
+  bs.release();
+  bq.release();
+}
+
+void conve_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rels, float* out) {
+  if (n <= 0) return;
+  DevBuf bh, br, bs;
+  int32_t* dh = upload(c, bh, heads, (size_t)n);
+  int32_t* dr = upload(c, br, rels, (size_t)n);
+  float* dS = reinterpret_cast<float*>(bs.ensure(sizeof(float) * (size_t)n * c->n_ent));
+  conve_scores_dev(c, n, dh, dr, dS, c->n_ent);
+  KP_HIP(hipMemcpyAsync(out, dS, sizeof(float) * (size_t)n * c->n_ent, hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  for (DevBuf* b : {&bh, &br, &bs}) b->release();
 }

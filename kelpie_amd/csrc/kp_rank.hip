@@ -16,9 +16,10 @@
 #define SG_BK 32
 #define SG_LD (SG_BK + 4)
 
-__global__ __launch_bounds__(256) void kp_score_gemm(const float* __restrict__ Q, int nq,
-                                                     const float* __restrict__ E, int n_ent, int dp,
-                                                     float* __restrict__ out, int ld, int act) {
+__global__ __launch_bounds__(256) void kp_gemm_abt(const float* __restrict__ A, int lda, int M,
+                                                   const float* __restrict__ B, int ldb, int N, int k_begin,
+                                                   int k_end, float* __restrict__ out, int ldo,
+                                                   const float* __restrict__ bias, int act) {
   __shared__ __attribute__((aligned(16))) float Qs[SG_BM * SG_LD];
   __shared__ __attribute__((aligned(16))) float Es[SG_BN * SG_LD];
   const int tid = threadIdx.x;
@@ -26,20 +27,25 @@ __global__ __launch_bounds__(256) void kp_score_gemm(const float* __restrict__ Q
   const int g = lane >> 4, c = lane & 15;
   const int q0 = blockIdx.y * SG_BM;
   const int e0 = blockIdx.x * SG_BN;
+  // split-K: blockIdx.z selects a K range and an output slab
+  const int ksplit = gridDim.z;
+  const int klen = (k_end - k_begin + ksplit - 1) / ksplit;
+  const int kb = k_begin + blockIdx.z * ((klen + SG_BK - 1) / SG_BK * SG_BK);
+  const int ke = min(k_end, kb + (klen + SG_BK - 1) / SG_BK * SG_BK);
+  out += (size_t)blockIdx.z * M * ldo;
   f32x4 acc[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = 0; k0 < dp; k0 += SG_BK) {
-    // stage: 64 rows x 32 floats for Q and E (8 float4 per row) -> 512 float4 each, 2 per thread
+  for (int k0 = kb; k0 < ke; k0 += SG_BK) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       int f = tid + 256 * u;
       int row = f >> 3, c4 = (f & 7) * 4;
       float4 vq = make_float4(0.f, 0.f, 0.f, 0.f), ve = vq;
       int kk = k0 + c4;
-      if (q0 + row < nq && kk < dp) vq = *reinterpret_cast<const float4*>(Q + (size_t)(q0 + row) * dp + kk);
-      if (e0 + row < n_ent && kk < dp) ve = *reinterpret_cast<const float4*>(E + (size_t)(e0 + row) * dp + kk);
+      if (q0 + row < M && kk < ke) vq = *reinterpret_cast<const float4*>(A + (size_t)(q0 + row) * lda + kk);
+      if (e0 + row < N && kk < ke) ve = *reinterpret_cast<const float4*>(B + (size_t)(e0 + row) * ldb + kk);
       *reinterpret_cast<float4*>(&Qs[row * SG_LD + c4]) = vq;
       *reinterpret_cast<float4*>(&Es[row * SG_LD + c4]) = ve;
     }
@@ -61,10 +67,11 @@ __global__ __launch_bounds__(256) void kp_score_gemm(const float* __restrict__ Q
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       int q = q0 + 16 * w + 4 * g + r;
-      if (q < nq && e < n_ent) {
+      if (q < M && e < N) {
         float v = acc[n][r];
+        if (bias && blockIdx.z == 0) v += bias[e];
         if (act == 1) v = 1.0f / (1.0f + __expf(-v));
-        out[(size_t)q * ld + e] = v;
+        out[(size_t)q * ldo + e] = v;
       }
     }
   }
@@ -137,11 +144,17 @@ void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, in
   KP_HIP(hipGetLastError());
 }
 
-void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld, int act) {
-  if (nq <= 0) return;
-  dim3 grid((c->n_ent + SG_BN - 1) / SG_BN, (nq + SG_BM - 1) / SG_BM);
-  hipLaunchKernelGGL(kp_score_gemm, grid, dim3(256), 0, c->stream, dQ, nq, c->dE, c->n_ent, c->dp, d_out, ld, act);
+void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
+                     int ldo, const float* bias, int act, int ksplit) {
+  if (M <= 0 || N <= 0) return;
+  KP_REQUIRE(K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0, "gemm: K and leading dims must be multiples of 4");
+  dim3 grid((N + SG_BN - 1) / SG_BN, (M + SG_BM - 1) / SG_BM, std::max(1, ksplit));
+  hipLaunchKernelGGL(kp_gemm_abt, grid, dim3(256), 0, c->stream, A, lda, M, B, ldb, N, 0, K, out, ldo, bias, act);
   KP_HIP(hipGetLastError());
+}
+
+void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld, int act) {
+  launch_gemm_abt(c, dQ, c->dp, nq, c->dE, c->dp, c->n_ent, c->dp, d_out, ld, nullptr, act, 1);
 }
 
 // ----------------------------------------------------------------------------

@@ -12,7 +12,7 @@ import kelpie_amd as ka
 
 pytestmark = pytest.mark.gpu
 
-GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny"]
+GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny", "conve60_tiny", "conve_tiny"]
 
 
 @pytest.mark.parametrize("name", GPU_CASES)
@@ -26,7 +26,7 @@ def test_sufficient_vs_reference_goldens(name):
     check_sufficient(name, "gpu", batched=True)
 
 
-@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny", "conve60_tiny"])
 @pytest.mark.parametrize("window", [1, 32])
 def test_builder_vs_reference_goldens(name, window):
     check_builder(name, "gpu", window=window)
@@ -78,6 +78,41 @@ def test_complex_vs_oracle_full_width(dim):
             assert abs(a[1] - b[1]) <= 1e-4 * max(1.0, abs(b[1])), (a, b)
             assert abs(a[3] - b[3]) <= 1e-4 * max(1.0, abs(b[3])), (a, b)
     assert match == n, f"rank match {match}/{n}"
+
+
+TE_HP = {"batch_size": 2048, "epochs": 30, "lr": 0.01, "margin": 5, "negative_triples_ratio": 5,
+         "regularizer_weight": 1.0}
+
+
+@pytest.mark.parametrize("dim", [200, 16])
+def test_transe_vs_oracle_full_width(dim):
+    from cpu_backend import OracleBackedContext
+    from kelpie_amd import synth
+    g = synth.make_graph("small", seed=5)
+    ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    w = synth.make_weights("TransE", g.num_entities, g.num_relations, dim, seed=5)
+    deg = ds.entity_to_degree
+    test = [tuple(int(v) for v in t) for t in g.test]
+    preds = [t for t in test if 8 <= deg.get(t[0], 0) <= 40][:2] + [max(test, key=lambda t: deg.get(t[0], 0))]
+    out = {}
+    for backend in ("gpu", "cpu"):
+        model = ka.TransE(ds, w["entity_embeddings"], w["relation_embeddings"])
+        if backend == "cpu":
+            model._ctx = OracleBackedContext(model)
+        seed_all(42)
+        eng = ka.NecessaryPostTrainingEngine(model, ds, TE_HP)
+        res = []
+        for pred in preds:
+            eng.set_cache()
+            cands = sorted(ds.entity_to_training_triples[pred[0]])[:4]
+            eng.compute_relevance_batch(pred, [[c] for c in cands])
+            res += [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+                    for pt, b in eng.last_results]
+        out[backend] = res
+    match = sum(int(a[0] == b[0] and a[2] == b[2]) for a, b in zip(out["gpu"], out["cpu"]))
+    for a, b in zip(out["gpu"], out["cpu"]):
+        assert abs(a[1] - b[1]) <= 1e-4 * max(1.0, abs(b[1])), (a, b)
+    assert match == len(out["cpu"]), f"rank match {match}/{len(out['cpu'])}"
 
 
 def test_complex_all_scores_matches_fp32_reference():
