@@ -37,17 +37,25 @@ sys.path.insert(0, ROOT)
 
 METRIC = "candidate explanations evaluated/sec (incl. post-train) + rank-delta match rate"
 
+COMPLEX_HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 43, "lr": 0.043, "decay1": 0.9,
+              "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0}  # ComplEx_DBpedia50_explanation.json
+TRANSE_HP = {"batch_size": 2048, "epochs": 65, "lr": 0.01, "margin": 5, "negative_triples_ratio": 5,
+             "regularizer_weight": 1.0}  # TransE_DBpedia50_explanation.json
+CONVE_HP = {"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.995,
+            "epochs": 109}  # ConvE_DB100K_explanation.json (hidden dropout 0.2)
+
 WORKLOADS = {
+    # BASELINE.json configs[2]: the north-star target (>= 50x, ComplEx on FB15k-237)
     "complex-fb15k237-sufficient": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="sufficient",
-                                        hp={"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 43,
-                                            "lr": 0.043, "decay1": 0.9, "decay2": 0.999,
-                                            "regularizer_name": "N3", "regularizer_weight": 0},
-                                        candidates=20, convert=10),
+                                        hp=COMPLEX_HP, candidates=20, convert=10, preds_per_step=1),
     "complex-fb15k237-necessary": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="necessary",
-                                       hp={"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 43,
-                                           "lr": 0.043, "decay1": 0.9, "decay2": 0.999,
-                                           "regularizer_name": "N3", "regularizer_weight": 0},
-                                       candidates=20, preds_per_step=16),
+                                       hp=COMPLEX_HP, candidates=20, preds_per_step=16),
+    # BASELINE.json configs[1]
+    "transe-fb15k237-necessary": dict(model="TransE", shape="FB15k-237", dim=200, mode="necessary",
+                                      hp=TRANSE_HP, candidates=20, preds_per_step=16),
+    # BASELINE.json configs[4]
+    "conve-yago310-necessary": dict(model="ConvE", shape="YAGO3-10", dim=200, mode="necessary", hp=CONVE_HP,
+                                    candidates=20, preds_per_step=8, hidden_dropout=0.2),
 }
 
 
@@ -56,14 +64,21 @@ def log(*a):
 
 
 def build(wl, device, rank):
-    from kelpie_amd import ComplEx, Dataset, synth
+    from kelpie_amd import ComplEx, ConvE, Dataset, TransE, synth
     t0 = time.time()
     g = synth.make_graph(wl["shape"], seed=0)
     ds = Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test, name=wl["shape"])
     w = synth.make_weights(wl["model"], g.num_entities, g.num_relations, wl["dim"], seed=0)
-    model = ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"], init_scale=1e-3, device=device)
+    if wl["model"] == "ComplEx":
+        model = ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"], init_scale=1e-3, device=device)
+    elif wl["model"] == "TransE":
+        model = TransE(ds, w["entity_embeddings"], w["relation_embeddings"], device=device)
+    else:
+        model = ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
+                      w["conv_bias"], w["fc_weight"], w["fc_bias"], hidden_dropout_rate=wl["hidden_dropout"],
+                      device=device)
     log(f"[rank {rank}] graph+indices {time.time() - t0:.1f}s  |E|={g.num_entities} train={len(g.train)}")
-    return ds, model
+    return ds, model, w
 
 
 def pick_preds(ds, n, seed, lo=5, hi=200):
@@ -92,14 +107,13 @@ def seed_all(seed=42):
     torch.manual_seed(seed)
 
 
-def cpu_baseline(wl, ds, model, pred, cands, gpu_details, ents=None):
+def cpu_baseline(wl, ds, weights, pred, cands, gpu_details, ents=None):
     """Time the oracle (numpy restatement, tests-only module) on a bounded sample
     of the same workload and compare its relevances with the GPU's."""
     from threadpoolctl import threadpool_info
     from oracle import kelpie_oracle as ko
-    om = ko.OracleModel(wl["model"], {"entity_embeddings": model.entity_embeddings,
-                                      "relation_embeddings": model.relation_embeddings},
-                        wl["dim"], {"init_scale": 1e-3})
+    om = ko.OracleModel(wl["model"], weights, wl["dim"],
+                        {"init_scale": 1e-3, "hidden_dropout_rate": wl.get("hidden_dropout", 0.0)})
     ods = ko.OracleDataset(ds.num_entities, ds.num_relations, ds.training_triples, ds.validation_triples,
                            ds.testing_triples)
     seed_all(42)
@@ -138,7 +152,7 @@ def main():
     from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine
     rank, world, local = kd.init_from_env()
     wl = WORKLOADS[args.workload]
-    ds, model = build(wl, local, rank)
+    ds, model, weights = build(wl, local, rank)
     engine_cls = SufficientPostTrainingEngine if wl["mode"] == "sufficient" else NecessaryPostTrainingEngine
     eng = engine_cls(model, ds, wl["hp"])
 
@@ -171,27 +185,20 @@ def main():
     breakdown = {"schedule_s": 0.0, "pack_s": 0.0, "lib_s": 0.0, "device_s": 0.0}
 
     def run_step(step, record=False):
-        recs = []
-        hot = [0.0, 0.0, 0]
-        units = 0
-        for pred, cands, ents in step:
-            eng.set_cache()
-            if ents is not None:
-                if not ents:
-                    continue
-                eng.entities_to_convert = ents
-            rels = eng.compute_relevance_batch(pred, [[c] for c in cands])
-            st = eng.last_batch_stats
-            hot[0] += st.get("hot_s", 0.0)
-            hot[1] += st.get("hot_work", 0.0)
-            hot[2] += st.get("hot_launches", 0)
-            if record:
-                for k in breakdown:
-                    breakdown[k] += st.get(k, 0.0)
-            units += len(cands)
-            for r in rels:
-                recs.append([r, 0, 0, 0, 0])
-        return units, recs, hot
+        """One engine batch: every singleton candidate of the step's predictions."""
+        eng.set_cache()  # per-prediction caches: the base post-trainings are part of the work
+        if wl["mode"] == "sufficient":
+            items = [(pred, [[c] for c in cands], ents) for pred, cands, ents in step if ents]
+        else:
+            items = [(pred, [[c] for c in cands]) for pred, cands, _ in step]
+        outs = eng.compute_relevance_multi(items)
+        st = eng.last_batch_stats
+        hot = [st.get("hot_s", 0.0), st.get("hot_work", 0.0), st.get("hot_launches", 0)]
+        if record:
+            for k in breakdown:
+                breakdown[k] += st.get(k, 0.0)
+        recs = [[r, 0, 0, 0, 0] for out in outs for r in out]
+        return len(recs), recs, hot
 
     for i in range(args.warmup):
         run_step(jobs[i])
@@ -213,15 +220,28 @@ def main():
     all_recs = kd.gather_records(np.array(recs, dtype=np.float64).reshape(-1, kd.RECORD))
     total_units = len(all_recs)
 
-    # roofline of the dominant kernel (kp_cx_attn): 4 * D * |E| flops per (query, entity)
-    D = model.dimension
-    flops = 4.0 * D * hot[1]
-    achieved = flops / hot[0] / 1e12 if hot[0] > 0 else None
-    peak = 157.3
-    roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-            "frac": (achieved / peak) if achieved else None, "traffic": None,
-            "kernel": "kp_cx_attn", "launches": hot[2],
-            "avg_launch_ms": (hot[0] / hot[2] * 1e3) if hot[2] else None}
+    # roofline of the dominant kernel, from its HIP-event launch durations inside the library
+    if wl["model"] == "TransE":
+        # algorithmic bytes: one fresh negative entity row per stepped pair,
+        # plus every positive-side row once per slot (= once per epoch's pairs / epochs)
+        d = model.dimension
+        nbytes = 4.0 * d * hot[1] * (1.0 + 1.0 / wl["hp"]["epochs"])
+        achieved = nbytes / hot[0] / 1e9 if hot[0] > 0 else None
+        peak = 8000.0
+        roof = {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                "frac": (achieved / peak) if achieved else None, "traffic": None, "kernel": "kp_te_posttrain"}
+    else:
+        # 4 * D flops per (query row, frozen entity): s = q.E_e and O += w(s) E_e
+        D = wl["dim"] * (2 if wl["model"] == "ComplEx" else 1)
+        flops = 4.0 * D * hot[1]
+        achieved = flops / hot[0] / 1e12 if hot[0] > 0 else None
+        peak = 157.3
+        roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": (achieved / peak) if achieved else None, "traffic": None,
+                "kernel": "kp_attn<%d,%s>" % (-(-D // 16), "ATT_SOFTMAX_O" if wl["model"] == "ComplEx"
+                                              else "ATT_BCE_O")}
+    roof["launches"] = hot[2]
+    roof["avg_launch_ms"] = (hot[0] / hot[2] * 1e3) if hot[2] else None
 
     cpu = None
     match_rate = None
@@ -240,7 +260,7 @@ def main():
         else:
             gpu_deltas = [pt["target_rank"] - b["target_rank"] for pt, b in eng.last_results]
         try:
-            cpu, cpu_rels, match = cpu_baseline(wl, ds, model, pred, sample, gpu_deltas, ents)
+            cpu, cpu_rels, match = cpu_baseline(wl, ds, weights, pred, sample, gpu_deltas, ents)
             match_rate = float(np.mean(match)) if match else None
             log(f"[rank 0] oracle rels {cpu_rels} gpu rels {gpu_rels} rank-delta matches {match}")
         except Exception as exc:  # the oracle is test infrastructure; report, never fake

@@ -192,30 +192,41 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
         """Relevances of ``rules`` for ``pred``, identical to calling
         ``compute_relevance`` on each rule in order.  When ``checkpoints`` is a
         list, the generator state after each rule's draws is appended to it."""
+        return self.compute_relevance_multi([(pred, rules)], checkpoints)[0]
+
+    def compute_relevance_multi(self, items, checkpoints: list | None = None):
+        """[(pred, rules), ...] -> [[relevance per rule], ...] in ONE device batch;
+        equal to the sequential compute_relevance calls in that order."""
         slots, pending, jobs = [], {}, []
         t0 = time.perf_counter()
-        for rule in rules:
-            pt_idx, key = self._schedule(pred, [tuple(t) for t in rule], "necessary", slots, pending)
-            jobs.append((pt_idx, key))
-            if checkpoints is not None:
-                checkpoints.append(StateCheckpoint())
+        for pred, rules in items:
+            pj = []
+            for rule in rules:
+                pj.append(self._schedule(pred, [tuple(t) for t in rule], "necessary", slots, pending))
+                if checkpoints is not None:
+                    checkpoints.append(StateCheckpoint())
+            jobs.append(pj)
         t_sched = time.perf_counter() - t0
         self._run(slots)
         self.last_batch_stats["schedule_s"] = t_sched
-        out = []
         minimizer = self.model.is_minimizer()
-        for pt_idx, key in jobs:
-            base = self._base_result(key, slots, pending)
-            pt = slots[pt_idx].result
-            rank_worsening = pt["target_rank"] - base["target_rank"]
-            if minimizer:
-                score_worsening = pt["target_score"] - base["target_score"]
-            else:
-                score_worsening = base["target_score"] - pt["target_score"]
-            # int64 tensor + python float -> float32 tensor (A-Q5)
-            out.append(float(np.float32(np.float32(rank_worsening) + np.float32(_sigmoid(score_worsening)))))
-        self.last_results = [(slots[i].result, self.base_pt_results[k]) for i, k in jobs]
-        return out
+        outs = []
+        self.last_results = []
+        for pj in jobs:
+            out = []
+            for pt_idx, key in pj:
+                base = self._base_result(key, slots, pending)
+                pt = slots[pt_idx].result
+                rank_worsening = pt["target_rank"] - base["target_rank"]
+                if minimizer:
+                    score_worsening = pt["target_score"] - base["target_score"]
+                else:
+                    score_worsening = base["target_score"] - pt["target_score"]
+                # int64 tensor + python float -> float32 tensor (A-Q5)
+                out.append(float(np.float32(np.float32(rank_worsening) + np.float32(_sigmoid(score_worsening)))))
+                self.last_results.append((pt, base))
+            outs.append(out)
+        return outs
 
 
 class SufficientPostTrainingEngine(PostTrainingEngine):
@@ -226,41 +237,51 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
         self.entities_to_convert = []
 
     def compute_relevance_batch(self, pred, rules, checkpoints: list | None = None):
-        pred = tuple(int(v) for v in pred)
-        s = pred[0]
-        if not self.entities_to_convert:
-            raise ZeroDivisionError("division by zero")  # sum([]) / len([]) in the reference
+        return self.compute_relevance_multi([(pred, rules, self.entities_to_convert)], checkpoints)[0]
+
+    def compute_relevance_multi(self, items, checkpoints: list | None = None):
+        """[(pred, rules, entities_to_convert), ...] in ONE device batch."""
         slots, pending, jobs = [], {}, []
         t0 = time.perf_counter()
-        for rule in rules:
-            rj = []
-            for e in self.entities_to_convert:
-                crule = Dataset.replace_entity_in_triples([tuple(t) for t in rule], s, e)
-                cpred = Dataset.replace_entity_in_triple(pred, s, e)
-                rj.append(self._schedule(cpred, crule, "sufficient", slots, pending))
-            jobs.append(rj)
-            if checkpoints is not None:
-                checkpoints.append(StateCheckpoint())
+        for pred, rules, ents in items:
+            pred = tuple(int(v) for v in pred)
+            s = pred[0]
+            if not ents:
+                raise ZeroDivisionError("division by zero")  # sum([]) / len([]) in the reference
+            pj = []
+            for rule in rules:
+                rj = []
+                for e in ents:
+                    crule = Dataset.replace_entity_in_triples([tuple(t) for t in rule], s, e)
+                    cpred = Dataset.replace_entity_in_triple(pred, s, e)
+                    rj.append(self._schedule(cpred, crule, "sufficient", slots, pending))
+                pj.append(rj)
+                if checkpoints is not None:
+                    checkpoints.append(StateCheckpoint())
+            jobs.append(pj)
         t_sched = time.perf_counter() - t0
         self._run(slots)
         self.last_batch_stats["schedule_s"] = t_sched
         minimizer = self.model.is_minimizer()
-        out = []
+        outs = []
         self.last_results = []
-        for rj in jobs:
-            rels = []
-            self.last_results.append([(slots[i].result, self.base_pt_results.get(k) or slots[pending[k]].result)
-                                      for i, k in rj])
-            for pt_idx, key in rj:
-                base = self._base_result(key, slots, pending)
-                pt = slots[pt_idx].result
-                rank_improvement = base["target_rank"] - pt["target_rank"]
-                if minimizer:
-                    score_improvement = base["target_score"] - pt["target_score"]
-                else:
-                    score_improvement = pt["target_score"] - base["target_score"]
-                rel = float(np.float32(np.float32(rank_improvement) + np.float32(_sigmoid(score_improvement))))
-                rel /= float(base["target_rank"])
-                rels.append(rel)
-            out.append(sum(rels) / len(rels))
-        return out
+        for pj in jobs:
+            out = []
+            for rj in pj:
+                rels, det = [], []
+                for pt_idx, key in rj:
+                    base = self._base_result(key, slots, pending)
+                    pt = slots[pt_idx].result
+                    det.append((pt, base))
+                    rank_improvement = base["target_rank"] - pt["target_rank"]
+                    if minimizer:
+                        score_improvement = base["target_score"] - pt["target_score"]
+                    else:
+                        score_improvement = pt["target_score"] - base["target_score"]
+                    rel = float(np.float32(np.float32(rank_improvement) + np.float32(_sigmoid(score_improvement))))
+                    rel /= float(base["target_rank"])
+                    rels.append(rel)
+                self.last_results.append(det)
+                out.append(sum(rels) / len(rels))
+            outs.append(out)
+        return outs
