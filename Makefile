@@ -4,7 +4,7 @@ ARCH ?= gfx950
 SRC := $(wildcard kelpie_amd/csrc/*.hip)
 OBJ := $(patsubst kelpie_amd/csrc/%.hip,build/%.o,$(SRC))
 FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
-         -Wno-unused-result -Iinclude
+         -Wno-unused-result -Iinclude -Xarch_host -mavx2
 LIB := kelpie_amd/libkelpie_hip.so
 
 all: $(LIB)

@@ -166,6 +166,22 @@ int kp_mt19937_discard(uint8_t* state, size_t state_len, uint64_t n);
  * (conve.py:151 via model.py:114-125, Dropout stays in train mode). */
 int kp_rng_bernoulli_bits(uint8_t* state, size_t state_len, uint64_t n, double p, uint32_t* out_bits);
 
+/* One TransE post-training's draws (pairwise_ranking_optimizer.py:166-172) for
+ * `epochs` epochs over R rows, from the two process-global generators the
+ * reference uses: per epoch np.random.shuffle of the rows (numpy's legacy
+ * MT19937 state: key[624] and *pos, from np.random.get_state()), then
+ * torch.randint(n_entities, ratio*R) and torch.randint(2, ratio*R) on the torch
+ * CPU generator.  Writes per epoch [row order (R) | entity (R) | head_or_tail (R)]
+ * (only the first R of the ratio*R draws are stepped) and advances both states. */
+int kp_rng_transe_epochs(uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos, int32_t R,
+                         int32_t epochs, int32_t ratio, int64_t n_entities, int32_t* out);
+
+/* ConvE hidden-dropout keep bits for n_steps steps of rows_per_step[i] x dim
+ * (torch.empty(b, dim).bernoulli_(keep) each), each step starting on a fresh
+ * 32-bit word; advances the torch state. */
+int kp_rng_conve_masks(uint8_t* torch_state, size_t torch_len, int32_t n_steps, const int32_t* rows_per_step,
+                       int32_t dim, double keep, uint32_t* out_words);
+
 /* Device time of the last kp_posttrain_rank (HIP events on the context's
  * stream): the whole call, the summed durations of its dominant kernel's
  * launches, their count, and the work units those launches processed

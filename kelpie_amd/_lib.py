@@ -18,7 +18,8 @@ KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
 
 # symbols declared by include/kelpie_hip.h
 EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_rank", "kp_all_scores",
-           "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits"]
+           "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
+           "kp_rng_transe_epochs", "kp_rng_conve_masks"]
 
 
 class ModelDesc(C.Structure):
@@ -64,6 +65,10 @@ def lib():
                                      C.c_void_p, C.c_void_p]
         L.kp_mt19937_discard.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         L.kp_rng_bernoulli_bits.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_double, C.c_void_p]
+        L.kp_rng_transe_epochs.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                           C.c_int32, C.c_int64, C.c_void_p]
+        L.kp_rng_conve_masks.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_int32, C.c_double,
+                                         C.c_void_p]
         L.kp_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                      C.POINTER(C.c_int64), C.POINTER(C.c_double)]
         L.kp_version.restype = C.c_char_p
@@ -93,6 +98,23 @@ def bernoulli_bits(state: np.ndarray, n: int, p: float) -> np.ndarray:
     words = np.zeros((n + 31) // 32, dtype=np.uint32)
     check(lib().kp_rng_bernoulli_bits(_ptr(state), state.size, int(n), float(p), _ptr(words)))
     return words
+
+
+def transe_epochs(torch_state: np.ndarray, np_key: np.ndarray, np_pos: np.ndarray, R: int, epochs: int,
+                  ratio: int, n_entities: int) -> np.ndarray:
+    out = np.zeros(max(1, epochs * 3 * R), np.int32)
+    check(lib().kp_rng_transe_epochs(_ptr(torch_state), torch_state.size, _ptr(np_key), _ptr(np_pos), int(R),
+                                     int(epochs), int(ratio), int(n_entities), _ptr(out)))
+    return out[:epochs * 3 * R]
+
+
+def conve_masks(torch_state: np.ndarray, rows_per_step, dim: int, keep: float) -> np.ndarray:
+    rows = np.ascontiguousarray(rows_per_step, dtype=np.int32)
+    words = int(sum((int(b) * dim + 31) // 32 for b in rows))
+    out = np.zeros(max(1, words), np.uint32)
+    check(lib().kp_rng_conve_masks(_ptr(torch_state), torch_state.size, len(rows), _ptr(rows), int(dim),
+                                   float(keep), _ptr(out)))
+    return out[:words]
 
 
 class Context:

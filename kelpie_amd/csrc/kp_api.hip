@@ -207,33 +207,151 @@ struct Mt {
   }
   void twist() {
     constexpr int N = 624, M = 397;
-    int i = 0;
-    for (; i < N - M; ++i) {
-      uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
-      s[i] = s[i + M] ^ (y >> 1) ^ ((s[i + 1] & 1u) ? 0x9908b0dfu : 0u);
+    // three dependency-free spans (distance >= N-M), written so the host
+    // compiler vectorises them
+#pragma clang loop vectorize(enable)
+    for (int i = 0; i < N - M; ++i) {
+      const uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
+      s[i] = s[i + M] ^ (y >> 1) ^ ((0u - (s[i + 1] & 1u)) & 0x9908b0dfu);
     }
-    for (; i < N - 1; ++i) {
-      uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
-      s[i] = s[i + M - N] ^ (y >> 1) ^ ((s[i + 1] & 1u) ? 0x9908b0dfu : 0u);
+#pragma clang loop vectorize(enable)
+    for (int i = N - M; i < N - 1; ++i) {
+      const uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
+      s[i] = s[i + M - N] ^ (y >> 1) ^ ((0u - (s[i + 1] & 1u)) & 0x9908b0dfu);
     }
-    uint32_t y = (s[N - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
-    s[N - 1] = s[M - 1] ^ (y >> 1) ^ ((s[0] & 1u) ? 0x9908b0dfu : 0u);
+    const uint32_t y = (s[N - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
+    s[N - 1] = s[M - 1] ^ (y >> 1) ^ ((0u - (s[0] & 1u)) & 0x9908b0dfu);
   }
-  uint32_t operator()() {
+  // tempered copy of the current block, refreshed after every twist
+  uint32_t tb[624];
+  bool tb_ok = false;
+  void temper_block() {
+#pragma clang loop vectorize(enable)
+    for (int i = 0; i < 624; ++i) {
+      uint32_t y = s[i];
+      y ^= (y >> 11);
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= (y >> 18);
+      tb[i] = y;
+    }
+    tb_ok = true;
+  }
+  // advance by n outputs (operator() semantics, nothing tempered)
+  void skip(uint64_t n) {
+    while (n > 0) {
+      const uint64_t k = std::min<uint64_t>(n, (uint64_t)(left - 1));
+      left -= (int32_t)k;
+      next += k;
+      n -= k;
+      if (n > 0) {
+        twist();
+        tb_ok = false;
+        left = 624;
+        next = 1;
+        n -= 1;
+      }
+    }
+  }
+  inline uint32_t operator()() {
     if (--left == 0) {
       twist();
       left = 624;
       next = 0;
+      tb_ok = false;
     }
-    uint32_t y = s[next++];
+    if (!tb_ok) temper_block();
+    return tb[next++];
+  }
+};
+}  // namespace
+
+// numpy's legacy MT19937 (numpy/random/src/mt19937): pos in [0, 624], regenerate at 624
+struct NpMt {
+  uint32_t* key;
+  int32_t* pos;
+  Mt core;  // reuse the twist
+  uint32_t next32() {
+    if (*pos >= 624) {
+      std::memcpy(core.s, key, sizeof(core.s));
+      core.twist();
+      std::memcpy(key, core.s, sizeof(core.s));
+      *pos = 0;
+    }
+    uint32_t y = key[(*pos)++];
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     return y;
   }
+  // numpy/random/src/distributions: random_interval (max <= 0xffffffff)
+  uint32_t interval(uint32_t max) {
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (next32() & mask)) > max) {
+    }
+    return v;
+  }
 };
-}  // namespace
+
+int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs,
+                         int32_t ratio, int64_t n_entities, int32_t* out) {
+  if (!ts || tlen < 24 + 624 * 8 || !np_key || !np_pos || R < 0 || epochs < 0 || ratio < 1 || n_entities < 1 ||
+      n_entities >= (1LL << 32) || (R > 0 && epochs > 0 && !out))
+    return KP_EINVAL;
+  Mt mt;
+  mt.load(ts);
+  NpMt np{np_key, np_pos, {}};
+  std::vector<int32_t> idx(R);
+  for (int i = 0; i < R; ++i) idx[i] = i;
+  const uint64_t n = (uint64_t)ratio * (uint64_t)R;
+  for (int e = 0; e < epochs; ++e) {
+    for (int i = R - 1; i >= 1; --i) {  // np.random.shuffle: for i in reversed(range(1, n))
+      const uint32_t j = np.interval((uint32_t)i);
+      std::swap(idx[i], idx[j]);
+    }
+    int32_t* o = out + (size_t)e * 3 * R;
+    std::memcpy(o, idx.data(), sizeof(int32_t) * R);
+    // randint(high=N): random() % N; only the first R values are stepped, the
+    // other (ratio-1)*R draws are skipped without tempering
+    for (int k = 0; k < R; ++k) o[R + k] = (int32_t)(mt() % (uint32_t)n_entities);
+    mt.skip(n - (uint64_t)R);
+    for (int k = 0; k < R; ++k) o[2 * R + k] = (int32_t)(mt() & 1u);  // randint(high=2)
+    mt.skip(n - (uint64_t)R);
+  }
+  mt.store(ts);
+  return KP_OK;
+}
+
+int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim, double keep,
+                       uint32_t* out) {
+  if (!ts || tlen < 24 + 624 * 8 || n_steps < 0 || dim <= 0 || (n_steps > 0 && (!rows || !out))) return KP_EINVAL;
+  Mt mt;
+  mt.load(ts);
+  const uint64_t mask53 = (1ULL << 53) - 1;
+  const double scale = std::ldexp(1.0, -53);
+  size_t w0 = 0;
+  for (int st = 0; st < n_steps; ++st) {
+    const uint64_t n = (uint64_t)rows[st] * (uint64_t)dim;
+    const size_t nw = (size_t)((n + 31) / 32);
+    for (size_t w = 0; w < nw; ++w) out[w0 + w] = 0u;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t hi = mt(), lo = mt();
+      const double u = (double)(((hi << 32) | lo) & mask53) * scale;
+      if (u < keep) out[w0 + (i >> 5)] |= 1u << (i & 31);
+    }
+    w0 += nw;  // u = m * 2^-53 is exact, so this is ATen's uniform < p test bit for bit
+  }
+  mt.store(ts);
+  return KP_OK;
+}
 
 int kp_rng_bernoulli_bits(uint8_t* st, size_t len, uint64_t n, double p, uint32_t* out) {
   if (!st || len < 24 + 624 * 8 || (n > 0 && !out)) return KP_EINVAL;
@@ -256,19 +374,7 @@ int kp_mt19937_discard(uint8_t* st, size_t len, uint64_t n) {
   if (!st || len < 24 + 624 * 8) return KP_EINVAL;
   Mt mt;
   mt.load(st);
-  // operator() semantics: --left == 0 -> twist, left = 624, next = 0; then next++
-  while (n > 0) {
-    uint64_t k = std::min<uint64_t>(n, (uint64_t)(mt.left - 1));
-    mt.left -= (int32_t)k;
-    mt.next += k;
-    n -= k;
-    if (n > 0) {
-      mt.twist();
-      mt.left = 624;
-      mt.next = 1;
-      n -= 1;
-    }
-  }
+  mt.skip(n);
   mt.store(st);
   return KP_OK;
 }

@@ -79,27 +79,27 @@ class ReferenceRNG:
         """Per epoch [row order (R) | negative entity (R) | head_or_tail (R)].
 
         The row order composes the in-place ``np.random.shuffle`` of every epoch;
-        of the ``ratio*R`` randint draws only the first R are stepped (SURVEY A-Q2)."""
-        out = np.zeros((epochs, 3, R), np.int32)
-        idx = np.arange(R, dtype=np.int64)
-        n = ratio * R
-        for e in range(epochs):
-            np.random.shuffle(idx)
-            ents = torch.randint(high=n_entities, size=(n,))
-            hot = torch.randint(high=2, size=(n,))
-            out[e, 0] = idx
-            out[e, 1] = ents[:R].numpy()
-            out[e, 2] = hot[:R].numpy()
-        return out.reshape(-1)
+        of the ``ratio*R`` randint draws only the first R are stepped (SURVEY A-Q2).
+        Generated in C++ from the two generators' states (kp_rng_transe_epochs)."""
+        if epochs <= 0:
+            return np.zeros(0, np.int32)
+        st = _get_state()
+        name, key, pos, has_gauss, cached = np.random.get_state()
+        key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+        posa = np.array([pos], dtype=np.int32)
+        out = _lib.transe_epochs(st, key, posa, R, epochs, ratio, n_entities)
+        np.random.set_state((name, key, int(posa[0]), has_gauss, cached))
+        _set_state(st)
+        return out
 
     def conve_masks(self, n_rows_per_step, dim: int, p_drop: float) -> np.ndarray:
         """Hidden-dropout keep bits for every step, packed per step in uint32 words."""
-        if p_drop <= 0.0:
+        if p_drop <= 0.0 or len(n_rows_per_step) == 0:
             return np.zeros(0, np.int32)
         st = _get_state()
-        chunks = [_lib.bernoulli_bits(st, int(b) * dim, 1.0 - p_drop) for b in n_rows_per_step]
+        words = _lib.conve_masks(st, n_rows_per_step, dim, 1.0 - p_drop)
         _set_state(st)
-        return np.concatenate(chunks).view(np.int32) if chunks else np.zeros(0, np.int32)
+        return words.view(np.int32)
 
 
 class StateCheckpoint:

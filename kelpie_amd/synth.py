@@ -117,8 +117,12 @@ def make_weights(model: str, n_ent: int, n_rel: int, dim: int, seed: int = 0,
         return {"entity_embeddings": (rng.random((n_ent, D)) * init_scale).astype(np.float32),
                 "relation_embeddings": (rng.random((R2, D)) * init_scale).astype(np.float32)}
     if model == "ConvE":
-        w = {"entity_embeddings": xavier_normal(rng, n_ent, dim),
-             "relation_embeddings": xavier_normal(rng, R2, dim)}
+        if trained_scale:
+            w = {"entity_embeddings": (rng.standard_normal((n_ent, dim)) * trained_scale).astype(np.float32),
+                 "relation_embeddings": (rng.standard_normal((R2, dim)) * trained_scale).astype(np.float32)}
+        else:
+            w = {"entity_embeddings": xavier_normal(rng, n_ent, dim),
+                 "relation_embeddings": xavier_normal(rng, R2, dim)}
         h = dim // 20
         hid = 32 * (2 * 20 - 2) * (h - 2)
         # torch default init for Conv2d(1,32,3) / Linear(hid, dim): U(-1/sqrt(fan_in), ..)

@@ -115,6 +115,45 @@ def test_transe_vs_oracle_full_width(dim):
     assert match == len(out["cpu"]), f"rank match {match}/{len(out['cpu'])}"
 
 
+CV_HP = {"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.995, "epochs": 25}
+
+
+@pytest.mark.parametrize("dim,p_drop", [(200, 0.2), (60, 0.0)])
+def test_conve_vs_oracle_full_width(dim, p_drop):
+    """d = 200 (the production 20x10 image, FC 9728 -> 200) on a 2,000-entity graph."""
+    from cpu_backend import OracleBackedContext
+    from kelpie_amd import synth
+    g = synth.make_graph("small", seed=9)
+    ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    w = synth.make_weights("ConvE", g.num_entities, g.num_relations, dim, seed=9, conve_random_bn=True,
+                           trained_scale=0.5)
+    deg = ds.entity_to_degree
+    test = [tuple(int(v) for v in t) for t in g.test]
+    preds = [t for t in test if 8 <= deg.get(t[0], 0) <= 40][:2]
+    bn = {i: {"weight": w[f"bn{i}_weight"], "bias": w[f"bn{i}_bias"], "running_mean": w[f"bn{i}_mean"],
+              "running_var": w[f"bn{i}_var"]} for i in (1, 2, 3)}
+    out = {}
+    for backend in ("gpu", "cpu"):
+        model = ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
+                         w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn, hidden_dropout_rate=p_drop)
+        if backend == "cpu":
+            model._ctx = OracleBackedContext(model)
+        seed_all(42)
+        eng = ka.NecessaryPostTrainingEngine(model, ds, CV_HP)
+        res = []
+        for pred in preds:
+            eng.set_cache()
+            cands = sorted(ds.entity_to_training_triples[pred[0]])[:3]
+            eng.compute_relevance_batch(pred, [[c] for c in cands])
+            res += [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+                    for pt, b in eng.last_results]
+        out[backend] = res
+    match = sum(int(a[0] == b[0] and a[2] == b[2]) for a, b in zip(out["gpu"], out["cpu"]))
+    for a, b in zip(out["gpu"], out["cpu"]):
+        assert abs(a[1] - b[1]) <= 1e-4 * max(1.0, abs(b[1])), (a, b)
+    assert match == len(out["cpu"]), f"rank match {match}/{len(out['cpu'])}: {out}"
+
+
 def test_complex_all_scores_matches_fp32_reference():
     g, ds, w = _small_complex(dim=200)
     model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"])

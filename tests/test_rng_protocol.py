@@ -74,3 +74,20 @@ def test_transe_epochs_match_reference_calls():
         assert np.array_equal(ents[:R].numpy(), blob[e, 1])
         assert np.array_equal(hot[:R].numpy(), blob[e, 2])
     assert torch.equal(torch.rand(2), after)
+
+
+def test_conve_masks_match_torch_dropout_sequence():
+    rng = ReferenceRNG()
+    steps = [3, 7, 1]
+    torch.manual_seed(21)
+    words = rng.conve_masks(steps, 20, 0.2)
+    after = torch.rand(2)
+    torch.manual_seed(21)
+    off = 0
+    for b in steps:
+        m = torch.empty(b, 20).bernoulli_(0.8).numpy().reshape(-1).astype(np.uint8)
+        nw = (b * 20 + 31) // 32
+        got = np.unpackbits(words[off:off + nw].view(np.uint32).view(np.uint8), bitorder="little")[:b * 20]
+        assert np.array_equal(got, m)
+        off += nw
+    assert torch.equal(torch.rand(2), after)
