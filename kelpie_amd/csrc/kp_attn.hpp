@@ -46,7 +46,7 @@ enum { ATT_SOFTMAX_O = 0, ATT_SOFTMAX = 1, ATT_BCE_O = 2 };
 
 template <int DB, int MODE>
 __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, int n_ent, int half,
-                                                  const int2* __restrict__ qdesc,
+                                                  const int4* __restrict__ qdesc,
                                                   const float* __restrict__ X,
                                                   const float* __restrict__ R,
                                                   const float* __restrict__ Qpre, int nq,
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
   float gsc = 0.f;
   if (MODE == ATT_BCE_O) gsc = valid ? qscale[q] : 0.f;
   if (MODE == ATT_SOFTMAX_O) {
-    int2 sr = valid ? qdesc[q] : make_int2(0, 0);
+    const int4 sr = valid ? qdesc[q] : make_int4(0, 0, 0, 0);
     const float* x = X + (size_t)sr.x * DP;
     const float* r = R + (size_t)sr.y * DP;
 #pragma unroll
@@ -138,15 +138,17 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
     const float* Es = lds + (t & 1) * (KT * S);
     const int k0 = key_begin + t * KT;
     // ---- S^T tile: s[r] = q_c . E[k0 + 4g + r]
-    f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // two independent accumulation chains (dependent-issue latency 40 > 32 cycles)
+    f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, s2 = s;
 #pragma unroll
     for (int j = 0; j < DB; ++j) {
       float4 a = *reinterpret_cast<const float4*>(Es + c * S + 16 * j + 4 * g);
       s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, qv[j][0], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, qv[j][1], s, 0, 0, 0);
+      s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, qv[j][1], s2, 0, 0, 0);
       s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, qv[j][2], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, qv[j][3], s, 0, 0, 0);
+      s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, qv[j][3], s2, 0, 0, 0);
     }
+    s += s2;
     if (MODE == ATT_BCE_O) {
       float p[4];
 #pragma unroll

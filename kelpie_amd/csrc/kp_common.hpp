@@ -85,7 +85,7 @@ struct kp_ctx {
   float* d_bn_a = nullptr;
   float* d_bn_b = nullptr;
   std::vector<float> hE;     // host copy (ConvE/TransE helpers)
-  DevBuf ws[24];             // workspace slots (see each model file)
+  DevBuf ws[32];             // workspace slots (see each model file)
   std::string err;
   Timing timing;
   bool time_hot = true;

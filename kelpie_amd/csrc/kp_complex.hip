@@ -81,149 +81,119 @@ struct CxOpt {
   float reg_w;
 };
 
-#define UPD_CHUNK 64
 #define UPD_MAXSPLIT 16
 
+// One wave per (query or frozen-head row) of this step: its contribution to the
+// kelpie row's gradient (un-normalised by the batch size).
+//   query (kelpie-head rows sharing relation r, count c, kelpie targets ck):
+//     J_r^T (c <E> - Tsum - ck x) + (c p_k - ck) q,   <E> = softmax-weighted entity
+//     (frozen part sum_sp w_sp O_sp merged with the kelpie column p_k x)
+//   frozen-head row pair (count c, target = kelpie):  c (p_k - 1) q_pair
+template <int DP>
+__global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __restrict__ stepq, int nq,
+                                                     const int4* __restrict__ stept, int nt,
+                                                     const CxQuery* __restrict__ pq, const float* __restrict__ X,
+                                                     const float* __restrict__ R, const float* __restrict__ Tsum,
+                                                     const float* __restrict__ Qpair, const float* __restrict__ lsef,
+                                                     const float* __restrict__ att_m, const float* __restrict__ att_l,
+                                                     const float* __restrict__ att_O, int n_split,
+                                                     float* __restrict__ contrib) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= nq + nt) return;
+  float* out = contrib + (size_t)item * DP;
+  if (item < nq) {
+    const int4 sq = stepq[item];  // slot, rel, plan-query index
+    const float* x = X + (size_t)sq.x * DP;
+    const float* rel = R + (size_t)sq.y * DP;
+    const CxQuery Q = pq[sq.z];
+    float z = 0.f;
+    for (int d = lane; d < 2 * half; d += 64) z += cx_q(x, rel, d, half) * x[d];
+    z = wave_sum(z);
+    float mm = kNegInf;
+    for (int sp = 0; sp < n_split; ++sp) mm = fmaxf(mm, att_m[(size_t)sp * nq + item]);
+    float ll = 0.f;
+    for (int sp = 0; sp < n_split; ++sp) {
+      const float ms = att_m[(size_t)sp * nq + item];
+      ll += (ms == kNegInf) ? 0.f : att_l[(size_t)sp * nq + item] * __expf(ms - mm);
+    }
+    const float lse_f = mm + __logf(ll);
+    const float hi = fmaxf(lse_f, z), lo = fminf(lse_f, z);
+    const float lse = hi + log1pf(__expf(lo - hi));
+    const float pk = __expf(z - lse);
+    float wsp[UPD_MAXSPLIT];
+#pragma unroll
+    for (int sp = 0; sp < UPD_MAXSPLIT; ++sp) {
+      float ms = (sp < n_split) ? att_m[(size_t)sp * nq + item] : kNegInf;
+      wsp[sp] = (ms == kNegInf) ? 0.f : __expf(ms - lse);
+    }
+    const float fc = (float)Q.c, fck = (float)Q.ck;
+    const float cf = fc * pk - fck;
+    const float* ts = Tsum + (size_t)sq.z * DP;
+    for (int i = lane; i < half; i += 64) {
+      const float a = x[i], b = x[i + half];
+      const float cc = rel[i], ee = rel[i + half];
+      float ore = 0.f, oim = 0.f;
+#pragma unroll
+      for (int sp = 0; sp < UPD_MAXSPLIT; ++sp) {
+        if (sp < n_split) {
+          const float* Op = att_O + ((size_t)sp * nq + item) * DP;
+          ore += wsp[sp] * Op[i];
+          oim += wsp[sp] * Op[i + half];
+        }
+      }
+      const float ere = ore + pk * a, eim = oim + pk * b;
+      const float dre = fc * ere - ts[i] - fck * a;
+      const float dim_ = fc * eim - ts[i + half] - fck * b;
+      const float qre = a * cc - b * ee, qim = a * ee + b * cc;
+      out[i] = dre * cc + dim_ * ee + cf * qre;
+      out[i + half] = -dre * ee + dim_ * cc + cf * qim;
+    }
+  } else {
+    const int4 st = stept[item - nq];  // slot, pair, count
+    const float* x = X + (size_t)st.x * DP;
+    const float* qp = Qpair + (size_t)st.y * DP;
+    float z = 0.f;
+    for (int d = lane; d < 2 * half; d += 64) z += qp[d] * x[d];
+    z = wave_sum(z);
+    const float lf = lsef[st.y];
+    const float hi = fmaxf(lf, z), lo = fminf(lf, z);
+    const float lse = hi + log1pf(__expf(lo - hi));
+    const float coef = (float)st.z * (__expf(z - lse) - 1.0f);
+    for (int d = lane; d < 2 * half; d += 64) out[d] = coef * qp[d];
+  }
+}
+
+// Sum a slot's contributions, add the N3 term, apply the optimizer (torch op order).
 template <int DP>
 __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __restrict__ act,
-                                                    const CxPlan* __restrict__ plans,
-                                                    const CxQuery* __restrict__ pq,
-                                                    const CxTail* __restrict__ pt,
-                                                    const float* __restrict__ R,
-                                                    const float* __restrict__ Tsum,
-                                                    const float* __restrict__ Qpair,
-                                                    const float* __restrict__ lsef,
-                                                    const float* __restrict__ att_m,
-                                                    const float* __restrict__ att_l,
-                                                    const float* __restrict__ att_O, int nq_step,
-                                                    int n_split, float* __restrict__ X,
-                                                    float* __restrict__ S1, float* __restrict__ S2,
-                                                    CxOpt opt) {
-  __shared__ __attribute__((aligned(16))) float xs[DP];
-  __shared__ float s_pk[UPD_CHUNK];
-  __shared__ float s_cf[UPD_CHUNK];
-  __shared__ float s_w[UPD_CHUNK][UPD_MAXSPLIT];
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int4 a4 = act[blockIdx.x];
+                                                    const CxPlan* __restrict__ plans, int nq,
+                                                    const float* __restrict__ contrib, float* __restrict__ X,
+                                                    float* __restrict__ S1, float* __restrict__ S2, CxOpt opt) {
+  const int tid = threadIdx.x;
+  const int4 a4 = act[blockIdx.x];  // slot, plan, qoff, toff
   const int slot = a4.x;
   const CxPlan P = plans[a4.y];
-  const int qoff = a4.z;
   float* x = X + (size_t)slot * DP;
-  for (int d = tid; d < DP; d += 256) xs[d] = x[d];
-  __syncthreads();
-
-  constexpr int PER = (DP / 2 + 255) / 256 > 0 ? (DP / 2 + 255) / 256 : 1;
-  float gre[PER], gim[PER];
-#pragma unroll
-  for (int u = 0; u < PER; ++u) gre[u] = gim[u] = 0.f;
-
-  // ---------------- kelpie-head queries
-  for (int c0 = 0; c0 < P.q_count; c0 += UPD_CHUNK) {
-    const int cn = min(UPD_CHUNK, P.q_count - c0);
-    for (int j = w; j < cn; j += 4) {
-      const CxQuery Q = pq[P.q_begin + c0 + j];
-      const float* rel = R + (size_t)Q.rel * DP;
-      float z = 0.f;
-      for (int d = lane; d < 2 * half; d += 64) z += cx_q(xs, rel, d, half) * xs[d];
-      z = wave_sum(z);
-      const int qi = qoff + c0 + j;
-      float mm = kNegInf;
-      for (int sp = 0; sp < n_split; ++sp) mm = fmaxf(mm, att_m[(size_t)sp * nq_step + qi]);
-      float ll = 0.f;
-      for (int sp = 0; sp < n_split; ++sp) {
-        float ms = att_m[(size_t)sp * nq_step + qi];
-        ll += (ms == kNegInf) ? 0.f : att_l[(size_t)sp * nq_step + qi] * __expf(ms - mm);
-      }
-      const float lse_f = mm + __logf(ll);
-      const float hi = fmaxf(lse_f, z), lo = fminf(lse_f, z);
-      const float lse = hi + log1pf(__expf(lo - hi));
-      if (lane == 0) {
-        const float pk = __expf(z - lse);
-        s_pk[j] = pk;
-        s_cf[j] = (float)Q.c * pk - (float)Q.ck;
-      }
-      if (lane < n_split) {
-        float ms = att_m[(size_t)lane * nq_step + qi];
-        s_w[j][lane] = (ms == kNegInf) ? 0.f : __expf(ms - lse);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int i = tid + 256 * u;
-      if (i < half) {
-        const float a = xs[i], b = xs[i + half];
-        float accr = gre[u], acci = gim[u];
-        for (int j = 0; j < cn; ++j) {
-          const CxQuery Q = pq[P.q_begin + c0 + j];
-          const int qi = qoff + c0 + j;
-          const float cc = R[(size_t)Q.rel * DP + i], ee = R[(size_t)Q.rel * DP + i + half];
-          float ore = 0.f, oim = 0.f;
-          for (int sp = 0; sp < n_split; ++sp) {
-            const float* Op = att_O + ((size_t)sp * nq_step + qi) * DP;
-            ore += s_w[j][sp] * Op[i];
-            oim += s_w[j][sp] * Op[i + half];
-          }
-          const float pk = s_pk[j];
-          const float ere = ore + pk * a, eim = oim + pk * b;
-          const float* ts = Tsum + (size_t)(P.q_begin + c0 + j) * DP;
-          const float fc = (float)Q.c, fck = (float)Q.ck;
-          const float dre = fc * ere - ts[i] - fck * a;
-          const float dim_ = fc * eim - ts[i + half] - fck * b;
-          const float qre = a * cc - b * ee, qim = a * ee + b * cc;
-          const float cf = s_cf[j];
-          accr += dre * cc + dim_ * ee + cf * qre;
-          acci += -dre * ee + dim_ * cc + cf * qim;
-        }
-        gre[u] = accr;
-        gim[u] = acci;
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---------------- frozen-head rows (target = kelpie)
-  for (int c0 = 0; c0 < P.t_count; c0 += UPD_CHUNK) {
-    const int cn = min(UPD_CHUNK, P.t_count - c0);
-    for (int j = w; j < cn; j += 4) {
-      const CxTail T = pt[P.t_begin + c0 + j];
-      const float* qp = Qpair + (size_t)T.pair * DP;
-      float z = 0.f;
-      for (int d = lane; d < 2 * half; d += 64) z += qp[d] * xs[d];
-      z = wave_sum(z);
-      const float lf = lsef[T.pair];
-      const float hi = fmaxf(lf, z), lo = fminf(lf, z);
-      const float lse = hi + log1pf(__expf(lo - hi));
-      if (lane == 0) s_cf[j] = (float)T.c * (__expf(z - lse) - 1.0f);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int i = tid + 256 * u;
-      if (i < half) {
-        float accr = gre[u], acci = gim[u];
-        for (int j = 0; j < cn; ++j) {
-          const CxTail T = pt[P.t_begin + c0 + j];
-          const float* qp = Qpair + (size_t)T.pair * DP;
-          accr += s_cf[j] * qp[i];
-          acci += s_cf[j] * qp[i + half];
-        }
-        gre[u] = accr;
-        gim[u] = acci;
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---------------- regulariser, optimizer
   const float inv_b = 1.0f / (float)P.b;
 #pragma unroll
-  for (int u = 0; u < PER; ++u) {
+  for (int u = 0; u < (DP / 2 + 255) / 256; ++u) {
     const int i = tid + 256 * u;
     if (i >= half) continue;
-    float gv[2] = {gre[u] * inv_b, gim[u] * inv_b};
-    const float a = xs[i], b = xs[i + half];
+    float gv[2] = {0.f, 0.f};
+    for (int j = 0; j < P.q_count; ++j) {
+      const float* cq = contrib + (size_t)(a4.z + j) * DP;
+      gv[0] += cq[i];
+      gv[1] += cq[i + half];
+    }
+    for (int j = 0; j < P.t_count; ++j) {
+      const float* ct = contrib + (size_t)(nq + a4.w + j) * DP;
+      gv[0] += ct[i];
+      gv[1] += ct[i + half];
+    }
+    gv[0] *= inv_b;
+    gv[1] *= inv_b;
+    const float a = x[i], b = x[i + half];
     if (opt.reg_w != 0.f) {
       const float mod = sqrtf(a * a + b * b);
       const float k3 = 3.0f * opt.reg_w * inv_b * (float)(P.cnt_l + P.cnt_r) * mod;
@@ -234,22 +204,23 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
     for (int h = 0; h < 2; ++h) {
       const int d = i + h * half;
       const float gd = gv[h];
-      float xd = xs[d];
+      float xd = h ? b : a;
+      const size_t o = (size_t)slot * DP + d;
       if (opt.kind == KP_OPT_ADAGRAD) {
-        float s1 = S1[(size_t)slot * DP + d];
+        float s1 = S1[o];
         s1 = s1 + gd * gd;
         const float stdv = sqrtf(s1) + opt.eps;
         xd = xd + (-opt.lr * gd) / stdv;
-        S1[(size_t)slot * DP + d] = s1;
+        S1[o] = s1;
       } else if (opt.kind == KP_OPT_ADAM) {
-        float m1 = S1[(size_t)slot * DP + d], v2 = S2[(size_t)slot * DP + d];
+        float m1 = S1[o], v2 = S2[o];
         m1 = m1 + opt.one_minus_b1 * (gd - m1);
         v2 = v2 * opt.b2;
         v2 = v2 + (opt.one_minus_b2 * gd) * gd;
         const float den = sqrtf(v2) / opt.bc2_sqrt + opt.eps;
         xd = xd + (-opt.step_size * m1) / den;
-        S1[(size_t)slot * DP + d] = m1;
-        S2[(size_t)slot * DP + d] = v2;
+        S1[o] = m1;
+        S2[o] = v2;
       } else {
         xd = xd + (-opt.lr) * gd;
       }
@@ -291,7 +262,7 @@ __global__ void kp_cx_scoreq(const float* __restrict__ E, const float* __restric
 // host side
 // ----------------------------------------------------------------------------
 template <int DB>
-void launch_attn(kp_ctx* c, bool with_o, const int2* qdesc, const float* X, const float* Qpre, int nq,
+void launch_attn(kp_ctx* c, bool with_o, const int4* qdesc, const float* X, const float* Qpre, int nq,
                  int n_split, float* m, float* l, float* O) {
   if (nq <= 0) return;
   const int keys_per_split = (c->n_ent + n_split - 1) / n_split;
@@ -309,12 +280,18 @@ void launch_attn(kp_ctx* c, bool with_o, const int2* qdesc, const float* X, cons
 
 template <int DB>
 void launch_update(kp_ctx* c, int n_act, const int4* act, const CxPlan* plans, const CxQuery* pq,
-                   const CxTail* pt, const float* tsum, const float* qpair, const float* lsef, const float* am,
-                   const float* al, const float* aO, int nq_step, int n_split, float* X, float* S1, float* S2,
-                   const CxOpt& opt) {
+                   const int4* stepq, int nq, const int4* stept, int nt, const float* tsum, const float* qpair,
+                   const float* lsef, const float* am, const float* al, const float* aO, int n_split, float* contrib,
+                   float* X, float* S1, float* S2, const CxOpt& opt) {
   if (n_act <= 0) return;
-  hipLaunchKernelGGL((kp_cx_update<16 * DB>), dim3(n_act), dim3(256), 0, c->stream, c->dim / 2, act, plans, pq, pt,
-                     c->dR, tsum, qpair, lsef, am, al, aO, nq_step, n_split, X, S1, S2, opt);
+  const int half = c->dim / 2;
+  if (nq + nt > 0) {
+    hipLaunchKernelGGL((kp_cx_contrib<16 * DB>), dim3((nq + nt + 3) / 4), dim3(256), 0, c->stream, half, stepq, nq,
+                       stept, nt, pq, X, c->dR, tsum, qpair, lsef, am, al, aO, n_split, contrib);
+    KP_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL((kp_cx_update<16 * DB>), dim3(n_act), dim3(256), 0, c->stream, half, act, plans, nq, contrib, X,
+                     S1, S2, opt);
   KP_HIP(hipGetLastError());
 }
 
@@ -489,27 +466,33 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   }
 
   // per-step active lists
-  std::vector<int> act_off(T + 1, 0), q_off(T + 1, 0);
+  std::vector<int> act_off(T + 1, 0), q_off(T + 1, 0), t_off(T + 1, 0);
   std::vector<int4> acts;
-  std::vector<int2> stepq;
-  int max_nq = 0;
+  std::vector<int4> stepq, stept;
+  int max_nq = 0, max_items = 0;
   for (int t = 0; t < T; ++t) {
     act_off[t] = (int)acts.size();
     q_off[t] = (int)stepq.size();
-    int qo = 0;
+    t_off[t] = (int)stept.size();
+    int qo = 0, to = 0;
     for (int s = 0; s < ns; ++s) {
       const int nst = nsteps[s];
       if (nst == 0 || t >= E * nst) continue;
       const int plan = plan_base[s] + (nst == 1 ? 0 : t);
-      acts.push_back(make_int4(s, plan, qo, 0));
+      acts.push_back(make_int4(s, plan, qo, to));
       const CxPlan& P = plans[plan];
-      for (int j = 0; j < P.q_count; ++j) stepq.push_back(make_int2(s, pqs[P.q_begin + j].rel));
+      for (int j = 0; j < P.q_count; ++j)
+        stepq.push_back(make_int4(s, pqs[P.q_begin + j].rel, P.q_begin + j, 0));
+      for (int j = 0; j < P.t_count; ++j) stept.push_back(make_int4(s, pts[P.t_begin + j].pair, pts[P.t_begin + j].c, 0));
       qo += P.q_count;
+      to += P.t_count;
     }
     max_nq = std::max(max_nq, qo);
+    max_items = std::max(max_items, qo + to);
   }
   act_off[T] = (int)acts.size();
   q_off[T] = (int)stepq.size();
+  t_off[T] = (int)stept.size();
 
   const int DP = c->dp;
   // ---- uploads
@@ -530,7 +513,10 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   int32_t* dTg = upload(c, c->ws[6], targets.data(), targets.size());
   int2* dPairs = upload(c, c->ws[7], pairs.data(), pairs.size());
   int4* dActs = upload(c, c->ws[8], acts.data(), acts.size());
-  int2* dStepQ = upload(c, c->ws[9], stepq.data(), stepq.size());
+  int4* dStepQ = upload(c, c->ws[9], stepq.data(), std::max<size_t>(1, stepq.size()));
+  DevBuf& bStepT = c->ws[24];
+  int4* dStepT = upload(c, bStepT, stept.data(), std::max<size_t>(1, stept.size()));
+  float* dContrib = reinterpret_cast<float*>(c->ws[25].ensure(sizeof(float) * (size_t)std::max(1, max_items) * DP));
   const int npq = (int)pqs.size(), npairs = (int)pairs.size();
   float* dTsum = reinterpret_cast<float*>(c->ws[10].ensure(sizeof(float) * (size_t)std::max(npq, 1) * DP));
   float* dQpair = reinterpret_cast<float*>(c->ws[11].ensure(sizeof(float) * (size_t)std::max(npairs, 1) * DP));
@@ -617,8 +603,9 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     const double step = (double)(t + 1);
     opt.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, step)));
     opt.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)hp->beta2, step));
-    CX_DISPATCH(DBV, launch_update<DB>(c, na, dActs + act_off[t], dPlans, dPq, dPt, dTsum, dQpair, dLsef, dAm, dAl,
-                                       dAO, nq, sp, dX, dS1, dS2, opt));
+    CX_DISPATCH(DBV, launch_update<DB>(c, na, dActs + act_off[t], dPlans, dPq, dStepQ + q_off[t], nq,
+                                       dStepT + t_off[t], t_off[t + 1] - t_off[t], dTsum, dQpair, dLsef, dAm, dAl, dAO,
+                                       sp, dContrib, dX, dS1, dS2, opt));
   }
   KP_HIP(hipEventRecord(h1, c->stream));
 
