@@ -27,63 +27,85 @@ __device__ __forceinline__ float cx_q(const float* __restrict__ lhs, const float
 }
 
 // ----------------------------------------------------------------------------
-// kp_cx_attn: per query q, over frozen entities [key_begin, key_end):
+// LDS-DMA: one wave-instruction copies 64 lanes x 16 B from per-lane global
+// addresses to the wave-uniform LDS byte address `lds_base` (+16 B per lane).
+// Issued through inline asm so the compiler does not track the asynchronous LDS
+// write: it would otherwise drain it (s_waitcnt vmcnt(0)) before the first LDS
+// read of the OTHER buffer.  The kernel owns the wait: `s_waitcnt vmcnt(0)`
+// before the barrier that hands the buffer to the readers.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
+}
+
+// ----------------------------------------------------------------------------
+// kp_attn: per query q (row of Qpre), over frozen entities [key_begin, key_end):
 //   m = max_e s_e,  l = sum_e exp(s_e - m),  O = sum_e exp(s_e - m) E_e
-// with s_e = q . E_e.  4 waves x 16 queries per workgroup share a 16-entity
-// E tile in LDS (double buffered, register prefetch).  fp32 MFMA 16x16x4 in the
-// swapped form: S^T = E . Q^T (key on the C row), so P already sits in the
-// B-operand layout of O^T += E^T . P (no LDS round trip for P).
+// with s_e = q . E_e.  4 waves x 16 queries per workgroup share a 32-entity E
+// tile in LDS (double buffered, staged by LDS-DMA while the previous tile is
+// consumed).  fp32 MFMA 16x16x4 in the swapped form S^T = E . Q^T (key on the C
+// row), so P already sits in the B-operand layout of O^T += E^T . P.
 //   lane l: g = l>>4, c = l&15.  Q fragment qv[j][i] = Q[c][16j+4g+i] stays in
 //   VGPRs; O^T accumulators O[j][r] = O[d = 16j+4g+r][q = c].
-// MODE 0 (ComplEx step):  queries q = x_slot o R_rel built from qdesc, softmax + O.
-// MODE 1 (ComplEx pairs):  queries read from Qpre, softmax statistics only.
-// MODE 2 (ConvE BCE):      queries read from Qpre; instead of the softmax the
-//   BCELoss-through-sigmoid gradient G(s) = ((p - y)/max(p(1-p),1e-12) * gs) * p(1-p)
+// The running max is only moved when a tile's max exceeds it by more than
+// kLazy (p = exp(s - m) <= e^8 stays well inside fp32), so the AGPR-resident O
+// is almost never rescaled.
+// MODE ATT_SOFTMAX_O (ComplEx step) / ATT_SOFTMAX (pairs: statistics only) /
+// ATT_BCE_O (ConvE): instead of the softmax the BCELoss-through-sigmoid gradient
+//   G(s) = ((p - y)/max(p(1-p),1e-12) * gs) * p(1-p)
 //   (p = sigmoid(s), y = the smoothed non-target label, gs = 1/(b*N) per query,
 //   bce_optimizer.py:35,98-112) weights O = sum_e G(s_e) E_e.
 // ----------------------------------------------------------------------------
 enum { ATT_SOFTMAX_O = 0, ATT_SOFTMAX = 1, ATT_BCE_O = 2 };
+constexpr float kLazy = 8.0f;
 
 template <int DB, int MODE>
-__global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, int n_ent, int half,
-                                                  const int4* __restrict__ qdesc,
-                                                  const float* __restrict__ X,
-                                                  const float* __restrict__ R,
-                                                  const float* __restrict__ Qpre, int nq,
-                                                  int keys_per_split, float* __restrict__ out_m,
-                                                  float* __restrict__ out_l, float* __restrict__ out_O,
-                                                  const float* __restrict__ qscale, float ylo) {
+__global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, int n_ent,
+                                                  const float* __restrict__ Qpre, int nq, int keys_per_split,
+                                                  float* __restrict__ out_m, float* __restrict__ out_l,
+                                                  float* __restrict__ out_O, const float* __restrict__ qscale,
+                                                  float ylo) {
   constexpr bool WITH_O = MODE != ATT_SOFTMAX;
   constexpr int DP = 16 * DB;
-  constexpr int S = DP + 4;  // LDS row stride: 2-way b128 / conflict-free b32
-  constexpr int KT = 16;
+  constexpr int S = DP + 4;  // LDS row stride: 2-way ds_read_b128, conflict-free ds_read_b32
+  constexpr int KT = 32;     // entities per LDS tile (two 16-entity MFMA sub-tiles)
   constexpr int F4_ROW = DP / 4;
-  constexpr int NF4 = KT * F4_ROW;
-  constexpr int PF = (NF4 + 255) / 256;
+  constexpr int SEGS = (F4_ROW + 63) / 64;  // 1-KiB LDS-DMA pieces per row (no piece crosses a row)
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][KT][S]
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
   const int q = blockIdx.x * 64 + 16 * w + c;
   const bool valid = q < nq;
   const int split = blockIdx.y;
   const int key_begin = split * keys_per_split;
   const int key_end = min(n_ent, key_begin + keys_per_split);
+  const int nkeys = max(0, key_end - key_begin);
+  const int ntiles = (nkeys + KT - 1) / KT;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
 
-  // ---- Q fragment -> registers
+  // LDS-DMA staging: piece (row, seg) = 64 lanes x 16 B of one entity row, landing at
+  // row*S + seg*256.  Rows past the table are clamped to a valid row; their scores
+  // are masked, so they add 0.
+  auto issue = [&](int tile, int buf) {
+    const int k0 = key_begin + tile * KT;
+    for (int ins = w; ins < KT * SEGS; ins += 4) {
+      const int row = ins / SEGS, seg = ins - row * SEGS;
+      const int f4 = seg * 64 + lane;
+      const int grow = min(k0 + row, n_ent - 1);
+      const uint32_t dst = lds0 + 4u * (uint32_t)(buf * (KT * S) + row * S + seg * 256);
+      if (f4 < F4_ROW) glds16(E + (size_t)grow * DP + 4 * f4, __builtin_amdgcn_readfirstlane(dst));
+    }
+  };
+  if (ntiles > 0) issue(0, 0);
+
+  // ---- Q fragment -> registers (overlaps the first tile's DMA)
   float qv[DB][4];
   float gsc = 0.f;
   if (MODE == ATT_BCE_O) gsc = valid ? qscale[q] : 0.f;
-  if (MODE == ATT_SOFTMAX_O) {
-    const int4 sr = valid ? qdesc[q] : make_int4(0, 0, 0, 0);
-    const float* x = X + (size_t)sr.x * DP;
-    const float* r = R + (size_t)sr.y * DP;
-#pragma unroll
-    for (int j = 0; j < DB; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) qv[j][i] = valid ? cx_q(x, r, 16 * j + 4 * g + i, half) : 0.f;
-  } else {
+  {
     const float* qp = Qpre + (size_t)(valid ? q : 0) * DP;
 #pragma unroll
     for (int j = 0; j < DB; ++j) {
@@ -94,110 +116,93 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
       qv[j][3] = valid ? v.w : 0.f;
     }
   }
-
   f32x4 O[WITH_O ? DB : 1];
 #pragma unroll
   for (int j = 0; j < (WITH_O ? DB : 1); ++j) O[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m_run = kNegInf, l_run = 0.f;
 
-  const int nkeys = max(0, key_end - key_begin);
-  const int ntiles = (nkeys + KT - 1) / KT;
-  float4 pf[PF];
-
-  auto gload = [&](int tile) {
-    const int k0 = key_begin + tile * KT;
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      int f = tid + 256 * u;
-      int row = f / F4_ROW, c4 = f - row * F4_ROW;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (f < NF4 && k0 + row < key_end) v = *reinterpret_cast<const float4*>(E + (size_t)(k0 + row) * DP + 4 * c4);
-      pf[u] = v;
-    }
-  };
-  auto lstore = [&](int buf) {
-    float* base = lds + buf * (KT * S);
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      int f = tid + 256 * u;
-      if (f < NF4) {
-        int row = f / F4_ROW, c4 = f - row * F4_ROW;
-        *reinterpret_cast<float4*>(base + row * S + 4 * c4) = pf[u];
-      }
-    }
-  };
-
-  if (ntiles > 0) {
-    gload(0);
-    lstore(0);
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) gload(t + 1);
+    if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
     const float* Es = lds + (t & 1) * (KT * S);
     const int k0 = key_begin + t * KT;
-    // ---- S^T tile: s[r] = q_c . E[k0 + 4g + r]
-    // two independent accumulation chains (dependent-issue latency 40 > 32 cycles)
-    f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, s2 = s;
+    // ---- S^T for two 16-entity sub-tiles: sA[r] = q_c . E[k0+4g+r], sB[r] = q_c . E[k0+16+4g+r]
+    f32x4 sA = (f32x4){0.f, 0.f, 0.f, 0.f}, sB = sA;
 #pragma unroll
     for (int j = 0; j < DB; ++j) {
-      float4 a = *reinterpret_cast<const float4*>(Es + c * S + 16 * j + 4 * g);
-      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, qv[j][0], s, 0, 0, 0);
-      s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, qv[j][1], s2, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, qv[j][2], s, 0, 0, 0);
-      s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, qv[j][3], s2, 0, 0, 0);
+      const float4 a0 = *reinterpret_cast<const float4*>(Es + c * S + 16 * j + 4 * g);
+      const float4 a1 = *reinterpret_cast<const float4*>(Es + (16 + c) * S + 16 * j + 4 * g);
+      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, qv[j][0], sA, 0, 0, 0);
+      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, qv[j][0], sB, 0, 0, 0);
+      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, qv[j][1], sA, 0, 0, 0);
+      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, qv[j][1], sB, 0, 0, 0);
+      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, qv[j][2], sA, 0, 0, 0);
+      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, qv[j][2], sB, 0, 0, 0);
+      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, qv[j][3], sA, 0, 0, 0);
+      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, qv[j][3], sB, 0, 0, 0);
     }
-    s += s2;
+    float pA[4], pB[4];
     if (MODE == ATT_BCE_O) {
-      float p[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pr = 1.0f / (1.0f + __expf(-s[r]));
-        const float w = (1.0f - pr) * pr;
-        const float gr = ((pr - ylo) / fmaxf(w, 1e-12f) * gsc) * w;
-        p[r] = (k0 + 4 * g + r < key_end) ? gr : 0.f;
+        const float x0 = 1.0f / (1.0f + __expf(-sA[r]));
+        const float w0 = (1.0f - x0) * x0;
+        const float x1 = 1.0f / (1.0f + __expf(-sB[r]));
+        const float w1 = (1.0f - x1) * x1;
+        pA[r] = (k0 + 4 * g + r < key_end) ? ((x0 - ylo) / fmaxf(w0, 1e-12f) * gsc) * w0 : 0.f;
+        pB[r] = (k0 + 16 + 4 * g + r < key_end) ? ((x1 - ylo) / fmaxf(w1, 1e-12f) * gsc) * w1 : 0.f;
       }
+    } else {
+      float vA[4], vB[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        vA[r] = (k0 + 4 * g + r < key_end) ? sA[r] : kNegInf;
+        vB[r] = (k0 + 16 + 4 * g + r < key_end) ? sB[r] : kNegInf;
+      }
+      float tmax = fmaxf(fmaxf(fmaxf(vA[0], vA[1]), fmaxf(vA[2], vA[3])),
+                         fmaxf(fmaxf(vB[0], vB[1]), fmaxf(vB[2], vB[3])));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      if (__any(tmax > m_run + kLazy)) {
+        const float m_new = fmaxf(m_run, tmax);
+        const float scale = __expf(m_run - m_new);
+        l_run *= scale;
+        m_run = m_new;
+        if (WITH_O) {
 #pragma unroll
-        for (int j = 0; j < DB; ++j) {
-          float a = Es[(4 * g + r) * S + 16 * j + c];
-          O[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, p[r], O[j], 0, 0, 0);
+          for (int j = 0; j < DB; ++j) O[j] *= scale;
         }
       }
-      if (t + 1 < ntiles) lstore((t + 1) & 1);
-      __syncthreads();
-      continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pA[r] = __expf(vA[r] - m_run);
+        pB[r] = __expf(vB[r] - m_run);
+      }
+      l_run += ((pA[0] + pA[1]) + (pA[2] + pA[3])) + ((pB[0] + pB[1]) + (pB[2] + pB[3]));
     }
-    float sv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sv[r] = (k0 + 4 * g + r < key_end) ? s[r] : kNegInf;
-    float tmax = fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float scale = __expf(m_run - m_new);
-    float p[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) p[r] = __expf(sv[r] - m_new);
-    l_run = l_run * scale + ((p[0] + p[1]) + (p[2] + p[3]));
-    m_run = m_new;
     if (WITH_O) {
-      if (__any(scale != 1.0f)) {
+      // O^T += E^T P over the 32 entities: k-step r of sub-tile A / B takes entities 4g+r
 #pragma unroll
-        for (int j = 0; j < DB; ++j) O[j] *= scale;
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int j = 0; j < DB; ++j) {
+          const float a = Es[(4 * g + r) * S + 16 * j + c];
+          O[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, pA[r], O[j], 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
 #pragma unroll
         for (int j = 0; j < DB; ++j) {
-          float a = Es[(4 * g + r) * S + 16 * j + c];
-          O[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, p[r], O[j], 0, 0, 0);
+          const float a = Es[(16 + 4 * g + r) * S + 16 * j + c];
+          O[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, pB[r], O[j], 0, 0, 0);
         }
       }
     }
-    if (t + 1 < ntiles) lstore((t + 1) & 1);
+    // tile t+1 landed (each wave waits for its own DMA) and every wave is done with buffer t&1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
@@ -218,5 +223,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
   }
 }
 
+// LDS bytes of kp_attn<DB, *>
+constexpr size_t attn_lds_bytes(int DB) { return 2u * 32u * (16u * DB + 4u) * sizeof(float); }
 
 }  // namespace kpattn

@@ -261,20 +261,37 @@ __global__ void kp_cx_scoreq(const float* __restrict__ E, const float* __restric
 // ----------------------------------------------------------------------------
 // host side
 // ----------------------------------------------------------------------------
+// step queries q_j = x_slot o R_rel (complex.py:65-72), one row per step query
+template <int DP>
+__global__ void kp_cx_stepq(const float* __restrict__ X, const float* __restrict__ R, int half,
+                            const int4* __restrict__ stepq, int nq, float* __restrict__ Q) {
+  const int j = blockIdx.x;
+  if (j >= nq) return;
+  const int4 sq = stepq[j];
+  const float* x = X + (size_t)sq.x * DP;
+  const float* rel = R + (size_t)sq.y * DP;
+  for (int d = threadIdx.x; d < DP; d += blockDim.x) Q[(size_t)j * DP + d] = cx_q(x, rel, d, half);
+}
+
 template <int DB>
-void launch_attn(kp_ctx* c, bool with_o, const int4* qdesc, const float* X, const float* Qpre, int nq,
-                 int n_split, float* m, float* l, float* O) {
+void launch_stepq(kp_ctx* c, const int4* stepq, const float* X, int nq, float* Q) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL((kp_cx_stepq<16 * DB>), dim3(nq), dim3(64), 0, c->stream, X, c->dR, c->dim / 2, stepq, nq, Q);
+  KP_HIP(hipGetLastError());
+}
+
+template <int DB>
+void launch_attn(kp_ctx* c, bool with_o, const float* Q, int nq, int n_split, float* m, float* l, float* O) {
   if (nq <= 0) return;
   const int keys_per_split = (c->n_ent + n_split - 1) / n_split;
   dim3 grid((nq + 63) / 64, n_split);
-  const size_t shm = 2 * 16 * (16 * DB + 4) * sizeof(float);
-  const int half = c->dim / 2;
+  const size_t shm = attn_lds_bytes(DB);
   if (with_o)
-    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX_O>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, half, qdesc,
-                       X, c->dR, Qpre, nq, keys_per_split, m, l, O, nullptr, 0.f);
+    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX_O>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, Q, nq,
+                       keys_per_split, m, l, O, nullptr, 0.f);
   else
-    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, half, qdesc, X,
-                       c->dR, Qpre, nq, keys_per_split, m, l, O, nullptr, 0.f);
+    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, Q, nq,
+                       keys_per_split, m, l, O, nullptr, 0.f);
   KP_HIP(hipGetLastError());
 }
 
@@ -541,12 +558,13 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float* dAm = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * att_rows));
   float* dAl = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * att_rows));
   float* dAO = reinterpret_cast<float*>(c->ws[15].ensure(sizeof(float) * att_rows * DP));
+  float* dQs = reinterpret_cast<float*>(c->ws[26].ensure(sizeof(float) * (size_t)std::max(max_nq, 1) * DP));
   (void)n_split_max;
   if (npairs > 0) {
     hipLaunchKernelGGL(kp_cx_qpair, dim3(npairs), dim3(128), 0, c->stream, c->dE, c->dR, DP, half, dPairs, npairs,
                        dQpair);
     KP_HIP(hipGetLastError());
-    CX_DISPATCH(DBV, launch_attn<DB>(c, false, nullptr, nullptr, dQpair, npairs, split_pairs, dAm, dAl, nullptr));
+    CX_DISPATCH(DBV, launch_attn<DB>(c, false, dQpair, npairs, split_pairs, dAm, dAl, nullptr));
     // combine splits into lsef (host-free: small kernel via update-style math on host is avoided)
     std::vector<float> hm((size_t)npairs * split_pairs), hl((size_t)npairs * split_pairs);
     KP_HIP(hipMemcpyAsync(hm.data(), dAm, sizeof(float) * hm.size(), hipMemcpyDeviceToHost, c->stream));
@@ -590,9 +608,10 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     if (nq > 0 && c->time_hot) {
       ea = c->event(2 * hot_launches);
       eb = c->event(2 * hot_launches + 1);
-      KP_HIP(hipEventRecord(ea, c->stream));
     }
-    CX_DISPATCH(DBV, launch_attn<DB>(c, true, dStepQ + q_off[t], dX, nullptr, nq, sp, dAm, dAl, dAO));
+    CX_DISPATCH(DBV, launch_stepq<DB>(c, dStepQ + q_off[t], dX, nq, dQs));
+    if (nq > 0 && c->time_hot) KP_HIP(hipEventRecord(ea, c->stream));
+    CX_DISPATCH(DBV, launch_attn<DB>(c, true, dQs, nq, sp, dAm, dAl, dAO));
     if (nq > 0) {
       if (c->time_hot) {
         KP_HIP(hipEventRecord(eb, c->stream));

@@ -542,7 +542,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   double hot = 0.0, work = 0.0;
   int64_t launches = 0;
   c->hot_pairs.clear();
-  const size_t shm_attn = 2 * 16 * (DP + 4) * sizeof(float);
+  const size_t shm_attn = attn_lds_bytes(DP / 16);
   const size_t shm_cbwd = sizeof(float) * 32 * 20 * (c->dim / 20 - 2);
   for (int t = 0; t < T; ++t) {
     const int nk = kin_off[t + 1] - kin_off[t];
@@ -566,8 +566,8 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       const int kps = (K + n_split - 1) / n_split;
       dim3 grid((nk + 63) / 64, n_split);
 #define CV_ATT(DBX)                                                                                                  \
-  hipLaunchKernelGGL((kp_attn<DBX, ATT_BCE_O>), grid, dim3(256), shm_attn, c->stream, c->dE, K, 0, nullptr, nullptr, \
-                     nullptr, dQ, nk, kps, nullptr, nullptr, dO, dgs + kin_off[t], kc.ylo)
+  hipLaunchKernelGGL((kp_attn<DBX, ATT_BCE_O>), grid, dim3(256), shm_attn, c->stream, c->dE, K, dQ, nk, kps, \
+                     nullptr, nullptr, dO, dgs + kin_off[t], kc.ylo)
       switch (DBV) {
         case 4: CV_ATT(4); break;
         case 8: CV_ATT(8); break;
