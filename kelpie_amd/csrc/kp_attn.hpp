@@ -46,10 +46,16 @@ __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
 // consumed).  fp32 MFMA 16x16x4 in the swapped form S^T = E . Q^T (key on the C
 // row), so P already sits in the B-operand layout of O^T += E^T . P.
 //   lane l: g = l>>4, c = l&15.  Q fragment qv[j][i] = Q[c][16j+4g+i] stays in
-//   VGPRs; O^T accumulators O[j][r] = O[d = 16j+4g+r][q = c].
-// The running max is only moved when a tile's max exceeds it by more than
-// kLazy (p = exp(s - m) <= e^8 stays well inside fp32), so the AGPR-resident O
-// is almost never rescaled.
+//   VGPRs; O^T accumulators O[j][r] = O[d = od(j, 4g+r)][q = c] with the
+//   dimension map od(j, i) = 64(j/4) + 4i + j%4 for j < 4(DB/4), else
+//   64(DB/4) + 16(j%4) + i, so a lane's A operands for four blocks are one
+//   16-byte LDS read.
+// Softmax reference: instead of the online max (whose rescaling of O under a
+// branch makes the compiler copy the whole AGPR-resident O block every tile),
+// weights are exp(s - m_ref) with m_ref = the first tile's max.  fp32 is scale
+// invariant, so this is as accurate as long as s - m_ref <= kMargin; the running
+// max is tracked on the side and, in the rare case a later score exceeds
+// m_ref + kMargin, the workgroup recomputes the split with m_ref = the exact max.
 // MODE ATT_SOFTMAX_O (ComplEx step) / ATT_SOFTMAX (pairs: statistics only) /
 // ATT_BCE_O (ConvE): instead of the softmax the BCELoss-through-sigmoid gradient
 //   G(s) = ((p - y)/max(p(1-p),1e-12) * gs) * p(1-p)
@@ -57,7 +63,7 @@ __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
 //   bce_optimizer.py:35,98-112) weights O = sum_e G(s_e) E_e.
 // ----------------------------------------------------------------------------
 enum { ATT_SOFTMAX_O = 0, ATT_SOFTMAX = 1, ATT_BCE_O = 2 };
-constexpr float kLazy = 8.0f;
+constexpr float kMargin = 40.0f;  // max exponent s - m_ref of a pass-1 weight (e^40 * N * |E| << FLT_MAX)
 
 template <int DB, int MODE>
 __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, int n_ent,
@@ -99,9 +105,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
       if (f4 < F4_ROW) glds16(E + (size_t)grow * DP + 4 * f4, __builtin_amdgcn_readfirstlane(dst));
     }
   };
-  if (ntiles > 0) issue(0, 0);
-
-  // ---- Q fragment -> registers (overlaps the first tile's DMA)
+  // ---- Q fragment -> registers
   float qv[DB][4];
   float gsc = 0.f;
   if (MODE == ATT_BCE_O) gsc = valid ? qscale[q] : 0.f;
@@ -117,93 +121,101 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
     }
   }
   f32x4 O[WITH_O ? DB : 1];
-#pragma unroll
-  for (int j = 0; j < (WITH_O ? DB : 1); ++j) O[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m_run = kNegInf, l_run = 0.f;
+  float m_ref = kNegInf, l_run = 0.f;
 
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
-    const float* Es = lds + (t & 1) * (KT * S);
-    const int k0 = key_begin + t * KT;
-    // ---- S^T for two 16-entity sub-tiles: sA[r] = q_c . E[k0+4g+r], sB[r] = q_c . E[k0+16+4g+r]
-    f32x4 sA = (f32x4){0.f, 0.f, 0.f, 0.f}, sB = sA;
+  for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-    for (int j = 0; j < DB; ++j) {
-      const float4 a0 = *reinterpret_cast<const float4*>(Es + c * S + 16 * j + 4 * g);
-      const float4 a1 = *reinterpret_cast<const float4*>(Es + (16 + c) * S + 16 * j + 4 * g);
-      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, qv[j][0], sA, 0, 0, 0);
-      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, qv[j][0], sB, 0, 0, 0);
-      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, qv[j][1], sA, 0, 0, 0);
-      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, qv[j][1], sB, 0, 0, 0);
-      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, qv[j][2], sA, 0, 0, 0);
-      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, qv[j][2], sB, 0, 0, 0);
-      sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, qv[j][3], sA, 0, 0, 0);
-      sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, qv[j][3], sB, 0, 0, 0);
-    }
-    float pA[4], pB[4];
-    if (MODE == ATT_BCE_O) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x0 = 1.0f / (1.0f + __expf(-sA[r]));
-        const float w0 = (1.0f - x0) * x0;
-        const float x1 = 1.0f / (1.0f + __expf(-sB[r]));
-        const float w1 = (1.0f - x1) * x1;
-        pA[r] = (k0 + 4 * g + r < key_end) ? ((x0 - ylo) / fmaxf(w0, 1e-12f) * gsc) * w0 : 0.f;
-        pB[r] = (k0 + 16 + 4 * g + r < key_end) ? ((x1 - ylo) / fmaxf(w1, 1e-12f) * gsc) * w1 : 0.f;
-      }
-    } else {
-      float vA[4], vB[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        vA[r] = (k0 + 4 * g + r < key_end) ? sA[r] : kNegInf;
-        vB[r] = (k0 + 16 + 4 * g + r < key_end) ? sB[r] : kNegInf;
-      }
-      float tmax = fmaxf(fmaxf(fmaxf(vA[0], vA[1]), fmaxf(vA[2], vA[3])),
-                         fmaxf(fmaxf(vB[0], vB[1]), fmaxf(vB[2], vB[3])));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      if (__any(tmax > m_run + kLazy)) {
-        const float m_new = fmaxf(m_run, tmax);
-        const float scale = __expf(m_run - m_new);
-        l_run *= scale;
-        m_run = m_new;
-        if (WITH_O) {
-#pragma unroll
-          for (int j = 0; j < DB; ++j) O[j] *= scale;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pA[r] = __expf(vA[r] - m_run);
-        pB[r] = __expf(vB[r] - m_run);
-      }
-      l_run += ((pA[0] + pA[1]) + (pA[2] + pA[3])) + ((pB[0] + pB[1]) + (pB[2] + pB[3]));
-    }
-    if (WITH_O) {
-      // O^T += E^T P over the 32 entities: k-step r of sub-tile A / B takes entities 4g+r
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int j = 0; j < DB; ++j) {
-          const float a = Es[(4 * g + r) * S + 16 * j + c];
-          O[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, pA[r], O[j], 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int j = 0; j < DB; ++j) {
-          const float a = Es[(16 + 4 * g + r) * S + 16 * j + c];
-          O[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, pB[r], O[j], 0, 0, 0);
-        }
-      }
-    }
-    // tile t+1 landed (each wave waits for its own DMA) and every wave is done with buffer t&1
+    for (int j = 0; j < (WITH_O ? DB : 1); ++j) O[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    l_run = 0.f;
+    float m_seen = kNegInf;  // running max of this lane's scores
+    if (ntiles > 0) issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+
+    for (int t = 0; t < ntiles; ++t) {
+      if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
+      const float* Es = lds + (t & 1) * (KT * S);
+      const int k0 = key_begin + t * KT;
+      // ---- S^T for two 16-entity sub-tiles: sA[r] = q_c . E[k0+4g+r], sB[r] = q_c . E[k0+16+4g+r]
+      f32x4 sA = (f32x4){0.f, 0.f, 0.f, 0.f}, sB = sA;
+#pragma unroll
+      for (int j = 0; j < DB; ++j) {
+        const float4 a0 = *reinterpret_cast<const float4*>(Es + c * S + 16 * j + 4 * g);
+        const float4 a1 = *reinterpret_cast<const float4*>(Es + (16 + c) * S + 16 * j + 4 * g);
+        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, qv[j][0], sA, 0, 0, 0);
+        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, qv[j][0], sB, 0, 0, 0);
+        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, qv[j][1], sA, 0, 0, 0);
+        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, qv[j][1], sB, 0, 0, 0);
+        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, qv[j][2], sA, 0, 0, 0);
+        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, qv[j][2], sB, 0, 0, 0);
+        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, qv[j][3], sA, 0, 0, 0);
+        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, qv[j][3], sB, 0, 0, 0);
+      }
+      float pA[4], pB[4];
+      if (MODE == ATT_BCE_O) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x0 = 1.0f / (1.0f + __expf(-sA[r]));
+          const float w0 = (1.0f - x0) * x0;
+          const float x1 = 1.0f / (1.0f + __expf(-sB[r]));
+          const float w1 = (1.0f - x1) * x1;
+          pA[r] = (k0 + 4 * g + r < key_end) ? ((x0 - ylo) / fmaxf(w0, 1e-12f) * gsc) * w0 : 0.f;
+          pB[r] = (k0 + 16 + 4 * g + r < key_end) ? ((x1 - ylo) / fmaxf(w1, 1e-12f) * gsc) * w1 : 0.f;
+        }
+      } else {
+        float vA[4], vB[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vA[r] = (k0 + 4 * g + r < key_end) ? sA[r] : kNegInf;
+          vB[r] = (k0 + 16 + 4 * g + r < key_end) ? sB[r] : kNegInf;
+        }
+        const float tmax = fmaxf(fmaxf(fmaxf(vA[0], vA[1]), fmaxf(vA[2], vA[3])),
+                                 fmaxf(fmaxf(vB[0], vB[1]), fmaxf(vB[2], vB[3])));
+        m_seen = fmaxf(m_seen, tmax);
+        if (pass == 0 && t == 0) {  // the reference max of pass 1: the first tile's
+          float mq = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+          m_ref = fmaxf(mq, __shfl_xor(mq, 32, 64));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pA[r] = __expf(vA[r] - m_ref);
+          pB[r] = __expf(vB[r] - m_ref);
+        }
+        l_run += ((pA[0] + pA[1]) + (pA[2] + pA[3])) + ((pB[0] + pB[1]) + (pB[2] + pB[3]));
+      }
+      if (WITH_O) {
+        // O^T += E^T P over the 32 entities: k-step rr takes entity 4g+rr (sub-tile A,
+        // rr < 4) / 16+4g+rr-4 (sub-tile B).  A-operand lane (i = c, k = g) of block j
+        // is E[entity][od(j, c)]: 4 consecutive blocks share one 16-B LDS read.
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          const float* rowp = Es + ((rr < 4) ? 4 * g + rr : 16 + 4 * g + rr - 4) * S;
+          const float pv = (rr < 4) ? pA[rr & 3] : pB[rr & 3];
+#pragma unroll
+          for (int m = 0; m < DB / 4; ++m) {
+            const float4 v = *reinterpret_cast<const float4*>(rowp + 64 * m + 4 * c);
+            O[4 * m + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, pv, O[4 * m + 0], 0, 0, 0);
+            O[4 * m + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, pv, O[4 * m + 1], 0, 0, 0);
+            O[4 * m + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, pv, O[4 * m + 2], 0, 0, 0);
+            O[4 * m + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, pv, O[4 * m + 3], 0, 0, 0);
+          }
+#pragma unroll
+          for (int k = 0; k < DB % 4; ++k) {
+            const float v = rowp[64 * (DB / 4) + 16 * k + c];
+            O[4 * (DB / 4) + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, pv, O[4 * (DB / 4) + k], 0, 0, 0);
+          }
+        }
+      }
+      // tile t+1 landed (each wave waits for its own DMA) and every wave is done with buffer t&1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (MODE == ATT_BCE_O) break;
+    // exact max of the query; a second pass only if some weight exceeded e^kMargin
+    float mq = fmaxf(m_seen, __shfl_xor(m_seen, 16, 64));
+    mq = fmaxf(mq, __shfl_xor(mq, 32, 64));
+    if (pass == 1 || !__syncthreads_or(mq > m_ref + kMargin)) break;
+    m_ref = mq;
   }
 
   float l_tot = l_run + __shfl_xor(l_run, 16, 64);
@@ -211,14 +223,22 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
   if (valid) {
     const size_t o = (size_t)split * nq + q;
     if (g == 0 && MODE != ATT_BCE_O) {
-      out_m[o] = m_run;
+      out_m[o] = m_ref;
       out_l[o] = l_tot;
     }
     if (WITH_O) {
+      // O^T row i = 4g+r of block j holds dimension od(j, i)
       float* dst = out_O + o * DP;
 #pragma unroll
-      for (int j = 0; j < DB; ++j)
-        *reinterpret_cast<float4*>(dst + 16 * j + 4 * g) = make_float4(O[j][0], O[j][1], O[j][2], O[j][3]);
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * g + r;
+#pragma unroll
+        for (int m = 0; m < DB / 4; ++m)
+          *reinterpret_cast<float4*>(dst + 64 * m + 4 * i) =
+              make_float4(O[4 * m][r], O[4 * m + 1][r], O[4 * m + 2][r], O[4 * m + 3][r]);
+#pragma unroll
+        for (int k = 0; k < DB % 4; ++k) dst[64 * (DB / 4) + 16 * k + i] = O[4 * (DB / 4) + k][r];
+      }
     }
   }
 }
