@@ -44,12 +44,20 @@ HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 20, "lr": 0.043,
       "regularizer_name": "N3", "regularizer_weight": 0}
 
 
-@pytest.mark.parametrize("dim", [200, 8])
-def test_complex_vs_oracle_full_width(dim):
+@pytest.mark.parametrize("dim,hot", [(200, False), (8, False), (200, True)])
+def test_complex_vs_oracle_full_width(dim, hot):
     """D = 400 (the production kernel instantiation) and D = 16 on a 2,000-entity
-    graph, including a hub subject with more rows than one minibatch."""
+    graph, including a hub subject with more rows than one minibatch.
+
+    ``hot``: the last entity row is scaled so that its scores exceed every split's
+    first-tile maximum by far more than kpattn::kMargin, which exercises the
+    attention kernel's exact-max second pass (step and frozen-pair queries)."""
     from cpu_backend import OracleBackedContext
     g, ds, w = _small_complex(dim=dim)
+    init_scale = 1e-3
+    if hot:
+        w["entity_embeddings"][-1] = 40.0
+        init_scale = 1.0
     deg = ds.entity_to_degree
     test = [tuple(int(v) for v in t) for t in g.test]
     preds = [t for t in test if 8 <= deg.get(t[0], 0) <= 40][:2]
@@ -57,7 +65,7 @@ def test_complex_vs_oracle_full_width(dim):
     assert deg[preds[-1][0]] > 256
     out = {}
     for backend in ("gpu", "cpu"):
-        model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"], init_scale=1e-3)
+        model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"], init_scale=init_scale)
         if backend == "cpu":
             model._ctx = OracleBackedContext(model)
         seed_all(42)
