@@ -100,10 +100,14 @@ def bernoulli_bits(state: np.ndarray, n: int, p: float) -> np.ndarray:
     return words
 
 
-def transe_epochs(torch_state: np.ndarray, np_key: np.ndarray, np_pos: np.ndarray, R: int, epochs: int,
+def transe_epochs(torch_state: np.ndarray, np_key, np_pos, R: int, epochs: int,
                   ratio: int, n_entities: int) -> np.ndarray:
+    """``np_key`` / ``np_pos``: numpy arrays, or raw addresses (int) of a live
+    MT19937 ``key[624]`` / ``pos`` pair, which are then advanced in place."""
     out = np.zeros(max(1, epochs * 3 * R), np.int32)
-    check(lib().kp_rng_transe_epochs(_ptr(torch_state), torch_state.size, _ptr(np_key), _ptr(np_pos), int(R),
+    key = C.c_void_p(np_key) if isinstance(np_key, int) else _ptr(np_key)
+    pos = C.c_void_p(np_pos) if isinstance(np_pos, int) else _ptr(np_pos)
+    check(lib().kp_rng_transe_epochs(_ptr(torch_state), torch_state.size, key, pos, int(R),
                                      int(epochs), int(ratio), int(n_entities), _ptr(out)))
     return out[:epochs * 3 * R]
 

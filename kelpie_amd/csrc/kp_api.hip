@@ -61,6 +61,7 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     c->n_rel2 = m->n_rel2;
     c->dim = m->dim;
     KP_HIP(hipSetDevice(device));
+    KP_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
     if (m->model == KP_MODEL_COMPLEX || m->model == KP_MODEL_CONVE) {
       KP_REQUIRE(m->model != KP_MODEL_COMPLEX || m->dim % 2 == 0, "ComplEx: row width must be even ([Re | Im])");
       int db = cx_pick_db(m->dim);
@@ -253,6 +254,24 @@ struct Mt {
       }
     }
   }
+  // the next n outputs, in order (operator() n times, block-wise)
+  void fill(uint32_t* out, size_t n) {
+    size_t k = 0;
+    while (k < n) {
+      if (left <= 1) {  // the next operator() call twists
+        twist();
+        temper_block();
+        left = 625;
+        next = 0;
+      }
+      if (!tb_ok) temper_block();
+      const size_t m = std::min<size_t>(n - k, (size_t)(left - 1));
+      std::memcpy(out + k, tb + next, sizeof(uint32_t) * m);
+      k += m;
+      next += m;
+      left -= (int32_t)m;
+    }
+  }
   inline uint32_t operator()() {
     if (--left == 0) {
       twist();
@@ -267,6 +286,12 @@ struct Mt {
 }  // namespace
 
 // numpy's legacy MT19937 (numpy/random/src/mt19937): pos in [0, 624], regenerate at 624
+// a % d for 32-bit a, d >= 1 (Lemire, Kaser & Kurz 2019), fm = 2^64 / d rounded up
+static inline uint32_t fastmod_u32(uint32_t a, uint64_t fm, uint32_t d) {
+  const uint64_t lowbits = fm * a;
+  return (uint32_t)(((__uint128_t)lowbits * d) >> 64);
+}
+
 struct NpMt {
   uint32_t* key;
   int32_t* pos;
@@ -312,6 +337,9 @@ int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np
   std::vector<int32_t> idx(R);
   for (int i = 0; i < R; ++i) idx[i] = i;
   const uint64_t n = (uint64_t)ratio * (uint64_t)R;
+  const uint32_t nent = (uint32_t)n_entities;
+  const uint64_t fm = UINT64_C(0xFFFFFFFFFFFFFFFF) / nent + 1;
+  std::vector<uint32_t> draw(std::max(R, 1));
   for (int e = 0; e < epochs; ++e) {
     for (int i = R - 1; i >= 1; --i) {  // np.random.shuffle: for i in reversed(range(1, n))
       const uint32_t j = np.interval((uint32_t)i);
@@ -321,13 +349,42 @@ int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np
     std::memcpy(o, idx.data(), sizeof(int32_t) * R);
     // randint(high=N): random() % N; only the first R values are stepped, the
     // other (ratio-1)*R draws are skipped without tempering
-    for (int k = 0; k < R; ++k) o[R + k] = (int32_t)(mt() % (uint32_t)n_entities);
+    mt.fill(draw.data(), R);
+    for (int k = 0; k < R; ++k) o[R + k] = (int32_t)fastmod_u32(draw[k], fm, nent);
     mt.skip(n - (uint64_t)R);
-    for (int k = 0; k < R; ++k) o[2 * R + k] = (int32_t)(mt() & 1u);  // randint(high=2)
+    mt.fill(draw.data(), R);
+    for (int k = 0; k < R; ++k) o[2 * R + k] = (int32_t)(draw[k] & 1u);  // randint(high=2)
     mt.skip(n - (uint64_t)R);
   }
   mt.store(ts);
   return KP_OK;
+}
+
+// ATen's bernoulli_(p) on a float tensor draws u = random64() * 2^-53 (hi word first)
+// per element and keeps it when u < p.  u is exact, so u < p <=> m < ceil(p * 2^53)
+// for the 53-bit integer m: the test runs on integers, block-wise over bulk draws.
+static void bernoulli_words(Mt& mt, uint64_t n, double p, uint32_t* out, std::vector<uint32_t>& buf) {
+  const uint64_t mask53 = (1ULL << 53) - 1;
+  const uint64_t thr = (uint64_t)std::ceil(std::ldexp(std::min(std::max(p, 0.0), 1.0), 53));
+  constexpr uint64_t CH = 1u << 14;  // elements per chunk (multiple of 32)
+  buf.resize(2 * CH);
+  for (uint64_t i0 = 0; i0 < n; i0 += CH) {
+    const uint64_t m = std::min<uint64_t>(CH, n - i0);
+    mt.fill(buf.data(), 2 * m);
+    const uint32_t* b = buf.data();
+    uint32_t* o = out + (i0 >> 5);
+    const uint64_t nw = (m + 31) / 32;
+    for (uint64_t w = 0; w < nw; ++w) {
+      uint32_t acc = 0;
+      const uint64_t lim = std::min<uint64_t>(32, m - 32 * w);
+      for (uint64_t j = 0; j < lim; ++j) {
+        const uint64_t e = 32 * w + j;
+        const uint64_t v = (((uint64_t)b[2 * e] << 32) | b[2 * e + 1]) & mask53;
+        acc |= (uint32_t)(v < thr) << j;
+      }
+      o[w] = acc;
+    }
+  }
 }
 
 int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim, double keep,
@@ -335,19 +392,12 @@ int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t*
   if (!ts || tlen < 24 + 624 * 8 || n_steps < 0 || dim <= 0 || (n_steps > 0 && (!rows || !out))) return KP_EINVAL;
   Mt mt;
   mt.load(ts);
-  const uint64_t mask53 = (1ULL << 53) - 1;
-  const double scale = std::ldexp(1.0, -53);
+  std::vector<uint32_t> buf;
   size_t w0 = 0;
   for (int st = 0; st < n_steps; ++st) {
     const uint64_t n = (uint64_t)rows[st] * (uint64_t)dim;
-    const size_t nw = (size_t)((n + 31) / 32);
-    for (size_t w = 0; w < nw; ++w) out[w0 + w] = 0u;
-    for (uint64_t i = 0; i < n; ++i) {
-      const uint64_t hi = mt(), lo = mt();
-      const double u = (double)(((hi << 32) | lo) & mask53) * scale;
-      if (u < keep) out[w0 + (i >> 5)] |= 1u << (i & 31);
-    }
-    w0 += nw;  // u = m * 2^-53 is exact, so this is ATen's uniform < p test bit for bit
+    bernoulli_words(mt, n, keep, out + w0, buf);  // each step's mask starts on a word
+    w0 += (size_t)((n + 31) / 32);
   }
   mt.store(ts);
   return KP_OK;
@@ -357,15 +407,8 @@ int kp_rng_bernoulli_bits(uint8_t* st, size_t len, uint64_t n, double p, uint32_
   if (!st || len < 24 + 624 * 8 || (n > 0 && !out)) return KP_EINVAL;
   Mt mt;
   mt.load(st);
-  const uint64_t mask53 = (1ULL << 53) - 1;
-  const double scale = std::ldexp(1.0, -53);
-  for (uint64_t w = 0; w < (n + 31) / 32; ++w) out[w] = 0u;
-  for (uint64_t i = 0; i < n; ++i) {
-    uint64_t hi = mt(), lo = mt();
-    uint64_t x = (hi << 32) | lo;
-    double u = (double)(x & mask53) * scale;
-    if (u < p) out[i >> 5] |= 1u << (i & 31);
-  }
+  std::vector<uint32_t> buf;
+  bernoulli_words(mt, n, p, out, buf);
   mt.store(st);
   return KP_OK;
 }

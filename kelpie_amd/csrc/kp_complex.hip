@@ -332,26 +332,6 @@ void launch_rankq(kp_ctx* c, const float* X, const int32_t* pred, int n, float* 
     default: throw KpError{KP_ENOTSUP, "ComplEx: unsupported padded dimension"}; \
   }
 
-static int choose_split(int nq, int n_ent) {
-  // enough workgroups to fill 256 CUs (1 workgroup/CU), limited by keys per split
-  const int tiles = (nq + 63) / 64;
-  int best = 1;
-  double best_eff = 0;
-  for (int s = 1; s <= UPD_MAXSPLIT; ++s) {
-    if (n_ent / s < 256 && s > 1) break;
-    const int wgs = tiles * s;
-    const int rounds = (wgs + 255) / 256;
-    // time ~ rounds * (keys per split) + combine overhead per split
-    const double t = rounds * ((double)n_ent / s) + 0.02 * n_ent * (s - 1) * tiles / 256.0;
-    const double eff = 1.0 / t;
-    if (eff > best_eff) {
-      best_eff = eff;
-      best = s;
-    }
-  }
-  return best;
-}
-
 }  // namespace
 
 int cx_pick_db(int dim) {
@@ -526,7 +506,6 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   KP_HIP(hipMemsetAsync(dS2, 0, sizeof(float) * (size_t)ns * DP, c->stream));
   CxPlan* dPlans = upload(c, c->ws[3], plans.data(), plans.size());
   CxQuery* dPq = upload(c, c->ws[4], pqs.data(), pqs.size());
-  CxTail* dPt = upload(c, c->ws[5], pts.data(), pts.size());
   int32_t* dTg = upload(c, c->ws[6], targets.data(), targets.size());
   int2* dPairs = upload(c, c->ws[7], pairs.data(), pairs.size());
   int4* dActs = upload(c, c->ws[8], acts.data(), acts.size());
@@ -547,12 +526,12 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   }
   // frozen-head pairs: q and frozen log-sum-exp
   const int n_split_max = UPD_MAXSPLIT;
-  const int split_pairs = choose_split(npairs, c->n_ent);
-  const int split_step = choose_split(max_nq, c->n_ent);
+  const int split_pairs = kp_choose_split(c, npairs, UPD_MAXSPLIT);
+  const int split_step = kp_choose_split(c, max_nq, UPD_MAXSPLIT);
   size_t att_rows = (size_t)std::max(npairs, 1) * split_pairs;
   for (int t = 0; t < T; ++t) {
     const int nq = q_off[t + 1] - q_off[t];
-    att_rows = std::max(att_rows, (size_t)nq * choose_split(nq, c->n_ent));
+    att_rows = std::max(att_rows, (size_t)nq * kp_choose_split(c, nq, UPD_MAXSPLIT));
   }
   (void)split_step;
   float* dAm = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * att_rows));
@@ -603,7 +582,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   for (int t = 0; t < T; ++t) {
     const int nq = q_off[t + 1] - q_off[t];
     const int na = act_off[t + 1] - act_off[t];
-    const int sp = choose_split(nq, c->n_ent);
+    const int sp = kp_choose_split(c, nq, UPD_MAXSPLIT);
     hipEvent_t ea = nullptr, eb = nullptr;
     if (nq > 0 && c->time_hot) {
       ea = c->event(2 * hot_launches);

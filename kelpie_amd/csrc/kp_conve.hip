@@ -524,8 +524,13 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       KP_HIP(hipMemcpyAsync(dgs, gsv.data(), sizeof(float) * gsv.size(), hipMemcpyHostToDevice, c->stream));
     }
   }
-  const int n_split = 4;
-  float* dO = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * (size_t)n_split * mk * DP));
+  constexpr int CV_MAXSPLIT = 16;
+  size_t o_rows = 1;
+  for (int t = 0; t < T; ++t) {
+    const int nk = kin_off[t + 1] - kin_off[t];
+    o_rows = std::max(o_rows, (size_t)nk * kp_choose_split(c, nk, CV_MAXSPLIT));
+  }
+  float* dO = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * o_rows * DP));
   float* ddfc = reinterpret_cast<float*>(c->ws[18].ensure(sizeof(float) * (size_t)mk * c->dim));
   float* dgk = reinterpret_cast<float*>(c->ws[19].ensure(sizeof(float) * (size_t)mk));
   float* ddflat = reinterpret_cast<float*>(c->ws[20].ensure(sizeof(float) * (size_t)mk * c->hidden));
@@ -549,6 +554,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     const int na = act_o[t + 1] - act_o[t];
     const CvInst* KI = dKI + kin_off[t];
     if (nk > 0) {
+      const int n_split = kp_choose_split(c, nk, CV_MAXSPLIT);
       hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
                          kc, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
       KP_HIP(hipGetLastError());

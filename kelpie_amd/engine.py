@@ -184,6 +184,65 @@ class PostTrainingEngine(RelevanceEngine):
     def compute_relevance_batch(self, pred, rules, checkpoints: list | None = None):
         raise NotImplementedError
 
+    def _schedule_multi(self, items, checkpoints):
+        raise NotImplementedError
+
+    def _finalize_multi(self, slots, pending, jobs):
+        raise NotImplementedError
+
+    def _multi(self, items, checkpoints=None):
+        t0 = time.perf_counter()
+        slots, pending, jobs = self._schedule_multi(items, checkpoints)
+        t_sched = time.perf_counter() - t0
+        self._run(slots)
+        self.last_batch_stats["schedule_s"] = t_sched
+        return self._finalize_multi(slots, pending, jobs)
+
+    def compute_relevance_pipeline(self, batches):
+        """Equivalent to ``[(self.set_cache(), self.compute_relevance_multi(b))[1] for b in batches]``
+        but the host schedules batch k+1 (its reference-order random draws and
+        slot assembly) while batch k runs on the device: the library call
+        releases the GIL.  Draw order is unchanged because scheduling stays
+        sequential on this thread; each batch starts from a cleared cache, so no
+        batch's schedule depends on another's results.  ``last_batch_stats`` is
+        a list of the per-batch stats."""
+        import threading
+
+        def run(state):
+            try:
+                self._run(state["slots"])
+                state["stats"] = dict(self.last_batch_stats)
+            except BaseException as e:  # re-raised on the scheduling thread
+                state["error"] = e
+
+        outs, stats, inflight = [], [], None
+
+        def finish(state):
+            state["thread"].join()
+            if "error" in state:
+                raise state["error"]
+            self.base_pt_results = {}
+            o = self._finalize_multi(state["slots"], state["pending"], state["jobs"])
+            st = state["stats"]
+            st["schedule_s"] = state["schedule_s"]
+            stats.append(st)
+            outs.append(o)
+
+        for items in batches:
+            self.set_cache()
+            t0 = time.perf_counter()
+            slots, pending, jobs = self._schedule_multi(items, None)
+            t_sched = time.perf_counter() - t0
+            if inflight is not None:
+                finish(inflight)
+            inflight = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched}
+            inflight["thread"] = threading.Thread(target=run, args=(inflight,), daemon=True)
+            inflight["thread"].start()
+        if inflight is not None:
+            finish(inflight)
+        self.last_batch_stats = stats
+        return outs
+
 
 class NecessaryPostTrainingEngine(PostTrainingEngine):
     """post_training_engine.py:128-157."""
@@ -197,8 +256,10 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
     def compute_relevance_multi(self, items, checkpoints: list | None = None):
         """[(pred, rules), ...] -> [[relevance per rule], ...] in ONE device batch;
         equal to the sequential compute_relevance calls in that order."""
+        return self._multi(items, checkpoints)
+
+    def _schedule_multi(self, items, checkpoints):
         slots, pending, jobs = [], {}, []
-        t0 = time.perf_counter()
         for pred, rules in items:
             pj = []
             for rule in rules:
@@ -206,9 +267,9 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
                 if checkpoints is not None:
                     checkpoints.append(StateCheckpoint())
             jobs.append(pj)
-        t_sched = time.perf_counter() - t0
-        self._run(slots)
-        self.last_batch_stats["schedule_s"] = t_sched
+        return slots, pending, jobs
+
+    def _finalize_multi(self, slots, pending, jobs):
         minimizer = self.model.is_minimizer()
         outs = []
         self.last_results = []
@@ -241,8 +302,10 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
 
     def compute_relevance_multi(self, items, checkpoints: list | None = None):
         """[(pred, rules, entities_to_convert), ...] in ONE device batch."""
+        return self._multi(items, checkpoints)
+
+    def _schedule_multi(self, items, checkpoints):
         slots, pending, jobs = [], {}, []
-        t0 = time.perf_counter()
         for pred, rules, ents in items:
             pred = tuple(int(v) for v in pred)
             s = pred[0]
@@ -259,9 +322,9 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
                 if checkpoints is not None:
                     checkpoints.append(StateCheckpoint())
             jobs.append(pj)
-        t_sched = time.perf_counter() - t0
-        self._run(slots)
-        self.last_batch_stats["schedule_s"] = t_sched
+        return slots, pending, jobs
+
+    def _finalize_multi(self, slots, pending, jobs):
         minimizer = self.model.is_minimizer()
         outs = []
         self.last_results = []

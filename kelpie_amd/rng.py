@@ -44,6 +44,11 @@ def _set_state(st):
     torch.set_rng_state(torch.from_numpy(st))
 
 
+def _np_mt_state_address() -> int:
+    """Address of the global RandomState's ``mt19937_state`` (numpy/random/src/mt19937/mt19937.h)."""
+    return int(np.random.mtrand._rand._bit_generator.ctypes.state_address)
+
+
 class ReferenceRNG:
     """Draws from the process-global torch / numpy generators (reference order)."""
 
@@ -84,11 +89,11 @@ class ReferenceRNG:
         if epochs <= 0:
             return np.zeros(0, np.int32)
         st = _get_state()
-        name, key, pos, has_gauss, cached = np.random.get_state()
-        key = np.ascontiguousarray(key, dtype=np.uint32).copy()
-        posa = np.array([pos], dtype=np.int32)
-        out = _lib.transe_epochs(st, key, posa, R, epochs, ratio, n_entities)
-        np.random.set_state((name, key, int(posa[0]), has_gauss, cached))
+        # numpy's global MT19937 is advanced in place through its C state struct
+        # (BitGenerator.ctypes.state_address -> {uint32 key[624]; int pos}):
+        # get_state/set_state would cost ~0.1 ms per slot
+        addr = _np_mt_state_address()
+        out = _lib.transe_epochs(st, addr, addr + 4 * 624, R, epochs, ratio, n_entities)
         _set_state(st)
         return out
 

@@ -105,3 +105,31 @@ def check_builder(name, backend, window=32):
         for (rule, rel), (erule, erel) in zip(out["rule_to_relevance"], b["rule_to_relevance"]):
             assert [list(t) for t in rule] == [list(t) for t in erule]
             assert abs(rel - erel) <= TOL
+
+
+def check_pipeline(name, backend):
+    """compute_relevance_pipeline (host schedules batch k+1 while batch k runs)
+    over every recorded prediction equals the reference's sequential calls."""
+    rec, ds, model = build_product(name, backend)
+    seed_all(rec["seed"])
+    eng = ka.NecessaryPostTrainingEngine(model, ds, rec["hp"])
+    batches = [[(tuple(b["pred"]), [[tuple(t) for t in c["rule"]] for c in b["calls"]])] for b in rec["necessary"]]
+    outs = eng.compute_relevance_pipeline(batches)
+    assert len(eng.last_batch_stats) == len(batches)
+    for block, out in zip(rec["necessary"], outs):
+        for call, rel in zip(block["calls"], out[0]):
+            assert abs(rel - call["relevance"]) <= TOL, (name, call["rule"], rel, call["relevance"])
+    if not rec.get("sufficient"):
+        return
+    rec, ds, model = build_product(name, backend)
+    seed_all(rec["seed"])
+    eng = ka.SufficientPostTrainingEngine(model, ds, rec["hp"])
+    batches = []
+    for block in rec["sufficient"]:
+        eng.set_cache()
+        pred = tuple(block["pred"])
+        ents = eng.select_entities_to_convert(pred, block["k"], block["degree_cap"])
+        batches.append([(pred, [[tuple(t) for t in c["rule"]] for c in block["calls"]], ents)])
+    for block, out in zip(rec["sufficient"], eng.compute_relevance_pipeline(batches)):
+        for call, rel in zip(block["calls"], out[0]):
+            assert abs(rel - call["relevance"]) <= TOL, (name, call["rule"], rel, call["relevance"])

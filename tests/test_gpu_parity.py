@@ -5,7 +5,7 @@ Run on an MI355X: ``python -m pytest tests -m gpu``.
 import numpy as np
 import pytest
 
-from engine_cases import build_product, check_builder, check_necessary, check_sufficient
+from engine_cases import build_product, check_builder, check_necessary, check_pipeline, check_sufficient
 from golden_io import seed_all
 
 import kelpie_amd as ka
@@ -30,6 +30,11 @@ def test_sufficient_vs_reference_goldens(name):
 @pytest.mark.parametrize("window", [1, 32])
 def test_builder_vs_reference_goldens(name, window):
     check_builder(name, "gpu", window=window)
+
+
+@pytest.mark.parametrize("name", GPU_CASES)
+def test_pipeline_vs_reference_goldens(name):
+    check_pipeline(name, "gpu")
 
 
 def _small_complex(dim=200, scale=0.3, seed=3):

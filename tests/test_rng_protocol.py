@@ -91,3 +91,16 @@ def test_conve_masks_match_torch_dropout_sequence():
         assert np.array_equal(got, m)
         off += nw
     assert torch.equal(torch.rand(2), after)
+
+
+def test_numpy_state_address_layout():
+    """The in-place numpy path relies on mt19937_state = {uint32 key[624]; int pos}."""
+    import ctypes
+    from kelpie_amd.rng import _np_mt_state_address
+    np.random.seed(7)
+    np.random.random(5)
+    _, key, pos, _, _ = np.random.get_state()
+    addr = _np_mt_state_address()
+    k = np.ctypeslib.as_array((ctypes.c_uint32 * 624).from_address(addr))
+    p = ctypes.c_int.from_address(addr + 4 * 624).value
+    assert np.array_equal(k, np.asarray(key, np.uint32)) and p == pos
