@@ -59,6 +59,30 @@ WORKLOADS = {
 }
 
 
+def committed_traffic(workload, kernel):
+    """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 FETCH_SIZE
+    pass of this workload (profiles/rNN_<workload>_pmc.json, tools/prof_summary.py).
+    PMC counters cannot be read from inside the timed run, so the bench line cites them."""
+    import glob
+    import json
+    import re
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_{workload}_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f).get("fetch_bytes_per_launch", {})
+    m = re.match(r"kp_attn<(\d+),(\w+)>", kernel)
+    want = f"kp_attn<{m.group(1)}, {ATT_MODES[m.group(2)]}>" if m else kernel
+    for name, v in d.items():
+        if want in name:
+            return v["hbm_bytes"], os.path.relpath(files[-1], here)
+    return None, None
+
+
+ATT_MODES = {"ATT_SOFTMAX_O": 0, "ATT_SOFTMAX": 1, "ATT_BCE_O": 2}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -234,6 +258,7 @@ def main():
                 "frac": (achieved / peak) if achieved else None, "traffic": None,
                 "kernel": "kp_attn<%d,%s>" % (-(-D // 16), "ATT_SOFTMAX_O" if wl["model"] == "ComplEx"
                                               else "ATT_BCE_O")}
+    roof["traffic"], roof["traffic_source"] = committed_traffic(args.workload, roof["kernel"])
     roof["launches"] = hot[2]
     roof["avg_launch_ms"] = (hot[0] / hot[2] * 1e3) if hot[2] else None
 
