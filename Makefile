@@ -2,7 +2,9 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 SRC := $(wildcard kelpie_amd/csrc/*.hip)
-OBJ := $(patsubst kelpie_amd/csrc/%.hip,build/%.o,$(SRC))
+CPP := $(wildcard kelpie_amd/csrc/*.cpp)
+OBJ := $(patsubst kelpie_amd/csrc/%.hip,build/%.o,$(SRC)) $(patsubst kelpie_amd/csrc/%.cpp,build/%.cpp.o,$(CPP))
+CXX ?= g++
 FLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
          -Wno-unused-result -Iinclude -Xarch_host -mavx2
 LIB := kelpie_amd/libkelpie_hip.so
@@ -13,8 +15,13 @@ build/%.o: kelpie_amd/csrc/%.hip kelpie_amd/csrc/kp_common.hpp kelpie_amd/csrc/k
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) -c $< -o $@
 
+# host-only C++ (prefilter graphs)
+build/%.cpp.o: kelpie_amd/csrc/%.cpp include/kelpie_hip.h
+	@mkdir -p build
+	$(CXX) -O3 -std=c++17 -fPIC -Wall -mavx2 -pthread -Iinclude -c $< -o $@
+
 $(LIB): $(OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $(OBJ)
 
 resources: $(SRC)
 	@mkdir -p build

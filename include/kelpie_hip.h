@@ -190,6 +190,33 @@ int kp_rng_conve_masks(uint8_t* torch_state, size_t torch_len, int32_t n_steps, 
 int kp_last_timing(const kp_ctx* ctx, double* device_seconds, double* hot_kernel_seconds,
                    int64_t* hot_kernel_launches, double* hot_work_units);
 
+/* ---- candidate prefilters, host C++ ----------------
+ * The undirected multigraph of TopologyPreFilter / WeightedTopologyPreFilter
+ * (topology_prefilter.py:12-14, weighted_topology_prefilter.py:16-18): one
+ * edge per training triple (h, t) over entities [0, n_ent); neighbour order is
+ * networkx's insertion order.  Errors: kp_graph_last_error() (thread-local). */
+typedef struct kp_graph kp_graph;
+int kp_graph_create(int32_t n_ent, int64_t n_triples, const int32_t* triples, kp_graph** out);
+void kp_graph_destroy(kp_graph* g);
+const char* kp_graph_last_error(void);
+
+/* Hop distance from each source to every entity, dist[i * n_ent + v]; -1 when
+ * unreachable (nx.NetworkXNoPath -> 1e6 at topology_prefilter.py:36-37).  One
+ * search from a prediction's object serves all of its candidates
+ * (topology_prefilter.py:29-34 searches once per candidate; distances are symmetric). */
+int kp_graph_bfs(const kp_graph* g, int32_t n_src, const int32_t* src, int32_t* dist);
+
+/* Entity classes (CSR: class ids of entity v at cls[cls_off[v] .. cls_off[v+1]))
+ * for the edge cost 1 - jaccard_similarity(classes(u), classes(v))
+ * (weighted_topology_prefilter.py:40-44, utils/utils.py:11-14), float64. */
+int kp_graph_set_classes(kp_graph* g, const int64_t* cls_off, const int32_t* cls);
+
+/* nx.shortest_path_length(G, src[i], dst[i], weight=semantic_score) for each i
+ * (weighted_topology_prefilter.py:46-56), replaying networkx's Dijkstra
+ * (neighbour order, (distance, push counter) heap) so sums match bit for bit;
+ * +inf when there is no path. */
+int kp_graph_dijkstra_pairs(const kp_graph* g, int32_t n, const int32_t* src, const int32_t* dst, double* out);
+
 /* Library version string. */
 const char* kp_version(void);
 

@@ -9,5 +9,7 @@ from .data import Dataset, KelpieView  # noqa: F401
 from .engine import NecessaryPostTrainingEngine, PostTrainingEngine, SufficientPostTrainingEngine  # noqa: F401
 from .models import MODEL_REGISTRY, ComplEx, ConvE, TransE, from_state_dict  # noqa: F401
 from .builder import StochasticBuilder  # noqa: F401
+from .prefilters import NoPreFilter, TopologyPreFilter, WeightedTopologyPreFilter  # noqa: F401
+from .pipeline import NecessaryPipeline, SufficientPipeline, build_pipeline, explain_preds, read_preds  # noqa: F401
 
 __version__ = "0.1.0"

@@ -19,7 +19,8 @@ KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
 # symbols declared by include/kelpie_hip.h
 EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_rank", "kp_all_scores",
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
-           "kp_rng_transe_epochs", "kp_rng_conve_masks"]
+           "kp_rng_transe_epochs", "kp_rng_conve_masks", "kp_graph_create", "kp_graph_destroy",
+           "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs"]
 
 
 class ModelDesc(C.Structure):
@@ -64,6 +65,13 @@ def lib():
         L.kp_convertible.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
                                      C.c_void_p, C.c_void_p]
         L.kp_mt19937_discard.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.kp_graph_create.argtypes = [C.c_int32, C.c_int64, C.c_void_p, C.POINTER(C.c_void_p)]
+        L.kp_graph_destroy.argtypes = [C.c_void_p]
+        L.kp_graph_destroy.restype = None
+        L.kp_graph_last_error.restype = C.c_char_p
+        L.kp_graph_bfs.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        L.kp_graph_set_classes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.kp_graph_dijkstra_pairs.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_rng_bernoulli_bits.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_double, C.c_void_p]
         L.kp_rng_transe_epochs.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                            C.c_int32, C.c_int64, C.c_void_p]
@@ -193,3 +201,45 @@ class Context:
         a, b, n, w = C.c_double(), C.c_double(), C.c_int64(), C.c_double()
         check(lib().kp_last_timing(self.h, C.byref(a), C.byref(b), C.byref(n), C.byref(w)), self.h)
         return {"device_s": a.value, "hot_s": b.value, "hot_launches": n.value, "hot_work": w.value}
+
+
+class Graph:
+    """Prefilter graph (kp_graph_*): undirected multigraph of the training triples."""
+
+    def __init__(self, n_ent: int, triples):
+        t = np.ascontiguousarray(np.asarray(triples, dtype=np.int32).reshape(-1, 3))
+        h = C.c_void_p()
+        self._lib = lib()
+        self._check(self._lib.kp_graph_create(int(n_ent), len(t), _ptr(t), C.byref(h)))
+        self._h = h
+        self.n_ent = int(n_ent)
+
+    def _check(self, rc):
+        if rc != 0:
+            raise KelpieHipError(f"libkelpie_hip error {rc}: {self._lib.kp_graph_last_error().decode()}")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.kp_graph_destroy(h)
+            self._h = None
+
+    def bfs(self, sources) -> np.ndarray:
+        src = np.ascontiguousarray(sources, dtype=np.int32).reshape(-1)
+        out = np.empty((len(src), self.n_ent), np.int32)
+        self._check(self._lib.kp_graph_bfs(self._h, len(src), _ptr(src), _ptr(out)))
+        return out
+
+    def set_classes(self, cls_off, cls):
+        off = np.ascontiguousarray(cls_off, dtype=np.int64)
+        c = np.ascontiguousarray(cls, dtype=np.int32) if len(cls) else np.zeros(1, np.int32)
+        assert len(off) == self.n_ent + 1
+        self._check(self._lib.kp_graph_set_classes(self._h, _ptr(off), _ptr(c)))
+
+    def dijkstra_pairs(self, src, dst) -> np.ndarray:
+        s = np.ascontiguousarray(src, dtype=np.int32).reshape(-1)
+        d = np.ascontiguousarray(dst, dtype=np.int32).reshape(-1)
+        assert len(s) == len(d)
+        out = np.empty(len(s), np.float64)
+        self._check(self._lib.kp_graph_dijkstra_pairs(self._h, len(s), _ptr(s), _ptr(d), _ptr(out)))
+        return out

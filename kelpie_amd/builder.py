@@ -56,8 +56,7 @@ class StochasticBuilder:
         rule_to_rel = sorted(rule_to_rel, key=lambda x: (x[1], 1 / len(x[0])), reverse=True)[:k]
         mapped = [(self.dataset.labels_triples(rule), rel) for rule, rel in rule_to_rel]
         return {"triple": self.dataset.labels_triple(tuple(pred)), "rule_to_relevance": mapped,
-                "#relevances": rels_num, "execution_time": time.time() - start,
-                "rules": rule_to_rel}
+                "#relevances": rels_num, "execution_time": time.time() - start}
 
     def explore_singleton_rules(self, pred, triples: list):
         # one engine batch for every singleton; a duplicated candidate is evaluated

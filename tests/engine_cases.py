@@ -133,3 +133,32 @@ def check_pipeline(name, backend):
     for block, out in zip(rec["sufficient"], eng.compute_relevance_pipeline(batches)):
         for call, rel in zip(block["calls"], out[0]):
             assert abs(rel - call["relevance"]) <= TOL, (name, call["rule"], rel, call["relevance"])
+
+
+def check_pipeline_explain(name, backend, tmpdir):
+    """NecessaryPipeline (prefilter -> builder, src/pipeline.py:21-29) over read_preds /
+    explain_preds / output.json equals the reference's recorded builder run."""
+    import json
+    import os
+    from kelpie_amd.pipeline import build_pipeline, explain_preds, read_preds
+    rec, ds, model = build_product(name, backend)
+    b = rec["builder"]
+    pred = tuple(b["pred"])
+    preds_path = os.path.join(tmpdir, "preds.csv")
+    with open(preds_path, "w") as f:
+        f.write("\t".join(ds.labels_triple(pred)) + "\n")
+    seed_all(rec["seed"])
+    pipe = build_pipeline(model, ds, rec["hp"], "necessary", xsi=b["xsi"])
+    out_path = os.path.join(tmpdir, "output.json")
+    res = explain_preds(pipe, ds, read_preds(preds_path), prefilter_k=len(b["candidates"]), output_path=out_path)
+    with open(out_path) as f:
+        on_disk = json.load(f)
+    assert len(res) == len(on_disk) == 1
+    out = on_disk[0]
+    assert set(out) == {"triple", "rule_to_relevance", "#relevances", "execution_time"}
+    assert out["triple"] == list(b["triple"])
+    assert out["#relevances"] == b["n_relevances"]
+    assert len(out["rule_to_relevance"]) == len(b["rule_to_relevance"])
+    for (rule, rel), (erule, erel) in zip(out["rule_to_relevance"], b["rule_to_relevance"]):
+        assert [list(t) for t in rule] == [list(t) for t in erule]  # label triples
+        assert abs(rel - erel) <= TOL

@@ -7,7 +7,7 @@ formulas, batching and the builder's speculative windows with RNG rewind.
 """
 import pytest
 
-from engine_cases import check_builder, check_necessary, check_pipeline, check_sufficient
+from engine_cases import check_builder, check_necessary, check_pipeline, check_pipeline_explain, check_sufficient
 from golden_io import CASES
 
 FAST = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve60_tiny"]
@@ -33,3 +33,8 @@ def test_builder_speculative_windows(name, window):
 @pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
 def test_pipeline_host_protocol(name):
     check_pipeline(name, "cpu")
+
+
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
+def test_explain_pipeline_and_output_json(name, tmp_path):
+    check_pipeline_explain(name, "cpu", str(tmp_path))

@@ -5,7 +5,8 @@ Run on an MI355X: ``python -m pytest tests -m gpu``.
 import numpy as np
 import pytest
 
-from engine_cases import build_product, check_builder, check_necessary, check_pipeline, check_sufficient
+from engine_cases import (build_product, check_builder, check_necessary, check_pipeline, check_pipeline_explain,
+                          check_sufficient)
 from golden_io import seed_all
 
 import kelpie_amd as ka
@@ -35,6 +36,11 @@ def test_builder_vs_reference_goldens(name, window):
 @pytest.mark.parametrize("name", GPU_CASES)
 def test_pipeline_vs_reference_goldens(name):
     check_pipeline(name, "gpu")
+
+
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny", "conve60_tiny"])
+def test_explain_pipeline_vs_reference_goldens(name, tmp_path):
+    check_pipeline_explain(name, "gpu", str(tmp_path))
 
 
 def _small_complex(dim=200, scale=0.3, seed=3):
