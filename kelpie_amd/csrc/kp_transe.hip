@@ -36,6 +36,65 @@ struct TeHp {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+constexpr int TE_CH = 256;  // stepped pairs whose descriptors are staged in LDS at a time
+
+// one (positive, negative) pair: the two difference vectors of 16 lanes x VPL float4
+template <int VPL>
+struct TePair {
+  float4 vp[VPL], vn[VPL];
+  float sp, sn;
+};
+
+template <int VPL>
+__device__ __forceinline__ void te_load(TePair<VPL>& P, const float* Lp, const float* Rp, const float* Ln,
+                                        const float* Rn, const float* rel, int l16, int NF4) {
+  P.sp = 0.f;
+  P.sn = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int f = l16 + 16 * u;
+    if (f < NF4) {
+      const float4 a = ld4(Lp + 4 * f), b = ld4(rel + 4 * f), c = ld4(Rp + 4 * f);
+      const float4 a2 = ld4(Ln + 4 * f), c2 = ld4(Rn + 4 * f);
+      P.vp[u] = make_float4((a.x + b.x) - c.x, (a.y + b.y) - c.y, (a.z + b.z) - c.z, (a.w + b.w) - c.w);
+      P.vn[u] = make_float4((a2.x + b.x) - c2.x, (a2.y + b.y) - c2.y, (a2.z + b.z) - c2.z, (a2.w + b.w) - c2.w);
+    } else {
+      P.vp[u] = P.vn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+template <int VPL>
+__device__ __forceinline__ void te_accum(TePair<VPL>& P, const int4 dsc, int tn, int K, float margin, float4* g,
+                                         int& cnt) {
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    P.sp += P.vp[u].x * P.vp[u].x + P.vp[u].y * P.vp[u].y + P.vp[u].z * P.vp[u].z + P.vp[u].w * P.vp[u].w;
+    P.sn += P.vn[u].x * P.vn[u].x + P.vn[u].y * P.vn[u].y + P.vn[u].z * P.vn[u].z + P.vn[u].w * P.vn[u].w;
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    P.sp += __shfl_xor(P.sp, o, 16);
+    P.sn += __shfl_xor(P.sn, o, 16);
+  }
+  const int h = dsc.x, t = dsc.z, hn = dsc.w;
+  const float fp = sqrtf(P.sp), fn = sqrtf(P.sn);
+  const float z = (fp - fn) + margin;
+  const bool act = z >= 0.f;  // clamp_min backward passes grad where self >= min
+  const float sgn_p = (float)((h == K) - (t == K));
+  const float sgn_n = (float)((hn == K) - (tn == K));
+  const float cp = (act && fp > 0.f) ? sgn_p / fp : 0.f;
+  const float cn = (act && fn > 0.f) ? -sgn_n / fn : 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    g[u].x += cp * P.vp[u].x + cn * P.vn[u].x;
+    g[u].y += cp * P.vp[u].y + cn * P.vn[u].y;
+    g[u].z += cp * P.vp[u].z + cn * P.vn[u].z;
+    g[u].w += cp * P.vp[u].w + cn * P.vn[u].w;
+  }
+  cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
+}
+
 template <int VPL>  // float4 per lane (16 lanes per row): DP <= 64 * VPL
 __global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d, const float* __restrict__ E,
                                                        const float* __restrict__ R,
@@ -44,8 +103,10 @@ __global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d,
                                                        const int32_t* __restrict__ rng, TeHp hp,
                                                        float* __restrict__ X) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* xs = sm;                 // [dp]
-  float* red = sm + dp;           // [16][dp] per-group gradient partials
+  float* xs = sm;                                            // [dp]
+  float* red = sm + dp;                                      // [16][dp] per-group gradient partials
+  int4* dsc = reinterpret_cast<int4*>(sm + 17 * dp);         // [TE_CH] (h, r, t, h_neg)
+  int* dtn = reinterpret_cast<int*>(dsc + TE_CH);            // [TE_CH] t_neg
   __shared__ int cnt_s[16];
   const int tid = threadIdx.x;
   const int grp = tid >> 4, l16 = tid & 15;
@@ -69,53 +130,37 @@ __global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d,
 #pragma unroll
       for (int u = 0; u < VPL; ++u) g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       int cnt = 0;
-      for (int j = st + grp; j < st + B; j += 16) {
-        const int ri = order[j / hp.ratio];
-        const int h = rw[3 * ri], r = rw[3 * ri + 1], t = rw[3 * ri + 2];
-        const int ent = ents[j];
-        const bool corrupt_head = hot[j] == 1;
-        const int hn = corrupt_head ? ent : h, tn = corrupt_head ? t : ent;
-        const float* Lp = (h == K) ? xs : E + (size_t)h * dp;
-        const float* Rp = (t == K) ? xs : E + (size_t)t * dp;
-        const float* Ln = (hn == K) ? xs : E + (size_t)hn * dp;
-        const float* Rn = (tn == K) ? xs : E + (size_t)tn * dp;
-        const float* rel = R + (size_t)r * dp;
-        float4 vp[VPL], vn[VPL];
-        float sp = 0.f, sn = 0.f;
-#pragma unroll
-        for (int u = 0; u < VPL; ++u) {
-          const int f = l16 + 16 * u;
-          if (f < NF4) {
-            const float4 a = ld4(Lp + 4 * f), b = ld4(rel + 4 * f), c = ld4(Rp + 4 * f);
-            const float4 a2 = ld4(Ln + 4 * f), c2 = ld4(Rn + 4 * f);
-            vp[u] = make_float4((a.x + b.x) - c.x, (a.y + b.y) - c.y, (a.z + b.z) - c.z, (a.w + b.w) - c.w);
-            vn[u] = make_float4((a2.x + b.x) - c2.x, (a2.y + b.y) - c2.y, (a2.z + b.z) - c2.z, (a2.w + b.w) - c2.w);
-          } else {
-            vp[u] = vn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-          sp += vp[u].x * vp[u].x + vp[u].y * vp[u].y + vp[u].z * vp[u].z + vp[u].w * vp[u].w;
-          sn += vn[u].x * vn[u].x + vn[u].y * vn[u].y + vn[u].z * vn[u].z + vn[u].w * vn[u].w;
+      for (int c0 = st; c0 < st + B; c0 += TE_CH) {
+        const int n = min(TE_CH, st + B - c0);
+        // ---- stage the chunk's pair descriptors (coalesced draws, row gathers from L2)
+        for (int k = tid; k < n; k += 256) {
+          const int j = c0 + k;
+          const int ri = order[j / hp.ratio];
+          const int h = rw[3 * ri], r = rw[3 * ri + 1], t = rw[3 * ri + 2];
+          const int ent = ents[j];
+          const bool corrupt_head = hot[j] == 1;
+          dsc[k] = make_int4(h, r, t, corrupt_head ? ent : h);
+          dtn[k] = corrupt_head ? t : ent;
         }
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-          sp += __shfl_xor(sp, o, 16);
-          sn += __shfl_xor(sn, o, 16);
+        __syncthreads();
+        // ---- two pairs per group in flight: all ten row loads issued before the math
+        for (int k = grp; k < n; k += 32) {
+          const bool two = k + 16 < n;
+          const int4 da = dsc[k];
+          const int ta = dtn[k];
+          const int4 db = two ? dsc[k + 16] : da;
+          const int tb = two ? dtn[k + 16] : ta;
+          TePair<VPL> A, Bp;
+          te_load<VPL>(A, (da.x == K) ? xs : E + (size_t)da.x * dp, (da.z == K) ? xs : E + (size_t)da.z * dp,
+                       (da.w == K) ? xs : E + (size_t)da.w * dp, (ta == K) ? xs : E + (size_t)ta * dp,
+                       R + (size_t)da.y * dp, l16, NF4);
+          te_load<VPL>(Bp, (db.x == K) ? xs : E + (size_t)db.x * dp, (db.z == K) ? xs : E + (size_t)db.z * dp,
+                       (db.w == K) ? xs : E + (size_t)db.w * dp, (tb == K) ? xs : E + (size_t)tb * dp,
+                       R + (size_t)db.y * dp, l16, NF4);
+          te_accum<VPL>(A, da, ta, K, hp.margin, g, cnt);
+          if (two) te_accum<VPL>(Bp, db, tb, K, hp.margin, g, cnt);
         }
-        const float fp = sqrtf(sp), fn = sqrtf(sn);
-        const float z = (fp - fn) + hp.margin;
-        const bool act = z >= 0.f;  // clamp_min backward passes grad where self >= min
-        const float sgn_p = (float)((h == K) - (t == K));
-        const float sgn_n = (float)((hn == K) - (tn == K));
-        const float cp = (act && fp > 0.f) ? sgn_p / fp : 0.f;
-        const float cn = (act && fn > 0.f) ? -sgn_n / fn : 0.f;
-#pragma unroll
-        for (int u = 0; u < VPL; ++u) {
-          g[u].x += cp * vp[u].x + cn * vn[u].x;
-          g[u].y += cp * vp[u].y + cn * vn[u].y;
-          g[u].z += cp * vp[u].z + cn * vn[u].z;
-          g[u].w += cp * vp[u].w + cn * vn[u].w;
-        }
-        cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
+        __syncthreads();  // the next chunk overwrites the descriptors
       }
       // ---- reduce the 16 group partials
 #pragma unroll
@@ -264,7 +309,7 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   KP_HIP(hipEventRecord(c->ev0, c->stream));
   hipEvent_t ea = c->event(0), eb = c->event(1);
   KP_HIP(hipEventRecord(ea, c->stream));
-  const size_t shm = sizeof(float) * (size_t)17 * DP;
+  const size_t shm = sizeof(float) * (size_t)17 * DP + sizeof(int4) * TE_CH + sizeof(int) * TE_CH;
   const int vpl = (DP + 63) / 64;
   switch (vpl) {
 #define TE_CASE(V)                                                                                              \
