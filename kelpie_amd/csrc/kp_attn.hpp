@@ -73,10 +73,14 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
                                                   float ylo) {
   constexpr bool WITH_O = MODE != ATT_SOFTMAX;
   constexpr int DP = 16 * DB;
-  constexpr int S = DP + 4;  // LDS row stride: 2-way ds_read_b128, conflict-free ds_read_b32
   constexpr int KT = 32;     // entities per LDS tile (two 16-entity MFMA sub-tiles)
   constexpr int F4_ROW = DP / 4;
   constexpr int SEGS = (F4_ROW + 63) / 64;  // 1-KiB LDS-DMA pieces per row (no piece crosses a row)
+  // LDS row stride: whole pieces plus 4 floats (S = 4 mod 64 banks: conflict-free
+  // ds_read_b128 across the 16 rows of an S read and along the row of an O read).
+  // Lanes past the row's end load a clamped duplicate into the padding, so every
+  // LDS-DMA instruction runs with all 64 lanes and no branch.
+  constexpr int S = 256 * SEGS + 4;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][KT][S]
 
   const int tid = threadIdx.x;
@@ -95,15 +99,21 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
   // LDS-DMA staging: piece (row, seg) = 64 lanes x 16 B of one entity row, landing at
   // row*S + seg*256.  Rows past the table are clamped to a valid row; their scores
   // are masked, so they add 0.
+  // Wave w issues pieces ins = w + 4p, p < PIECES; with SEGS in {1, 2} the piece's
+  // segment (ins % SEGS) is fixed per wave, so the lane mask is too.
+  static_assert(SEGS == 1 || SEGS == 2, "rows wider than 512 floats need more LDS-DMA pieces");
+  constexpr int PIECES = KT * SEGS / 4;
+  const int my_seg = w % SEGS;
+  const float* lane_src = E + 4 * min(my_seg * 64 + lane, F4_ROW - 1);
+  auto issue_piece = [&](int tile, int buf, int p) {
+    const int row = (w + 4 * p) / SEGS;
+    const int grow = min(key_begin + tile * KT + row, n_ent - 1);
+    const uint32_t dst = lds0 + 4u * (uint32_t)(buf * (KT * S) + row * S + my_seg * 256);
+    glds16(lane_src + (size_t)grow * DP, __builtin_amdgcn_readfirstlane(dst));
+  };
   auto issue = [&](int tile, int buf) {
-    const int k0 = key_begin + tile * KT;
-    for (int ins = w; ins < KT * SEGS; ins += 4) {
-      const int row = ins / SEGS, seg = ins - row * SEGS;
-      const int f4 = seg * 64 + lane;
-      const int grow = min(k0 + row, n_ent - 1);
-      const uint32_t dst = lds0 + 4u * (uint32_t)(buf * (KT * S) + row * S + seg * 256);
-      if (f4 < F4_ROW) glds16(E + (size_t)grow * DP + 4 * f4, __builtin_amdgcn_readfirstlane(dst));
-    }
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) issue_piece(tile, buf, p);
   };
   // ---- Q fragment -> registers
   float qv[DB][4];
@@ -133,7 +143,8 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
     __syncthreads();
 
     for (int t = 0; t < ntiles; ++t) {
-      if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
+      // the next tile's LDS-DMA pieces are spread over the S MFMA stream below (after
+      // the last tile they reload clamped rows into the idle buffer: harmless, branch-free)
       const float* Es = lds + (t & 1) * (KT * S);
       const int k0 = key_begin + t * KT;
       // ---- S^T for two 16-entity sub-tiles: sA[r] = q_c . E[k0+4g+r], sB[r] = q_c . E[k0+16+4g+r]
@@ -150,7 +161,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
         sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, qv[j][2], sB, 0, 0, 0);
         sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, qv[j][3], sA, 0, 0, 0);
         sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, qv[j][3], sB, 0, 0, 0);
+        if (j < PIECES) issue_piece(t + 1, (t + 1) & 1, j);
       }
+#pragma unroll
+      for (int p = DB; p < PIECES; ++p) issue_piece(t + 1, (t + 1) & 1, p);
       float pA[4], pB[4];
       if (MODE == ATT_BCE_O) {
 #pragma unroll
@@ -244,6 +258,6 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
 }
 
 // LDS bytes of kp_attn<DB, *>
-constexpr size_t attn_lds_bytes(int DB) { return 2u * 32u * (16u * DB + 4u) * sizeof(float); }
+constexpr size_t attn_lds_bytes(int DB) { return 2u * 32u * (256u * ((4u * DB + 63u) / 64u) + 4u) * sizeof(float); }
 
 }  // namespace kpattn
