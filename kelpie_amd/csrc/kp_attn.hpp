@@ -38,6 +38,33 @@ __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
 }
 
+// LDS reads issued through inline asm, so their placement is the source order:
+// each k-step's operands are read one k-step ahead, and the kernel waits with a
+// counted lgkmcnt (LDS returns in order).  tied() makes the consumer depend on the
+// wait, so no MFMA is scheduled above it.
+__device__ __forceinline__ f32x4 lds_rd128(uint32_t addr) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ float lds_rd32(uint32_t addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
+}
+__device__ __forceinline__ f32x4 tied(f32x4 v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ float tied(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // ----------------------------------------------------------------------------
 // kp_attn: per query q (row of Qpre), over frozen entities [key_begin, key_end):
 //   m = max_e s_e,  l = sum_e exp(s_e - m),  O = sum_e exp(s_e - m) E_e
@@ -143,16 +170,25 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
     __syncthreads();
 
     for (int t = 0; t < ntiles; ++t) {
-      // the next tile's LDS-DMA pieces are spread over the S MFMA stream below (after
-      // the last tile they reload clamped rows into the idle buffer: harmless, branch-free)
-      const float* Es = lds + (t & 1) * (KT * S);
       const int k0 = key_begin + t * KT;
       // ---- S^T for two 16-entity sub-tiles: sA[r] = q_c . E[k0+4g+r], sB[r] = q_c . E[k0+16+4g+r]
+      const uint32_t sbase = lds0 + 4u * (uint32_t)((t & 1) * (KT * S) + c * S + 4 * g);
+      const uint32_t sbase16 = sbase + 4u * 16u * S;
       f32x4 sA = (f32x4){0.f, 0.f, 0.f, 0.f}, sB = sA;
+      f32x4 ra[2], rb[2];
+      ra[0] = lds_rd128(sbase);
+      rb[0] = lds_rd128(sbase16);
 #pragma unroll
       for (int j = 0; j < DB; ++j) {
-        const float4 a0 = *reinterpret_cast<const float4*>(Es + c * S + 16 * j + 4 * g);
-        const float4 a1 = *reinterpret_cast<const float4*>(Es + (16 + c) * S + 16 * j + 4 * g);
+        if (j + 1 < DB) {
+          ra[(j + 1) & 1] = lds_rd128(sbase + 64u * (j + 1));
+          rb[(j + 1) & 1] = lds_rd128(sbase16 + 64u * (j + 1));
+          lgkm_wait<2>();
+        } else {
+          lgkm_wait<0>();
+        }
+        const f32x4 a0 = tied(ra[j & 1]);
+        const f32x4 a1 = tied(rb[j & 1]);
         sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, qv[j][0], sA, 0, 0, 0);
         sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, qv[j][0], sB, 0, 0, 0);
         sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, qv[j][1], sA, 0, 0, 0);
@@ -161,10 +197,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
         sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, qv[j][2], sB, 0, 0, 0);
         sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, qv[j][3], sA, 0, 0, 0);
         sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, qv[j][3], sB, 0, 0, 0);
-        if (j < PIECES) issue_piece(t + 1, (t + 1) & 1, j);
       }
-#pragma unroll
-      for (int p = DB; p < PIECES; ++p) issue_piece(t + 1, (t + 1) & 1, p);
+      // next tile's LDS-DMA (after the last tile it reloads clamped rows into the idle
+      // buffer: harmless and branch-free); issued while the last S MFMAs drain
+      issue(t + 1, (t + 1) & 1);
       float pA[4], pB[4];
       if (MODE == ATT_BCE_O) {
 #pragma unroll
@@ -200,23 +236,42 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
       if (WITH_O) {
         // O^T += E^T P over the 32 entities: k-step rr takes entity 4g+rr (sub-tile A,
         // rr < 4) / 16+4g+rr-4 (sub-tile B).  A-operand lane (i = c, k = g) of block j
-        // is E[entity][od(j, c)]: 4 consecutive blocks share one 16-B LDS read.
+        // is E[entity][od(j, c)]: 4 consecutive blocks share one 16-B LDS read; the
+        // DB % 4 remaining blocks take one 4-B read each.
+        constexpr int NB4 = DB / 4, REM = DB % 4, NR = NB4 + REM;
+        f32x4 ob[2][NB4 > 0 ? NB4 : 1];
+        float os[2][REM > 0 ? REM : 1];
+        auto load_k = [&](int rr, int b) {
+          const int row = (rr < 4) ? 4 * g + rr : 16 + 4 * g + rr - 4;
+          const uint32_t base = lds0 + 4u * (uint32_t)((t & 1) * (KT * S) + row * S);
+#pragma unroll
+          for (int m = 0; m < NB4; ++m) ob[b][m] = lds_rd128(base + 4u * (64 * m + 4 * c));
+#pragma unroll
+          for (int k = 0; k < REM; ++k) os[b][k] = lds_rd32(base + 4u * (64 * NB4 + 16 * k + c));
+        };
+        load_k(0, 0);
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) {
-          const float* rowp = Es + ((rr < 4) ? 4 * g + rr : 16 + 4 * g + rr - 4) * S;
+          const int b = rr & 1;
+          if (rr + 1 < 8) {
+            load_k(rr + 1, b ^ 1);
+            lgkm_wait<NR>();
+          } else {
+            lgkm_wait<0>();
+          }
           const float pv = (rr < 4) ? pA[rr & 3] : pB[rr & 3];
 #pragma unroll
-          for (int m = 0; m < DB / 4; ++m) {
-            const float4 v = *reinterpret_cast<const float4*>(rowp + 64 * m + 4 * c);
+          for (int m = 0; m < NB4; ++m) {
+            const f32x4 v = tied(ob[b][m]);
             O[4 * m + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, pv, O[4 * m + 0], 0, 0, 0);
             O[4 * m + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, pv, O[4 * m + 1], 0, 0, 0);
             O[4 * m + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, pv, O[4 * m + 2], 0, 0, 0);
             O[4 * m + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, pv, O[4 * m + 3], 0, 0, 0);
           }
 #pragma unroll
-          for (int k = 0; k < DB % 4; ++k) {
-            const float v = rowp[64 * (DB / 4) + 16 * k + c];
-            O[4 * (DB / 4) + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, pv, O[4 * (DB / 4) + k], 0, 0, 0);
+          for (int k = 0; k < REM; ++k) {
+            const float v = tied(os[b][k]);
+            O[4 * NB4 + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, pv, O[4 * NB4 + k], 0, 0, 0);
           }
         }
       }
