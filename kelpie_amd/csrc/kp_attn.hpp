@@ -100,7 +100,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
                                                   float ylo) {
   constexpr bool WITH_O = MODE != ATT_SOFTMAX;
   constexpr int DP = 16 * DB;
-  constexpr int KT = 32;     // entities per LDS tile (two 16-entity MFMA sub-tiles)
+  // entities per LDS tile: NSUB 16-entity MFMA sub-tiles.  32, not 64: a 64-entity
+  // double buffer of narrow rows (ConvE, 133 KB) leaves room for one workgroup per CU
+  // instead of two, and two co-resident workgroups measured faster (4.26 vs 4.63 ms).
+  constexpr int NSUB = 2;
+  constexpr int KT = 16 * NSUB;
   constexpr int F4_ROW = DP / 4;
   constexpr int SEGS = (F4_ROW + 63) / 64;  // 1-KiB LDS-DMA pieces per row (no piece crosses a row)
   // LDS row stride: whole pieces plus 4 floats (S = 4 mod 64 banks: conflict-free
@@ -171,78 +175,78 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
 
     for (int t = 0; t < ntiles; ++t) {
       const int k0 = key_begin + t * KT;
-      // ---- S^T for two 16-entity sub-tiles: sA[r] = q_c . E[k0+4g+r], sB[r] = q_c . E[k0+16+4g+r]
+      // ---- S^T per 16-entity sub-tile u: sc[u][r] = q_c . E[k0 + 16u + 4g + r]
       const uint32_t sbase = lds0 + 4u * (uint32_t)((t & 1) * (KT * S) + c * S + 4 * g);
-      const uint32_t sbase16 = sbase + 4u * 16u * S;
-      f32x4 sA = (f32x4){0.f, 0.f, 0.f, 0.f}, sB = sA;
-      f32x4 ra[2], rb[2];
-      ra[0] = lds_rd128(sbase);
-      rb[0] = lds_rd128(sbase16);
+      f32x4 sc[NSUB];
+      f32x4 ra[2][NSUB];
+#pragma unroll
+      for (int u = 0; u < NSUB; ++u) {
+        sc[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        ra[0][u] = lds_rd128(sbase + 4u * 16u * S * u);
+      }
 #pragma unroll
       for (int j = 0; j < DB; ++j) {
         if (j + 1 < DB) {
-          ra[(j + 1) & 1] = lds_rd128(sbase + 64u * (j + 1));
-          rb[(j + 1) & 1] = lds_rd128(sbase16 + 64u * (j + 1));
-          lgkm_wait<2>();
+#pragma unroll
+          for (int u = 0; u < NSUB; ++u) ra[(j + 1) & 1][u] = lds_rd128(sbase + 4u * 16u * S * u + 64u * (j + 1));
+          lgkm_wait<NSUB>();
         } else {
           lgkm_wait<0>();
         }
-        const f32x4 a0 = tied(ra[j & 1]);
-        const f32x4 a1 = tied(rb[j & 1]);
-        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, qv[j][0], sA, 0, 0, 0);
-        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, qv[j][0], sB, 0, 0, 0);
-        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, qv[j][1], sA, 0, 0, 0);
-        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, qv[j][1], sB, 0, 0, 0);
-        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, qv[j][2], sA, 0, 0, 0);
-        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, qv[j][2], sB, 0, 0, 0);
-        sA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, qv[j][3], sA, 0, 0, 0);
-        sB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, qv[j][3], sB, 0, 0, 0);
+        f32x4 a[NSUB];
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u) a[u] = tied(ra[j & 1][u]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int u = 0; u < NSUB; ++u) sc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][i], qv[j][i], sc[u], 0, 0, 0);
       }
       // next tile's LDS-DMA (after the last tile it reloads clamped rows into the idle
       // buffer: harmless and branch-free); issued while the last S MFMAs drain
       issue(t + 1, (t + 1) & 1);
-      float pA[4], pB[4];
+      float pw[NSUB][4];
       if (MODE == ATT_BCE_O) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x0 = 1.0f / (1.0f + __expf(-sA[r]));
-          const float w0 = (1.0f - x0) * x0;
-          const float x1 = 1.0f / (1.0f + __expf(-sB[r]));
-          const float w1 = (1.0f - x1) * x1;
-          pA[r] = (k0 + 4 * g + r < key_end) ? ((x0 - ylo) / fmaxf(w0, 1e-12f) * gsc) * w0 : 0.f;
-          pB[r] = (k0 + 16 + 4 * g + r < key_end) ? ((x1 - ylo) / fmaxf(w1, 1e-12f) * gsc) * w1 : 0.f;
-        }
-      } else {
-        float vA[4], vB[4];
+        for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          vA[r] = (k0 + 4 * g + r < key_end) ? sA[r] : kNegInf;
-          vB[r] = (k0 + 16 + 4 * g + r < key_end) ? sB[r] : kNegInf;
-        }
-        const float tmax = fmaxf(fmaxf(fmaxf(vA[0], vA[1]), fmaxf(vA[2], vA[3])),
-                                 fmaxf(fmaxf(vB[0], vB[1]), fmaxf(vB[2], vB[3])));
+          for (int r = 0; r < 4; ++r) {
+            const float x0 = 1.0f / (1.0f + __expf(-sc[u][r]));
+            const float w0 = (1.0f - x0) * x0;
+            pw[u][r] = (k0 + 16 * u + 4 * g + r < key_end) ? ((x0 - ylo) / fmaxf(w0, 1e-12f) * gsc) * w0 : 0.f;
+          }
+      } else {
+        float v[NSUB][4];
+        float tmax = kNegInf;
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[u][r] = (k0 + 16 * u + 4 * g + r < key_end) ? sc[u][r] : kNegInf;
+            tmax = fmaxf(tmax, v[u][r]);
+          }
         m_seen = fmaxf(m_seen, tmax);
         if (pass == 0 && t == 0) {  // the reference max of pass 1: the first tile's
           float mq = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
           m_ref = fmaxf(mq, __shfl_xor(mq, 32, 64));
         }
+        float lt = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pA[r] = __expf(vA[r] - m_ref);
-          pB[r] = __expf(vB[r] - m_ref);
+        for (int u = 0; u < NSUB; ++u) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pw[u][r] = __expf(v[u][r] - m_ref);
+          lt += (pw[u][0] + pw[u][1]) + (pw[u][2] + pw[u][3]);
         }
-        l_run += ((pA[0] + pA[1]) + (pA[2] + pA[3])) + ((pB[0] + pB[1]) + (pB[2] + pB[3]));
+        l_run += lt;
       }
       if (WITH_O) {
-        // O^T += E^T P over the 32 entities: k-step rr takes entity 4g+rr (sub-tile A,
-        // rr < 4) / 16+4g+rr-4 (sub-tile B).  A-operand lane (i = c, k = g) of block j
-        // is E[entity][od(j, c)]: 4 consecutive blocks share one 16-B LDS read; the
-        // DB % 4 remaining blocks take one 4-B read each.
-        constexpr int NB4 = DB / 4, REM = DB % 4, NR = NB4 + REM;
+        // O^T += E^T P over the KT entities: k-step rr takes entity 16(rr/4) + 4g + rr%4.
+        // A-operand lane (i = c, k = g) of block j is E[entity][od(j, c)]: 4 consecutive
+        // blocks share one 16-B LDS read; the DB % 4 remaining blocks take one 4-B read each.
+        constexpr int NB4 = DB / 4, REM = DB % 4, NR = NB4 + REM, NK = 4 * NSUB;
         f32x4 ob[2][NB4 > 0 ? NB4 : 1];
         float os[2][REM > 0 ? REM : 1];
         auto load_k = [&](int rr, int b) {
-          const int row = (rr < 4) ? 4 * g + rr : 16 + 4 * g + rr - 4;
+          const int row = 16 * (rr >> 2) + 4 * g + (rr & 3);
           const uint32_t base = lds0 + 4u * (uint32_t)((t & 1) * (KT * S) + row * S);
 #pragma unroll
           for (int m = 0; m < NB4; ++m) ob[b][m] = lds_rd128(base + 4u * (64 * m + 4 * c));
@@ -251,27 +255,27 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
         };
         load_k(0, 0);
 #pragma unroll
-        for (int rr = 0; rr < 8; ++rr) {
+        for (int rr = 0; rr < NK; ++rr) {
           const int b = rr & 1;
-          if (rr + 1 < 8) {
+          if (rr + 1 < NK) {
             load_k(rr + 1, b ^ 1);
             lgkm_wait<NR>();
           } else {
             lgkm_wait<0>();
           }
-          const float pv = (rr < 4) ? pA[rr & 3] : pB[rr & 3];
+          const float pv = pw[rr >> 2][rr & 3];
 #pragma unroll
           for (int m = 0; m < NB4; ++m) {
-            const f32x4 v = tied(ob[b][m]);
-            O[4 * m + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, pv, O[4 * m + 0], 0, 0, 0);
-            O[4 * m + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, pv, O[4 * m + 1], 0, 0, 0);
-            O[4 * m + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, pv, O[4 * m + 2], 0, 0, 0);
-            O[4 * m + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, pv, O[4 * m + 3], 0, 0, 0);
+            const f32x4 vv = tied(ob[b][m]);
+            O[4 * m + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.x, pv, O[4 * m + 0], 0, 0, 0);
+            O[4 * m + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.y, pv, O[4 * m + 1], 0, 0, 0);
+            O[4 * m + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.z, pv, O[4 * m + 2], 0, 0, 0);
+            O[4 * m + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.w, pv, O[4 * m + 3], 0, 0, 0);
           }
 #pragma unroll
           for (int k = 0; k < REM; ++k) {
-            const float v = tied(os[b][k]);
-            O[4 * NB4 + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, pv, O[4 * NB4 + k], 0, 0, 0);
+            const float vv = tied(os[b][k]);
+            O[4 * NB4 + k] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv, pv, O[4 * NB4 + k], 0, 0, 0);
           }
         }
       }
@@ -313,6 +317,8 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
 }
 
 // LDS bytes of kp_attn<DB, *>
-constexpr size_t attn_lds_bytes(int DB) { return 2u * 32u * (256u * ((4u * DB + 63u) / 64u) + 4u) * sizeof(float); }
+constexpr size_t attn_lds_bytes(int DB) {
+  return 2u * 32u * (256u * ((4u * DB + 63u) / 64u) + 4u) * sizeof(float);
+}
 
 }  // namespace kpattn
