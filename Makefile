@@ -27,7 +27,13 @@ resources: $(SRC)
 	@mkdir -p build
 	for f in $(SRC); do $(HIPCC) $(FLAGS) -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Spill|Occupancy|LDS" ; done
 
+# diagnostic build: kp_attn phase timestamps (s_memtime), kelpie_amd/libkelpie_hip_stamps.so
+stamps:
+	@mkdir -p build/stamps
+	for f in $(SRC); do $(HIPCC) $(FLAGS) -DKP_ATTN_STAMPS -c $$f -o build/stamps/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o kelpie_amd/libkelpie_hip_stamps.so build/stamps/*.o $(patsubst kelpie_amd/csrc/%.cpp,build/%.cpp.o,$(CPP))
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean resources
+.PHONY: all clean resources stamps

@@ -6,6 +6,15 @@
 
 namespace kpattn {
 
+#ifdef KP_ATTN_STAMPS
+// diagnostic build only (make stamps): per-phase issue cycles of kp_attn, summed
+// over waves: [S phase, softmax, O phase, tile end (DMA wait + barrier), tiles]
+__device__ unsigned long long g_attn_stamps[8];
+#define KP_STAMP(v) v = __builtin_amdgcn_s_memtime()
+#else
+#define KP_STAMP(v) (void)0
+#endif
+
 constexpr float kNegInf = -__builtin_huge_valf();
 
 // ----------------------------------------------------------------------------
@@ -173,7 +182,14 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+#ifdef KP_ATTN_STAMPS
+    unsigned long long st_acc[4] = {0, 0, 0, 0};
+#endif
     for (int t = 0; t < ntiles; ++t) {
+#ifdef KP_ATTN_STAMPS
+      unsigned long long ts0, ts1, ts2, ts3, ts4;
+#endif
+      KP_STAMP(ts0);
       const int k0 = key_begin + t * KT;
       // ---- S^T per 16-entity sub-tile u: sc[u][r] = q_c . E[k0 + 16u + 4g + r]
       const uint32_t sbase = lds0 + 4u * (uint32_t)((t & 1) * (KT * S) + c * S + 4 * g);
@@ -201,9 +217,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
 #pragma unroll
           for (int u = 0; u < NSUB; ++u) sc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][i], qv[j][i], sc[u], 0, 0, 0);
       }
-      // next tile's LDS-DMA (after the last tile it reloads clamped rows into the idle
-      // buffer: harmless and branch-free); issued while the last S MFMAs drain
+      // next tile's LDS-DMA, issued while the last S MFMAs drain (after the last tile
+      // it reloads clamped rows into the idle buffer: harmless and branch-free)
+#ifndef KP_ATTN_NODMA  // diagnostic: isolates the DMA issue cost (wrong results)
       issue(t + 1, (t + 1) & 1);
+#endif
+      KP_STAMP(ts1);
       float pw[NSUB][4];
       if (MODE == ATT_BCE_O) {
 #pragma unroll
@@ -238,6 +257,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
         }
         l_run += lt;
       }
+      KP_STAMP(ts2);
       if (WITH_O) {
         // O^T += E^T P over the KT entities: k-step rr takes entity 16(rr/4) + 4g + rr%4.
         // A-operand lane (i = c, k = g) of block j is E[entity][od(j, c)]: 4 consecutive
@@ -279,10 +299,24 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
           }
         }
       }
+      KP_STAMP(ts3);
       // tile t+1 landed (each wave waits for its own DMA) and every wave is done with buffer t&1
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      KP_STAMP(ts4);
+#ifdef KP_ATTN_STAMPS
+      st_acc[0] += ts1 - ts0;
+      st_acc[1] += ts2 - ts1;
+      st_acc[2] += ts3 - ts2;
+      st_acc[3] += ts4 - ts3;
+#endif
     }
+#ifdef KP_ATTN_STAMPS
+    if (lane == 0) {
+      for (int k = 0; k < 4; ++k) atomicAdd(&g_attn_stamps[k], st_acc[k]);
+      atomicAdd(&g_attn_stamps[4], (unsigned long long)ntiles);
+    }
+#endif
     if (MODE == ATT_BCE_O) break;
     // exact max of the query; a second pass only if some weight exceeded e^kMargin
     float mq = fmaxf(m_seen, __shfl_xor(m_seen, 16, 64));

@@ -673,3 +673,14 @@ void complex_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* r
   KP_HIP(hipMemcpyAsync(out, dS, sizeof(float) * (size_t)n * c->n_ent, hipMemcpyDeviceToHost, c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
 }
+
+#ifdef KP_ATTN_STAMPS
+extern "C" int kp_debug_attn_stamps(unsigned long long* out, int reset) {
+  KP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(kpattn::g_attn_stamps), sizeof(unsigned long long) * 8));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    KP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kpattn::g_attn_stamps), z, sizeof(z)));
+  }
+  return 0;
+}
+#endif
