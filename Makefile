@@ -30,7 +30,7 @@ resources: $(SRC)
 # diagnostic build: kp_attn phase timestamps (s_memtime), kelpie_amd/libkelpie_hip_stamps.so
 stamps:
 	@mkdir -p build/stamps
-	for f in $(SRC); do $(HIPCC) $(FLAGS) -DKP_ATTN_STAMPS -c $$f -o build/stamps/$$(basename $$f .hip).o || exit 1; done
+	for f in $(SRC); do $(HIPCC) $(FLAGS) -DKP_ATTN_STAMPS -DKP_TE_STAMPS -c $$f -o build/stamps/$$(basename $$f .hip).o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o kelpie_amd/libkelpie_hip_stamps.so build/stamps/*.o $(patsubst kelpie_amd/csrc/%.cpp,build/%.cpp.o,$(CPP))
 
 clean:

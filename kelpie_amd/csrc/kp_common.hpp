@@ -134,6 +134,17 @@ static inline T* upload(kp_ctx* c, DevBuf& b, const T* src, size_t n) {
 // ----------------------------------------------------------------------------
 // device helpers
 // ----------------------------------------------------------------------------
+// Sum over each 16-lane row with DPP (VALU lane moves, no LDS round trip):
+// xor 1, xor 2 (quad_perm), half-mirror (quads of 8), mirror (halves of 16).
+// Every lane of the row ends with the same bits (each step adds a symmetric pair).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -36,7 +36,17 @@ struct TeHp {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-constexpr int TE_CH = 256;  // stepped pairs whose descriptors are staged in LDS at a time
+constexpr int TE_CH = 256;
+constexpr int TE_PPG = 2;  // pairs in flight per 16-lane group (all their row loads issued before the math)
+
+#ifdef KP_TE_STAMPS
+// diagnostic build only: per-phase cycles of kp_te_posttrain summed over wave 0 of
+// every workgroup: [staging, pairs, chunk sync, reduce + Adam]
+__device__ unsigned long long g_te_stamps[8];
+#define TE_STAMP(k) te_ts[k] = __builtin_amdgcn_s_memtime()
+#else
+#define TE_STAMP(k) (void)0
+#endif  // stepped pairs whose descriptors are staged in LDS at a time
 
 // one (positive, negative) pair: the two difference vectors of 16 lanes x VPL float4
 template <int VPL>
@@ -45,22 +55,40 @@ struct TePair {
   float sp, sn;
 };
 
+// Row loads of one pair.  Frozen rows come from global memory (global_load, the
+// kelpie id K replaced by row 0) and the kelpie row from LDS, selected per value:
+// one flat load per row would let a 16-lane group's pointer alias either space.
 template <int VPL>
-__device__ __forceinline__ void te_load(TePair<VPL>& P, const float* Lp, const float* Rp, const float* Ln,
-                                        const float* Rn, const float* rel, int l16, int NF4) {
+__device__ __forceinline__ void te_load(TePair<VPL>& P, const float* __restrict__ E,
+                                        const float* __restrict__ Rt, const float* xs, int dp, int K, int4 dsc,
+                                        int tn, int l16, int NF4) {
+  const int h = dsc.x, r = dsc.y, t = dsc.z, hn = dsc.w;
+  const float* Lp = E + (size_t)(h == K ? 0 : h) * dp;
+  const float* Rp = E + (size_t)(t == K ? 0 : t) * dp;
+  const float* Ln = E + (size_t)(hn == K ? 0 : hn) * dp;
+  const float* Rn = E + (size_t)(tn == K ? 0 : tn) * dp;
+  const float* rel = Rt + (size_t)r * dp;
   P.sp = 0.f;
   P.sn = 0.f;
+  // branch-free: lanes past the row end load a clamped duplicate and are zeroed, so
+  // every pair's loads sit in one basic block and can all be in flight together
 #pragma unroll
   for (int u = 0; u < VPL; ++u) {
-    const int f = l16 + 16 * u;
-    if (f < NF4) {
-      const float4 a = ld4(Lp + 4 * f), b = ld4(rel + 4 * f), c = ld4(Rp + 4 * f);
-      const float4 a2 = ld4(Ln + 4 * f), c2 = ld4(Rn + 4 * f);
-      P.vp[u] = make_float4((a.x + b.x) - c.x, (a.y + b.y) - c.y, (a.z + b.z) - c.z, (a.w + b.w) - c.w);
-      P.vn[u] = make_float4((a2.x + b.x) - c2.x, (a2.y + b.y) - c2.y, (a2.z + b.z) - c2.z, (a2.w + b.w) - c2.w);
-    } else {
-      P.vp[u] = P.vn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    const int f0 = l16 + 16 * u;
+    const bool on = f0 < NF4;
+    const int f = on ? f0 : NF4 - 1;
+    const float4 xk = ld4(xs + 4 * f);
+    float4 a = ld4(Lp + 4 * f), c = ld4(Rp + 4 * f), a2 = ld4(Ln + 4 * f), c2 = ld4(Rn + 4 * f);
+    const float4 b = ld4(rel + 4 * f);
+    if (h == K) a = xk;
+    if (t == K) c = xk;
+    if (hn == K) a2 = xk;
+    if (tn == K) c2 = xk;
+    const float4 vp = make_float4((a.x + b.x) - c.x, (a.y + b.y) - c.y, (a.z + b.z) - c.z, (a.w + b.w) - c.w);
+    const float4 vn = make_float4((a2.x + b.x) - c2.x, (a2.y + b.y) - c2.y, (a2.z + b.z) - c2.z, (a2.w + b.w) - c2.w);
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    P.vp[u] = on ? vp : z;
+    P.vn[u] = on ? vn : z;
   }
 }
 
@@ -72,11 +100,8 @@ __device__ __forceinline__ void te_accum(TePair<VPL>& P, const int4 dsc, int tn,
     P.sp += P.vp[u].x * P.vp[u].x + P.vp[u].y * P.vp[u].y + P.vp[u].z * P.vp[u].z + P.vp[u].w * P.vp[u].w;
     P.sn += P.vn[u].x * P.vn[u].x + P.vn[u].y * P.vn[u].y + P.vn[u].z * P.vn[u].z + P.vn[u].w * P.vn[u].w;
   }
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) {
-    P.sp += __shfl_xor(P.sp, o, 16);
-    P.sn += __shfl_xor(P.sn, o, 16);
-  }
+  P.sp = row16_sum(P.sp);
+  P.sn = row16_sum(P.sn);
   const int h = dsc.x, t = dsc.z, hn = dsc.w;
   const float fp = sqrtf(P.sp), fn = sqrtf(P.sn);
   const float z = (fp - fn) + margin;
@@ -96,7 +121,7 @@ __device__ __forceinline__ void te_accum(TePair<VPL>& P, const int4 dsc, int tn,
 }
 
 template <int VPL>  // float4 per lane (16 lanes per row): DP <= 64 * VPL
-__global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d, const float* __restrict__ E,
+__global__ __launch_bounds__(256, 2) void kp_te_posttrain(int n_ent, int dp, int d, const float* __restrict__ E,
                                                        const float* __restrict__ R,
                                                        const TeSlot* __restrict__ slots,
                                                        const int32_t* __restrict__ rows,
@@ -120,6 +145,9 @@ __global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d,
   const int32_t* rw = rows + 3 * (size_t)S.row_off;
   const int NF4 = dp / 4;
   double b1t = 1.0, b2t = 1.0;
+#ifdef KP_TE_STAMPS
+  unsigned long long te_ts[5] = {0, 0, 0, 0, 0}, te_acc[4] = {0, 0, 0, 0}, te_wait = 0, te_rounds = 0;
+#endif
   for (int e = 0; e < hp.epochs; ++e) {
     const int32_t* order = rng + S.rng_off + (long long)e * 3 * S.R;
     const int32_t* ents = order + S.R;
@@ -131,6 +159,7 @@ __global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d,
       for (int u = 0; u < VPL; ++u) g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       int cnt = 0;
       for (int c0 = st; c0 < st + B; c0 += TE_CH) {
+        TE_STAMP(0);
         const int n = min(TE_CH, st + B - c0);
         // ---- stage the chunk's pair descriptors (coalesced draws, row gathers from L2)
         for (int k = tid; k < n; k += 256) {
@@ -143,25 +172,36 @@ __global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d,
           dtn[k] = corrupt_head ? t : ent;
         }
         __syncthreads();
-        // ---- two pairs per group in flight: all ten row loads issued before the math
-        for (int k = grp; k < n; k += 32) {
-          const bool two = k + 16 < n;
-          const int4 da = dsc[k];
-          const int ta = dtn[k];
-          const int4 db = two ? dsc[k + 16] : da;
-          const int tb = two ? dtn[k + 16] : ta;
-          TePair<VPL> A, Bp;
-          te_load<VPL>(A, (da.x == K) ? xs : E + (size_t)da.x * dp, (da.z == K) ? xs : E + (size_t)da.z * dp,
-                       (da.w == K) ? xs : E + (size_t)da.w * dp, (ta == K) ? xs : E + (size_t)ta * dp,
-                       R + (size_t)da.y * dp, l16, NF4);
-          te_load<VPL>(Bp, (db.x == K) ? xs : E + (size_t)db.x * dp, (db.z == K) ? xs : E + (size_t)db.z * dp,
-                       (db.w == K) ? xs : E + (size_t)db.w * dp, (tb == K) ? xs : E + (size_t)tb * dp,
-                       R + (size_t)db.y * dp, l16, NF4);
-          te_accum<VPL>(A, da, ta, K, hp.margin, g, cnt);
-          if (two) te_accum<VPL>(Bp, db, tb, K, hp.margin, g, cnt);
+        TE_STAMP(1);
+        // ---- TE_PPG pairs per group in flight: all their row loads issued before the math
+        for (int k0 = grp; k0 < n; k0 += 16 * TE_PPG) {
+          TePair<VPL> P[TE_PPG];
+          int4 dd[TE_PPG];
+          int tt[TE_PPG];
+#pragma unroll
+          for (int u = 0; u < TE_PPG; ++u) {
+            const int k = min(k0 + 16 * u, n - 1);  // past the chunk: reload a valid pair, not accumulated
+            dd[u] = dsc[k];
+            tt[u] = dtn[k];
+            te_load<VPL>(P[u], E, R, xs, dp, K, dd[u], tt[u], l16, NF4);
+          }
+#ifdef KP_TE_STAMPS
+          const unsigned long long r0 = __builtin_amdgcn_s_memtime();
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          const unsigned long long r1 = __builtin_amdgcn_s_memtime();
+          te_wait += r1 - r0;
+#endif
+#pragma unroll
+          for (int u = 0; u < TE_PPG; ++u)
+            if (k0 + 16 * u < n) te_accum<VPL>(P[u], dd[u], tt[u], K, hp.margin, g, cnt);
+#ifdef KP_TE_STAMPS
+          te_rounds += 1;
+#endif
         }
+        TE_STAMP(2);
         __syncthreads();  // the next chunk overwrites the descriptors
       }
+      TE_STAMP(3);
       // ---- reduce the 16 group partials
 #pragma unroll
       for (int u = 0; u < VPL; ++u) {
@@ -197,9 +237,27 @@ __global__ __launch_bounds__(256) void kp_te_posttrain(int n_ent, int dp, int d,
       __syncthreads();
       for (int i = tid; i < dp; i += 256) xs[i] = red[i];
       __syncthreads();
+      TE_STAMP(4);
+#ifdef KP_TE_STAMPS
+      te_acc[0] += te_ts[1] - te_ts[0];
+      te_acc[1] += te_ts[2] - te_ts[1];
+      te_acc[2] += te_ts[3] - te_ts[2];
+      te_acc[3] += te_ts[4] - te_ts[3];
+#endif
     }
   }
   for (int i = tid; i < dp; i += 256) x[i] = xs[i];
+#ifdef KP_TE_STAMPS
+  if (tid == 0) {
+    for (int k = 0; k < 2; ++k) atomicAdd(&g_te_stamps[k], te_acc[k]);
+    atomicAdd(&g_te_stamps[4], 1ull);
+    atomicAdd(&g_te_stamps[5], (unsigned long long)S.R);
+    atomicMax(&g_te_stamps[6], te_acc[0] + te_acc[1] + te_acc[2] + te_acc[3]);
+    atomicMax(&g_te_stamps[7], (unsigned long long)S.R);
+    atomicAdd(&g_te_stamps[2], te_wait);    // (reuses the chunk-sync slot: load wait inside the pair loop)
+    atomicAdd(&g_te_stamps[3], te_rounds);  // (reuses the reduce slot: rounds)
+  }
+#endif
 }
 
 // scores[q][e] = || (lhs_q + rel_q) - E_e ||_2 for e < n_ent (transe.py:48-65);
@@ -384,3 +442,14 @@ void transe_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* re
   KP_HIP(hipMemcpyAsync(out, dS, sizeof(float) * (size_t)n * c->n_ent, hipMemcpyDeviceToHost, c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
 }
+
+#ifdef KP_TE_STAMPS
+extern "C" int kp_debug_te_stamps(unsigned long long* out, int reset) {
+  KP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_te_stamps), sizeof(unsigned long long) * 8));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    KP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_te_stamps), z, sizeof(z)));
+  }
+  return 0;
+}
+#endif
