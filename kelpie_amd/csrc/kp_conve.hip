@@ -696,3 +696,15 @@ void conve_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rel
   KP_HIP(hipStreamSynchronize(c->stream));
   for (DevBuf* b : {&bh, &br, &bs}) b->release();
 }
+
+#ifdef KP_ATTN_STAMPS
+// the ConvE translation unit's copy of kpattn::g_attn_stamps (device globals are per code object)
+extern "C" int kp_debug_attn_stamps_conve(unsigned long long* out, int reset) {
+  KP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(kpattn::g_attn_stamps), sizeof(unsigned long long) * 8));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    KP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(kpattn::g_attn_stamps), z, sizeof(z)));
+  }
+  return 0;
+}
+#endif

@@ -24,14 +24,15 @@ eng = NecessaryPostTrainingEngine(model, ds, wl["hp"])
 preds = bench.pick_preds(ds, 2 * wl["preds_per_step"], seed=1234)
 bench.seed_all(42)
 L = _lib.lib()
-L.kp_debug_attn_stamps.argtypes = [C.c_void_p, C.c_int]
+fn = L.kp_debug_attn_stamps_conve if wl["model"] == "ConvE" else L.kp_debug_attn_stamps
+fn.argtypes = [C.c_void_p, C.c_int]
 buf = (C.c_ulonglong * 8)()
 k = wl["preds_per_step"]
 for i in range(2):
     eng.set_cache()
     eng.compute_relevance_multi([(p, [[c] for c in bench.candidates_of(ds, p, wl["candidates"])])
                                  for p in preds[i * k:(i + 1) * k]])
-    L.kp_debug_attn_stamps(buf, 1)
+    fn(buf, 1)
     tiles = max(1, buf[4])
     names = ["S+DMA issue", "softmax", "O phase", "tile end"]
     tot = sum(buf[j] for j in range(4))
