@@ -172,11 +172,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    import torch
     from kelpie_amd import distributed as kd
     from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine
     rank, world, local = kd.init_from_env()
     wl = WORKLOADS[args.workload]
-    ds, model, weights = build(wl, local, rank)
+    # one GPU per rank; on a box with fewer GPUs than ranks (gloo rehearsal) they share
+    device = local % max(1, torch.cuda.device_count()) if torch.cuda.is_available() else 0
+    ds, model, weights = build(wl, device, rank)
     engine_cls = SufficientPostTrainingEngine if wl["mode"] == "sufficient" else NecessaryPostTrainingEngine
     eng = engine_cls(model, ds, wl["hp"])
 
@@ -185,7 +188,6 @@ def main():
     all_preds = pick_preds(ds, world * n_steps * per_step, seed=1234)
     my_preds = kd.shard(all_preds, rank, world)
     import random
-    import torch
     random.seed(42)
     np.random.seed(42)
     torch.manual_seed(42)
