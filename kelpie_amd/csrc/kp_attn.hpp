@@ -2,6 +2,8 @@
 // shared by the ComplEx (softmax cross-entropy) and ConvE (sigmoid BCE)
 // post-training steps.
 #pragma once
+#include <algorithm>
+
 #include "kp_common.hpp"
 
 namespace kpattn {
@@ -101,9 +103,23 @@ __device__ __forceinline__ float tied(float v) {
 enum { ATT_SOFTMAX_O = 0, ATT_SOFTMAX = 1, ATT_BCE_O = 2 };
 constexpr float kMargin = 40.0f;  // max exponent s - m_ref of a pass-1 weight (e^40 * N * |E| << FLT_MAX)
 
+// Work partition (stream-K style): the (64-query tile, 32-entity key tile) iterations
+// of all query tiles, in query-tile-major order, are cut into equal contiguous
+// ranges of per_wg iterations, one per workgroup, with exactly as many workgroups
+// as the GPU holds at once.  A workgroup's range covers key-tile segments of one or
+// more query tiles; each segment writes a partial (m, l, O) into slot `part` of its
+// query tile, and the owner of a tile's last segment fills the unused slots up to
+// n_parts with empty partials (m = -inf, l = 0, O = 0).  Consumers merge n_parts
+// partials per query exactly as they merged N-split partials.
+struct AttnWork {
+  int ktq;      // key tiles per query tile, ceil(n_ent / 32)
+  int per_wg;   // iterations per workgroup
+  int n_parts;  // partial slots per query
+};
+
 template <int DB, int MODE>
 __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, int n_ent,
-                                                  const float* __restrict__ Qpre, int nq, int keys_per_split,
+                                                  const float* __restrict__ Qpre, int nq, AttnWork wk,
                                                   float* __restrict__ out_m, float* __restrict__ out_l,
                                                   float* __restrict__ out_O, const float* __restrict__ qscale,
                                                   float ylo) {
@@ -127,13 +143,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
-  const int q = blockIdx.x * 64 + 16 * w + c;
-  const bool valid = q < nq;
-  const int split = blockIdx.y;
-  const int key_begin = split * keys_per_split;
-  const int key_end = min(n_ent, key_begin + keys_per_split);
-  const int nkeys = max(0, key_end - key_begin);
-  const int ntiles = (nkeys + KT - 1) / KT;
+  int key_begin = 0, key_end = 0;  // the current segment's keys (captured by the DMA lambdas)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
 
   // LDS-DMA staging: piece (row, seg) = 64 lanes x 16 B of one entity row, landing at
@@ -155,6 +165,20 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
 #pragma unroll
     for (int p = 0; p < PIECES; ++p) issue_piece(tile, buf, p);
   };
+  const int QT = (nq + 63) / 64;
+  const long long total = (long long)QT * wk.ktq;
+  long long it = (long long)blockIdx.x * wk.per_wg;
+  const long long it_end = min(total, it + (long long)wk.per_wg);
+  while (it < it_end) {  // the segments of this workgroup's range (uniform across waves)
+  const int qt = (int)(it / wk.ktq);
+  const int kt0 = (int)(it - (long long)qt * wk.ktq);
+  const int kt1 = (int)min((long long)wk.ktq, (long long)kt0 + (it_end - it));
+  const int part = (int)blockIdx.x - (int)(((long long)qt * wk.ktq) / wk.per_wg);
+  key_begin = kt0 * KT;
+  key_end = min(n_ent, kt1 * KT);
+  const int ntiles = kt1 - kt0;
+  const int q = qt * 64 + 16 * w + c;
+  const bool valid = q < nq;
   // ---- Q fragment -> registers
   float qv[DB][4];
   float gsc = 0.f;
@@ -332,7 +356,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
   float l_tot = l_run + __shfl_xor(l_run, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
   if (valid) {
-    const size_t o = (size_t)split * nq + q;
+    const size_t o = (size_t)part * nq + q;
     if (g == 0 && MODE != ATT_BCE_O) {
       out_m[o] = m_ref;
       out_l[o] = l_tot;
@@ -352,6 +376,48 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
       }
     }
   }
+  // the owner of a query tile's last segment marks the unused partial slots empty
+  if (kt1 == wk.ktq && valid) {
+    for (int pp = part + 1; pp < wk.n_parts; ++pp) {
+      const size_t o = (size_t)pp * nq + q;
+      if (g == 0 && MODE != ATT_BCE_O) {
+        out_m[o] = kNegInf;
+        out_l[o] = 0.f;
+      }
+      if (WITH_O) {
+        float* dst = out_O + o * DP;
+        for (int d = 4 * g; d < DP; d += 16) *reinterpret_cast<float4*>(dst + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  it += kt1 - kt0;
+  }
+}
+
+// Host: the stream-K partition for nq queries over n_ent keys on `slots` co-resident
+// workgroups.  A workgroup takes at least ktq/15 key tiles, so a query tile is cut
+// into at most 16 partials (the consumers' merge limit).
+struct AttnPlan {
+  AttnWork wk;
+  int n_wg;
+};
+inline AttnPlan attn_plan(int nq, int n_ent, int slots) {
+  const int QT = (nq + 63) / 64, ktq = (n_ent + 31) / 32;
+  const long long total = (long long)QT * ktq;
+  long long per = (total + slots - 1) / slots;
+  per = std::max<long long>(per, (ktq + 14) / 15);
+  per = std::max<long long>(per, 1);
+  AttnPlan p{};
+  p.n_wg = (int)((total + per - 1) / per);
+  p.wk.ktq = ktq;
+  p.wk.per_wg = (int)per;
+  int parts = 1;
+  for (int qt = 0; qt < QT; ++qt) {
+    const long long w0 = ((long long)qt * ktq) / per, w1 = ((long long)(qt + 1) * ktq - 1) / per;
+    parts = std::max(parts, (int)(w1 - w0 + 1));
+  }
+  p.wk.n_parts = parts;
+  return p;
 }
 
 // LDS bytes of kp_attn<DB, *>

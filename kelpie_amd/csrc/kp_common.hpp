@@ -102,24 +102,6 @@ struct kp_ctx {
   }
 };
 
-// N-split of an attention pass over the n_ent frozen rows for nq queries (64 per
-// workgroup, one workgroup per CU): fill the CUs in as few rounds as possible,
-// charging each extra split a small combine cost.
-inline int kp_choose_split(const kp_ctx* c, int nq, int max_split) {
-  const int tiles = (nq + 63) / 64;
-  int best = 1;
-  double best_t = 1e300;
-  for (int s = 1; s <= max_split; ++s) {
-    if (c->n_ent / s < 256 && s > 1) break;
-    const int rounds = (tiles * s + c->n_cu - 1) / c->n_cu;
-    const double t = rounds * ((double)c->n_ent / s) + 0.02 * c->n_ent * (s - 1) * tiles / (double)c->n_cu;
-    if (t < best_t) {
-      best_t = t;
-      best = s;
-    }
-  }
-  return best;
-}
 
 static inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 

@@ -280,18 +280,21 @@ void launch_stepq(kp_ctx* c, const int4* stepq, const float* X, int nq, float* Q
   KP_HIP(hipGetLastError());
 }
 
+// co-resident attention workgroups: LDS and registers allow two per CU for rows up
+// to 208 floats, one for wider rows
+inline int attn_slots(const kp_ctx* c, int DB) { return c->n_cu * (DB <= 13 ? 2 : 1); }
+
 template <int DB>
-void launch_attn(kp_ctx* c, bool with_o, const float* Q, int nq, int n_split, float* m, float* l, float* O) {
+void launch_attn(kp_ctx* c, bool with_o, const float* Q, int nq, const AttnPlan& plan, float* m, float* l,
+                 float* O) {
   if (nq <= 0) return;
-  const int keys_per_split = (c->n_ent + n_split - 1) / n_split;
-  dim3 grid((nq + 63) / 64, n_split);
   const size_t shm = attn_lds_bytes(DB);
   if (with_o)
-    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX_O>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, Q, nq,
-                       keys_per_split, m, l, O, nullptr, 0.f);
+    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX_O>), dim3(plan.n_wg), dim3(256), shm, c->stream, c->dE, c->n_ent, Q,
+                       nq, plan.wk, m, l, O, nullptr, 0.f);
   else
-    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX>), grid, dim3(256), shm, c->stream, c->dE, c->n_ent, Q, nq,
-                       keys_per_split, m, l, O, nullptr, 0.f);
+    hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX>), dim3(plan.n_wg), dim3(256), shm, c->stream, c->dE, c->n_ent, Q,
+                       nq, plan.wk, m, l, O, nullptr, 0.f);
   KP_HIP(hipGetLastError());
 }
 
@@ -525,25 +528,24 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     KP_HIP(hipGetLastError());
   }
   // frozen-head pairs: q and frozen log-sum-exp
-  const int n_split_max = UPD_MAXSPLIT;
-  const int split_pairs = kp_choose_split(c, npairs, UPD_MAXSPLIT);
-  const int split_step = kp_choose_split(c, max_nq, UPD_MAXSPLIT);
+  const AttnPlan plan_pairs = attn_plan(std::max(npairs, 1), c->n_ent, attn_slots(c, DBV));
+  const int split_pairs = plan_pairs.wk.n_parts;
   size_t att_rows = (size_t)std::max(npairs, 1) * split_pairs;
+  std::vector<AttnPlan> step_plan(T);
   for (int t = 0; t < T; ++t) {
     const int nq = q_off[t + 1] - q_off[t];
-    att_rows = std::max(att_rows, (size_t)nq * kp_choose_split(c, nq, UPD_MAXSPLIT));
+    step_plan[t] = attn_plan(std::max(nq, 1), c->n_ent, attn_slots(c, DBV));
+    att_rows = std::max(att_rows, (size_t)nq * step_plan[t].wk.n_parts);
   }
-  (void)split_step;
   float* dAm = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * att_rows));
   float* dAl = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * att_rows));
   float* dAO = reinterpret_cast<float*>(c->ws[15].ensure(sizeof(float) * att_rows * DP));
   float* dQs = reinterpret_cast<float*>(c->ws[26].ensure(sizeof(float) * (size_t)std::max(max_nq, 1) * DP));
-  (void)n_split_max;
   if (npairs > 0) {
     hipLaunchKernelGGL(kp_cx_qpair, dim3(npairs), dim3(128), 0, c->stream, c->dE, c->dR, DP, half, dPairs, npairs,
                        dQpair);
     KP_HIP(hipGetLastError());
-    CX_DISPATCH(DBV, launch_attn<DB>(c, false, dQpair, npairs, split_pairs, dAm, dAl, nullptr));
+    CX_DISPATCH(DBV, launch_attn<DB>(c, false, dQpair, npairs, plan_pairs, dAm, dAl, nullptr));
     // combine splits into lsef (host-free: small kernel via update-style math on host is avoided)
     std::vector<float> hm((size_t)npairs * split_pairs), hl((size_t)npairs * split_pairs);
     KP_HIP(hipMemcpyAsync(hm.data(), dAm, sizeof(float) * hm.size(), hipMemcpyDeviceToHost, c->stream));
@@ -582,7 +584,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   for (int t = 0; t < T; ++t) {
     const int nq = q_off[t + 1] - q_off[t];
     const int na = act_off[t + 1] - act_off[t];
-    const int sp = kp_choose_split(c, nq, UPD_MAXSPLIT);
+    const int sp = step_plan[t].wk.n_parts;
     hipEvent_t ea = nullptr, eb = nullptr;
     if (nq > 0 && c->time_hot) {
       ea = c->event(2 * hot_launches);
@@ -590,7 +592,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     }
     CX_DISPATCH(DBV, launch_stepq<DB>(c, dStepQ + q_off[t], dX, nq, dQs));
     if (nq > 0 && c->time_hot) KP_HIP(hipEventRecord(ea, c->stream));
-    CX_DISPATCH(DBV, launch_attn<DB>(c, true, dQs, nq, sp, dAm, dAl, dAO));
+    CX_DISPATCH(DBV, launch_attn<DB>(c, true, dQs, nq, step_plan[t], dAm, dAl, dAO));
     if (nq > 0) {
       if (c->time_hot) {
         KP_HIP(hipEventRecord(eb, c->stream));

@@ -524,11 +524,13 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       KP_HIP(hipMemcpyAsync(dgs, gsv.data(), sizeof(float) * gsv.size(), hipMemcpyHostToDevice, c->stream));
     }
   }
-  constexpr int CV_MAXSPLIT = 16;
+  const int attn_slots = c->n_cu * (DBV <= 13 ? 2 : 1);  // co-resident attention workgroups
+  std::vector<AttnPlan> step_plan(T);
   size_t o_rows = 1;
   for (int t = 0; t < T; ++t) {
     const int nk = kin_off[t + 1] - kin_off[t];
-    o_rows = std::max(o_rows, (size_t)nk * kp_choose_split(c, nk, CV_MAXSPLIT));
+    step_plan[t] = attn_plan(std::max(nk, 1), K, attn_slots);
+    o_rows = std::max(o_rows, (size_t)nk * step_plan[t].wk.n_parts);
   }
   float* dO = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * o_rows * DP));
   float* ddfc = reinterpret_cast<float*>(c->ws[18].ensure(sizeof(float) * (size_t)mk * c->dim));
@@ -554,7 +556,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     const int na = act_o[t + 1] - act_o[t];
     const CvInst* KI = dKI + kin_off[t];
     if (nk > 0) {
-      const int n_split = kp_choose_split(c, nk, CV_MAXSPLIT);
+      const int n_split = step_plan[t].wk.n_parts;
       hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
                          kc, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
       KP_HIP(hipGetLastError());
@@ -569,10 +571,10 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
         eb = c->event(2 * launches + 1);
         KP_HIP(hipEventRecord(ea, c->stream));
       }
-      const int kps = (K + n_split - 1) / n_split;
-      dim3 grid((nk + 63) / 64, n_split);
+      dim3 grid(step_plan[t].n_wg);
 #define CV_ATT(DBX)                                                                                                  \
-  hipLaunchKernelGGL((kp_attn<DBX, ATT_BCE_O>), grid, dim3(256), shm_attn, c->stream, c->dE, K, dQ, nk, kps, \
+  hipLaunchKernelGGL((kp_attn<DBX, ATT_BCE_O>), grid, dim3(256), shm_attn, c->stream, c->dE, K, dQ, nk,            \
+                     step_plan[t].wk,                                                                                 \
                      nullptr, nullptr, dO, dgs + kin_off[t], kc.ylo)
       switch (DBV) {
         case 4: CV_ATT(4); break;
