@@ -153,6 +153,17 @@ int kp_all_scores(kp_ctx* ctx, int32_t n, const int32_t* heads, const int32_t* r
 int kp_convertible(kp_ctx* ctx, int32_t n, const int32_t* heads, int32_t rel, int32_t obj,
                    const int32_t* filt_off, const int32_t* filt, uint8_t* keep);
 
+/* Model.predict_tails (src/link_prediction/models/model.py:42-68; ConvE:
+ * conve.py:160-184) for n frozen triples (h, r, t), r in [0, n_rel2) (inverse
+ * relations give head prediction, model.py:30-31): out_score[i] = score of t,
+ * out_rank[i] = filtered rank of t among all entities with to_filter[(h, r)]
+ * (CSR as in kp_batch) masked to +-1e6 and t restored, counting <= (TransE) or
+ * >= (ComplEx) the target; ConvE ranks by a descending sort with filtered
+ * entries at 0.0, i.e. 1 + #(scores > target).  The Evaluator's MRR / Hits@k
+ * (link_prediction/evaluation.py:16-48) are computed from these ranks. */
+int kp_predict_tails(kp_ctx* ctx, int32_t n, const int32_t* triples, const int32_t* filt_off, const int32_t* filt,
+                     float* out_score, int64_t* out_rank);
+
 /* Advance a torch CPU generator state (the 5056-byte torch.get_rng_state()
  * blob) by n 32-bit mt19937 outputs, in place.  Used by the host RNG protocol
  * to replay the draws of reset_parameters() that each KelpieConvE

@@ -20,7 +20,8 @@ KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
 EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_rank", "kp_all_scores",
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
            "kp_rng_transe_epochs", "kp_rng_conve_masks", "kp_graph_create", "kp_graph_destroy",
-           "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs"]
+           "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
+           "kp_predict_tails"]
 
 
 class ModelDesc(C.Structure):
@@ -65,6 +66,8 @@ def lib():
         L.kp_convertible.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
                                      C.c_void_p, C.c_void_p]
         L.kp_mt19937_discard.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.kp_predict_tails.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]
         L.kp_graph_create.argtypes = [C.c_int32, C.c_int64, C.c_void_p, C.POINTER(C.c_void_p)]
         L.kp_graph_destroy.argtypes = [C.c_void_p]
         L.kp_graph_destroy.restype = None
@@ -196,6 +199,17 @@ class Context:
         check(lib().kp_convertible(self.h, len(heads), _ptr(heads), int(rel), int(obj), _ptr(filt_off),
                                    _ptr(filt), _ptr(keep)), self.h)
         return keep
+
+    def predict_tails(self, triples, filt_off, filt):
+        """kp_predict_tails: (target scores float32, filtered ranks int64) per triple."""
+        t = np.ascontiguousarray(np.asarray(triples, dtype=np.int32).reshape(-1, 3))
+        filt_off = np.ascontiguousarray(filt_off, dtype=np.int32)
+        filt = np.ascontiguousarray(filt, dtype=np.int32) if len(filt) else np.zeros(1, np.int32)
+        score = np.zeros(len(t), np.float32)
+        rank = np.zeros(len(t), np.int64)
+        check(lib().kp_predict_tails(self.h, len(t), _ptr(t), _ptr(filt_off), _ptr(filt), _ptr(score), _ptr(rank)),
+              self.h)
+        return score, rank
 
     def last_timing(self):
         a, b, n, w = C.c_double(), C.c_double(), C.c_int64(), C.c_double()

@@ -181,6 +181,57 @@ int kp_convertible(kp_ctx* c, int32_t n, const int32_t* heads, int32_t rel, int3
   });
 }
 
+int kp_predict_tails(kp_ctx* c, int32_t n, const int32_t* triples, const int32_t* filt_off, const int32_t* filt,
+                     float* out_score, int64_t* out_rank) {
+  if (!c || n < 0 || (n > 0 && (!triples || !filt_off || !out_score || !out_rank))) return KP_EINVAL;
+  return guarded(c, [&] {
+    if (n == 0) return;
+    KP_HIP(hipSetDevice(c->device));
+    for (int i = 0; i < n; ++i) {
+      KP_REQUIRE(triples[3 * i] >= 0 && triples[3 * i] < c->n_ent, "kp_predict_tails: head out of range");
+      KP_REQUIRE(triples[3 * i + 1] >= 0 && triples[3 * i + 1] < c->n_rel2, "kp_predict_tails: relation out of range");
+      KP_REQUIRE(triples[3 * i + 2] >= 0 && triples[3 * i + 2] < c->n_ent, "kp_predict_tails: tail out of range");
+      KP_REQUIRE(filt_off[i + 1] >= filt_off[i], "kp_predict_tails: bad filter offsets");
+    }
+    // Model.predict_tails (model.py:42-68) / ConvE.predict_tails (conve.py:160-184):
+    // score chunks of triples against every entity, then the filtered rank
+    const size_t budget = (size_t)256 << 20;
+    const int chunk = (int)std::max<size_t>(64, std::min<size_t>(4096, budget / ((size_t)c->n_ent * 4)));
+    const int ld = c->n_ent;
+    const int mode = (c->model == KP_MODEL_CONVE) ? RANK_SORT_POSITION : RANK_PREDICT_TAILS;
+    const bool minimizer = (c->model == KP_MODEL_TRANSE);
+    std::vector<int32_t> h(chunk), r(chunk), o(chunk), fo(chunk + 1);
+    DevBuf bS, bH, bR, bO, bFo, bF, bT, bK;
+    float* dS = reinterpret_cast<float*>(bS.ensure(sizeof(float) * (size_t)chunk * ld));
+    for (int i0 = 0; i0 < n; i0 += chunk) {
+      const int m = std::min(chunk, n - i0);
+      for (int j = 0; j < m; ++j) {
+        h[j] = triples[3 * (i0 + j)];
+        r[j] = triples[3 * (i0 + j) + 1];
+        o[j] = triples[3 * (i0 + j) + 2];
+      }
+      for (int j = 0; j <= m; ++j) fo[j] = filt_off[i0 + j] - filt_off[i0];
+      int32_t* dH = upload(c, bH, h.data(), (size_t)m);
+      int32_t* dR = upload(c, bR, r.data(), (size_t)m);
+      int32_t* dO = upload(c, bO, o.data(), (size_t)m);
+      int32_t* dFo = upload(c, bFo, fo.data(), (size_t)m + 1);
+      int32_t* dF = upload(c, bF, filt + filt_off[i0], (size_t)std::max(1, fo[m]));
+      float* dT = reinterpret_cast<float*>(bT.ensure(sizeof(float) * (size_t)m));
+      int64_t* dK = reinterpret_cast<int64_t*>(bK.ensure(sizeof(int64_t) * (size_t)m));
+      switch (c->model) {
+        case KP_MODEL_COMPLEX: complex_scores_dev(c, m, dH, dR, dS, ld); break;
+        case KP_MODEL_TRANSE: transe_scores_dev(c, m, dH, dR, dS, ld); break;
+        case KP_MODEL_CONVE: conve_scores_dev(c, m, dH, dR, dS, ld); break;
+      }
+      launch_rank_count(c, m, dS, ld, c->n_ent, dO, dFo, dF, minimizer ? 1 : 0, dT, dK, mode);
+      KP_HIP(hipMemcpyAsync(out_score + i0, dT, sizeof(float) * m, hipMemcpyDeviceToHost, c->stream));
+      KP_HIP(hipMemcpyAsync(out_rank + i0, dK, sizeof(int64_t) * m, hipMemcpyDeviceToHost, c->stream));
+      KP_HIP(hipStreamSynchronize(c->stream));
+    }
+    for (DevBuf* b : {&bS, &bH, &bR, &bO, &bFo, &bF, &bT, &bK}) b->release();
+  });
+}
+
 // MT19937 of ATen (aten/src/ATen/core/MT19937RNGEngine.h) over the legacy
 // CPU-generator state blob returned by torch.get_rng_state():
 //   { u64 seed; i32 left; i32 seeded; u64 next; u64 state[624]; ... }.

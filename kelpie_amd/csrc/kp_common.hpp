@@ -160,6 +160,8 @@ void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld,
 // out[z][m][n] = act(sum_{k in split z} A[m][k] B[n][k] + (z == 0 ? bias[n] : 0)), fp32 MFMA
 void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
                      int ldo, const float* bias, int act, int ksplit);
+enum { RANK_TRIPLE_RESULTS = 0, RANK_PREDICT_TAILS = 1, RANK_SORT_POSITION = 2 };
 void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
                        const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
-                       int minimizer, float* d_target, int64_t* d_rank);
+                       int minimizer, float* d_target, int64_t* d_rank,
+                       int mode = 0);

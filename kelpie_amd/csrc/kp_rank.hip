@@ -84,12 +84,20 @@ __global__ __launch_bounds__(256) void kp_gemm_abt(const float* __restrict__ A, 
 //   maximizer: v_e = -1e6 for e in F,             rank = #{v_e >= target}
 //   (post_training_engine.py:110-119; an o in F is excluded for maximizers)
 // ----------------------------------------------------------------------------
+// mode RANK_TRIPLE_RESULTS: PostTrainingEngine.get_triple_results (post_training_engine.py:101-125):
+//   minimizer: filtered -> 1e6, o restored, count <= target; maximizer: filtered ->
+//   -1e6 (o NOT restored when filtered), count >= target.
+// mode RANK_PREDICT_TAILS: Model.predict_tails (model.py:42-68): filtered -> +-1e6, o
+//   restored, count <= / >= target.
+// mode RANK_SORT_POSITION: ConvE.predict_tails (conve.py:160-184): filtered -> 0.0, o
+//   restored, rank = 1 + #(v > target), the position of o in a descending sort when
+//   no other entity ties with it (torch.sort's order among ties is unspecified).
 __global__ __launch_bounds__(256) void kp_rank_count(int n_slots, const float* __restrict__ scores, int ld,
                                                      int n_cols, const int32_t* __restrict__ pred_o,
                                                      const int32_t* __restrict__ filt_off,
                                                      const int32_t* __restrict__ filt, int minimizer,
                                                      float* __restrict__ target_out,
-                                                     int64_t* __restrict__ rank_out) {
+                                                     int64_t* __restrict__ rank_out, int mode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
   __shared__ int partial[4];
   const int s = blockIdx.x;
@@ -114,10 +122,19 @@ __global__ __launch_bounds__(256) void kp_rank_count(int n_slots, const float* _
       if (e == o) v = target;
       cnt += (v <= target) ? 1 : 0;
     }
+  } else if (mode == RANK_SORT_POSITION) {
+    for (int e = tid; e < n_cols; e += blockDim.x) {
+      float v = row[e];
+      if ((bits[e >> 5] >> (e & 31)) & 1u) v = 0.0f;
+      if (e == o) v = target;
+      cnt += (v > target) ? 1 : 0;
+    }
+    if (tid == 0) cnt += 1;
   } else {
     for (int e = tid; e < n_cols; e += blockDim.x) {
       float v = row[e];
       if ((bits[e >> 5] >> (e & 31)) & 1u) v = -1e6f;
+      if (mode == RANK_PREDICT_TAILS && e == o) v = target;
       cnt += (v >= target) ? 1 : 0;
     }
   }
@@ -135,12 +152,12 @@ __global__ __launch_bounds__(256) void kp_rank_count(int n_slots, const float* _
 
 void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
                        const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
-                       int minimizer, float* d_target, int64_t* d_rank) {
+                       int minimizer, float* d_target, int64_t* d_rank, int mode) {
   if (n_slots <= 0) return;
   size_t shm = (size_t)((n_cols + 31) / 32) * 4;
   KP_REQUIRE(shm <= 150 * 1024, "rank: too many entities for the LDS filter bitmap");
   hipLaunchKernelGGL(kp_rank_count, dim3(n_slots), dim3(256), shm, c->stream, n_slots, d_scores, ld, n_cols,
-                     d_pred_o, d_filt_off, d_filt, minimizer, d_target, d_rank);
+                     d_pred_o, d_filt_off, d_filt, minimizer, d_target, d_rank, mode);
   KP_HIP(hipGetLastError());
 }
 

@@ -56,6 +56,27 @@ class FrozenModel:
         t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
         return self.ctx.all_scores(t[:, 0], t[:, 1])
 
+    def predict_tails(self, triples):
+        """``Model.predict_tails`` (model.py:42-68; ConvE conve.py:160-184): target
+        scores and filtered ranks against ``dataset.to_filter``, on the device."""
+        t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        flt = [self.dataset.to_filter.get((int(h), int(r)), []) for h, r, _ in t.tolist()]
+        off = np.zeros(len(t) + 1, np.int32)
+        off[1:] = np.cumsum([len(f) for f in flt])
+        filt = np.array([e for f in flt for e in f], np.int32)
+        score, rank = self.ctx.predict_tails(t, off, filt)
+        return [float(x) for x in score], [int(x) for x in rank]
+
+    def predict_triples(self, triples):
+        """``Model.predict_triples`` (model.py:25-40): tail prediction on the triples,
+        head prediction on their inverses."""
+        direct = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        assert np.all(direct[:, 1] < self.dataset.num_relations)
+        direct_scores, tail_ranks = self.predict_tails(direct)
+        inverse_scores, head_ranks = self.predict_tails(self.dataset.invert_triples(direct))
+        return [{"score": {"tail": direct_scores[i], "head": inverse_scores[i]},
+                 "rank": {"tail": int(tail_ranks[i]), "head": int(head_ranks[i])}} for i in range(len(direct))]
+
     # ------------------------------------------------------------ kelpie hooks
     def kelpie_init(self, init: np.ndarray, rng: ReferenceRNG) -> np.ndarray:
         raise NotImplementedError

@@ -293,6 +293,33 @@ class OracleModel:
         return (1.0 / (1.0 + np.exp(-s.astype(np.float64)))).astype(F32)
 
 
+def predict_tails(om, dataset, triples):
+    """Model.predict_tails (model.py:42-68) / ConvE.predict_tails (conve.py:160-184):
+    target score and filtered rank of each triple's tail (f3, link-prediction eval)."""
+    t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+    sc = om.all_scores(t)
+    scores, ranks = [], []
+    for i, (h, r, o) in enumerate(t.tolist()):
+        row = sc[i].copy()
+        tgt = row[o]
+        F = list(dataset.to_filter.get((h, r), []))
+        if om.name == "ConvE":
+            row[F] = F32(0.0)
+            row[o] = tgt
+            rank = 1 + int((row > tgt).sum())  # descending-sort position (ties with o unordered)
+        elif om.name == "TransE":
+            row[F] = F32(1e6)
+            row[o] = tgt
+            rank = int((row <= tgt).sum())
+        else:
+            row[F] = F32(-1e6)
+            row[o] = tgt
+            rank = int((row >= tgt).sum())
+        scores.append(float(tgt))
+        ranks.append(rank)
+    return scores, ranks
+
+
 # =============================================================================
 # optimizers (torch semantics, float32)
 # =============================================================================

@@ -155,5 +155,9 @@ class OracleBackedContext:
                 keep[i] = 1 if (-1e6 < t < row.max()) else 0
         return keep
 
+    def predict_tails(self, triples, filt_off, filt):
+        sc, rk = ko.predict_tails(self.om, self.model.dataset, triples)
+        return np.array(sc, np.float32), np.array(rk, np.int64)
+
     def last_timing(self):
         return {"device_s": 0.0, "hot_s": 0.0, "hot_launches": 0}
