@@ -192,11 +192,24 @@ class PostTrainingEngine(RelevanceEngine):
 
     def _multi(self, items, checkpoints=None):
         t0 = time.perf_counter()
+        self._deferred_error = None
         slots, pending, jobs = self._schedule_multi(items, checkpoints)
         t_sched = time.perf_counter() - t0
         self._run(slots)
         self.last_batch_stats["schedule_s"] = t_sched
-        return self._finalize_multi(slots, pending, jobs)
+        outs = self._finalize_multi(slots, pending, jobs)
+        self._raise_deferred(slots, pending)
+        return outs
+
+    def _raise_deferred(self, slots, pending):
+        """Re-raise the reference's error of a call the batch stopped at, after caching
+        the base post-training it had already run (post_training_engine.py:46-62)."""
+        err, self._deferred_error = getattr(self, "_deferred_error", None), None
+        if err is None:
+            return
+        for key, i in pending.items():
+            self.base_pt_results.setdefault(key, slots[i].result)
+        raise err
 
     def compute_relevance_pipeline(self, batches):
         """Equivalent to ``[(self.set_cache(), self.compute_relevance_multi(b))[1] for b in batches]``
@@ -219,7 +232,7 @@ class PostTrainingEngine(RelevanceEngine):
 
         def finish(state):
             state["thread"].join()
-            if "error" in state:
+            if state.get("error") is not None:
                 raise state["error"]
             self.base_pt_results = {}
             o = self._finalize_multi(state["slots"], state["pending"], state["jobs"])
@@ -227,17 +240,24 @@ class PostTrainingEngine(RelevanceEngine):
             st["schedule_s"] = state["schedule_s"]
             stats.append(st)
             outs.append(o)
+            self._deferred_error = state.get("deferred")
+            self._raise_deferred(state["slots"], state["pending"])
 
         for items in batches:
             self.set_cache()
             t0 = time.perf_counter()
+            self._deferred_error = None
             slots, pending, jobs = self._schedule_multi(items, None)
+            err, self._deferred_error = self._deferred_error, None
             t_sched = time.perf_counter() - t0
             if inflight is not None:
                 finish(inflight)
-            inflight = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched}
+            inflight = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched, "error": None}
+            inflight["deferred"] = err
             inflight["thread"] = threading.Thread(target=run, args=(inflight,), daemon=True)
             inflight["thread"].start()
+            if err is not None:
+                break  # the sequential reference stops at the failing call
         if inflight is not None:
             finish(inflight)
         self.last_batch_stats = stats
@@ -263,7 +283,15 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
         for pred, rules in items:
             pj = []
             for rule in rules:
-                pj.append(self._schedule(pred, [tuple(t) for t in rule], "necessary", slots, pending))
+                rule = [tuple(t) for t in rule]
+                idx = self._schedule(pred, rule, "necessary", slots, pending)
+                if not rule:
+                    # KelpieDataset.undo_removal raises after the post-training
+                    # (kelpie_dataset.py:166-167): its draws are spent, nothing after it runs
+                    self._deferred_error = Exception("No removal to undo.")
+                    jobs.append(pj)
+                    return slots, pending, jobs
+                pj.append(idx)
                 if checkpoints is not None:
                     checkpoints.append(StateCheckpoint())
             jobs.append(pj)
@@ -309,15 +337,23 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
         for pred, rules, ents in items:
             pred = tuple(int(v) for v in pred)
             s = pred[0]
-            if not ents:
-                raise ZeroDivisionError("division by zero")  # sum([]) / len([]) in the reference
             pj = []
             for rule in rules:
+                if not ents:
+                    self._deferred_error = ZeroDivisionError("division by zero")  # sum([]) / len([])
+                    jobs.append(pj)
+                    return slots, pending, jobs
                 rj = []
                 for e in ents:
                     crule = Dataset.replace_entity_in_triples([tuple(t) for t in rule], s, e)
                     cpred = Dataset.replace_entity_in_triple(pred, s, e)
                     rj.append(self._schedule(cpred, crule, "sufficient", slots, pending))
+                    if not crule:
+                        # KelpieDataset.undo_addition raises after the first conversion's
+                        # post-training (kelpie_dataset.py:191-192)
+                        self._deferred_error = Exception("No addition to undo.")
+                        jobs.append(pj)
+                        return slots, pending, jobs
                 pj.append(rj)
                 if checkpoints is not None:
                     checkpoints.append(StateCheckpoint())
