@@ -41,6 +41,9 @@ COMPLEX_HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 43, "lr"
               "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0}  # ComplEx_DBpedia50_explanation.json
 TRANSE_HP = {"batch_size": 2048, "epochs": 65, "lr": 0.01, "margin": 5, "negative_triples_ratio": 5,
              "regularizer_weight": 1.0}  # TransE_DBpedia50_explanation.json
+COMPLEX_DB100K_HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 83, "lr": 0.0814, "decay1": 0.9,
+                     "decay2": 0.999, "regularizer_name": "N3",
+                     "regularizer_weight": 0}  # ComplEx_DB100K_explanation.json
 CONVE_HP = {"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.995,
             "epochs": 109}  # ConvE_DB100K_explanation.json (hidden dropout 0.2)
 
@@ -53,6 +56,11 @@ WORKLOADS = {
     # BASELINE.json configs[1]
     "transe-fb15k237-necessary": dict(model="TransE", shape="FB15k-237", dim=200, mode="necessary",
                                       hp=TRANSE_HP, candidates=20, preds_per_step=16),
+    # BASELINE.json configs[3] (necessary + sufficient; the 8-GPU sharding is bench.py --gpus N)
+    "complex-db100k-necessary": dict(model="ComplEx", shape="DB100K", dim=200, mode="necessary",
+                                     hp=COMPLEX_DB100K_HP, candidates=20, preds_per_step=16),
+    "complex-db100k-sufficient": dict(model="ComplEx", shape="DB100K", dim=200, mode="sufficient",
+                                      hp=COMPLEX_DB100K_HP, candidates=20, convert=10, preds_per_step=1),
     # BASELINE.json configs[4]
     "conve-yago310-necessary": dict(model="ConvE", shape="YAGO3-10", dim=200, mode="necessary", hp=CONVE_HP,
                                     candidates=20, preds_per_step=8, hidden_dropout=0.2),

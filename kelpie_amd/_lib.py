@@ -88,7 +88,10 @@ def lib():
 
 
 def _ptr(a):
-    return None if a is None else a.ctypes.data_as(C.c_void_p)
+    """Raw data address of a C-contiguous numpy array.  ``a.ctypes.data_as`` costs
+    15-40 us per call once torch is imported (most of the per-slot host time of
+    the TransE draws); the caller keeps ``a`` alive across the C call."""
+    return None if a is None else C.c_void_p(a.__array_interface__["data"][0])
 
 
 def check(rc, ctx=None):
@@ -115,7 +118,7 @@ def transe_epochs(torch_state: np.ndarray, np_key, np_pos, R: int, epochs: int,
                   ratio: int, n_entities: int) -> np.ndarray:
     """``np_key`` / ``np_pos``: numpy arrays, or raw addresses (int) of a live
     MT19937 ``key[624]`` / ``pos`` pair, which are then advanced in place."""
-    out = np.zeros(max(1, epochs * 3 * R), np.int32)
+    out = np.empty(max(1, epochs * 3 * R), np.int32)  # every element is written
     key = C.c_void_p(np_key) if isinstance(np_key, int) else _ptr(np_key)
     pos = C.c_void_p(np_pos) if isinstance(np_pos, int) else _ptr(np_pos)
     check(lib().kp_rng_transe_epochs(_ptr(torch_state), torch_state.size, key, pos, int(R),

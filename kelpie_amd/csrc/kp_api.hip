@@ -232,246 +232,7 @@ int kp_predict_tails(kp_ctx* c, int32_t n, const int32_t* triples, const int32_t
   });
 }
 
-// MT19937 of ATen (aten/src/ATen/core/MT19937RNGEngine.h) over the legacy
-// CPU-generator state blob returned by torch.get_rng_state():
-//   { u64 seed; i32 left; i32 seeded; u64 next; u64 state[624]; ... }.
-namespace {
-struct Mt {
-  int32_t left;
-  uint64_t next;
-  uint32_t s[624];
-  void load(const uint8_t* st) {
-    std::memcpy(&left, st + 8, 4);
-    std::memcpy(&next, st + 16, 8);
-    for (int i = 0; i < 624; ++i) {
-      uint64_t v;
-      std::memcpy(&v, st + 24 + 8 * i, 8);
-      s[i] = (uint32_t)v;
-    }
-  }
-  void store(uint8_t* st) const {
-    std::memcpy(st + 8, &left, 4);
-    std::memcpy(st + 16, &next, 8);
-    for (int i = 0; i < 624; ++i) {
-      uint64_t v = s[i];
-      std::memcpy(st + 24 + 8 * i, &v, 8);
-    }
-  }
-  void twist() {
-    constexpr int N = 624, M = 397;
-    // three dependency-free spans (distance >= N-M), written so the host
-    // compiler vectorises them
-#pragma clang loop vectorize(enable)
-    for (int i = 0; i < N - M; ++i) {
-      const uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
-      s[i] = s[i + M] ^ (y >> 1) ^ ((0u - (s[i + 1] & 1u)) & 0x9908b0dfu);
-    }
-#pragma clang loop vectorize(enable)
-    for (int i = N - M; i < N - 1; ++i) {
-      const uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
-      s[i] = s[i + M - N] ^ (y >> 1) ^ ((0u - (s[i + 1] & 1u)) & 0x9908b0dfu);
-    }
-    const uint32_t y = (s[N - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
-    s[N - 1] = s[M - 1] ^ (y >> 1) ^ ((0u - (s[0] & 1u)) & 0x9908b0dfu);
-  }
-  // tempered copy of the current block, refreshed after every twist
-  uint32_t tb[624];
-  bool tb_ok = false;
-  void temper_block() {
-#pragma clang loop vectorize(enable)
-    for (int i = 0; i < 624; ++i) {
-      uint32_t y = s[i];
-      y ^= (y >> 11);
-      y ^= (y << 7) & 0x9d2c5680u;
-      y ^= (y << 15) & 0xefc60000u;
-      y ^= (y >> 18);
-      tb[i] = y;
-    }
-    tb_ok = true;
-  }
-  // advance by n outputs (operator() semantics, nothing tempered)
-  void skip(uint64_t n) {
-    while (n > 0) {
-      const uint64_t k = std::min<uint64_t>(n, (uint64_t)(left - 1));
-      left -= (int32_t)k;
-      next += k;
-      n -= k;
-      if (n > 0) {
-        twist();
-        tb_ok = false;
-        left = 624;
-        next = 1;
-        n -= 1;
-      }
-    }
-  }
-  // the next n outputs, in order (operator() n times, block-wise)
-  void fill(uint32_t* out, size_t n) {
-    size_t k = 0;
-    while (k < n) {
-      if (left <= 1) {  // the next operator() call twists
-        twist();
-        temper_block();
-        left = 625;
-        next = 0;
-      }
-      if (!tb_ok) temper_block();
-      const size_t m = std::min<size_t>(n - k, (size_t)(left - 1));
-      std::memcpy(out + k, tb + next, sizeof(uint32_t) * m);
-      k += m;
-      next += m;
-      left -= (int32_t)m;
-    }
-  }
-  inline uint32_t operator()() {
-    if (--left == 0) {
-      twist();
-      left = 624;
-      next = 0;
-      tb_ok = false;
-    }
-    if (!tb_ok) temper_block();
-    return tb[next++];
-  }
-};
-}  // namespace
-
-// numpy's legacy MT19937 (numpy/random/src/mt19937): pos in [0, 624], regenerate at 624
-// a % d for 32-bit a, d >= 1 (Lemire, Kaser & Kurz 2019), fm = 2^64 / d rounded up
-static inline uint32_t fastmod_u32(uint32_t a, uint64_t fm, uint32_t d) {
-  const uint64_t lowbits = fm * a;
-  return (uint32_t)(((__uint128_t)lowbits * d) >> 64);
-}
-
-struct NpMt {
-  uint32_t* key;
-  int32_t* pos;
-  Mt core;  // reuse the twist
-  uint32_t next32() {
-    if (*pos >= 624) {
-      std::memcpy(core.s, key, sizeof(core.s));
-      core.twist();
-      std::memcpy(key, core.s, sizeof(core.s));
-      *pos = 0;
-    }
-    uint32_t y = key[(*pos)++];
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
-  }
-  // numpy/random/src/distributions: random_interval (max <= 0xffffffff)
-  uint32_t interval(uint32_t max) {
-    if (max == 0) return 0;
-    uint32_t mask = max;
-    mask |= mask >> 1;
-    mask |= mask >> 2;
-    mask |= mask >> 4;
-    mask |= mask >> 8;
-    mask |= mask >> 16;
-    uint32_t v;
-    while ((v = (next32() & mask)) > max) {
-    }
-    return v;
-  }
-};
-
-int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs,
-                         int32_t ratio, int64_t n_entities, int32_t* out) {
-  if (!ts || tlen < 24 + 624 * 8 || !np_key || !np_pos || R < 0 || epochs < 0 || ratio < 1 || n_entities < 1 ||
-      n_entities >= (1LL << 32) || (R > 0 && epochs > 0 && !out))
-    return KP_EINVAL;
-  Mt mt;
-  mt.load(ts);
-  NpMt np{np_key, np_pos, {}};
-  std::vector<int32_t> idx(R);
-  for (int i = 0; i < R; ++i) idx[i] = i;
-  const uint64_t n = (uint64_t)ratio * (uint64_t)R;
-  const uint32_t nent = (uint32_t)n_entities;
-  const uint64_t fm = UINT64_C(0xFFFFFFFFFFFFFFFF) / nent + 1;
-  std::vector<uint32_t> draw(std::max(R, 1));
-  for (int e = 0; e < epochs; ++e) {
-    for (int i = R - 1; i >= 1; --i) {  // np.random.shuffle: for i in reversed(range(1, n))
-      const uint32_t j = np.interval((uint32_t)i);
-      std::swap(idx[i], idx[j]);
-    }
-    int32_t* o = out + (size_t)e * 3 * R;
-    std::memcpy(o, idx.data(), sizeof(int32_t) * R);
-    // randint(high=N): random() % N; only the first R values are stepped, the
-    // other (ratio-1)*R draws are skipped without tempering
-    mt.fill(draw.data(), R);
-    for (int k = 0; k < R; ++k) o[R + k] = (int32_t)fastmod_u32(draw[k], fm, nent);
-    mt.skip(n - (uint64_t)R);
-    mt.fill(draw.data(), R);
-    for (int k = 0; k < R; ++k) o[2 * R + k] = (int32_t)(draw[k] & 1u);  // randint(high=2)
-    mt.skip(n - (uint64_t)R);
-  }
-  mt.store(ts);
-  return KP_OK;
-}
-
-// ATen's bernoulli_(p) on a float tensor draws u = random64() * 2^-53 (hi word first)
-// per element and keeps it when u < p.  u is exact, so u < p <=> m < ceil(p * 2^53)
-// for the 53-bit integer m: the test runs on integers, block-wise over bulk draws.
-static void bernoulli_words(Mt& mt, uint64_t n, double p, uint32_t* out, std::vector<uint32_t>& buf) {
-  const uint64_t mask53 = (1ULL << 53) - 1;
-  const uint64_t thr = (uint64_t)std::ceil(std::ldexp(std::min(std::max(p, 0.0), 1.0), 53));
-  constexpr uint64_t CH = 1u << 14;  // elements per chunk (multiple of 32)
-  buf.resize(2 * CH);
-  for (uint64_t i0 = 0; i0 < n; i0 += CH) {
-    const uint64_t m = std::min<uint64_t>(CH, n - i0);
-    mt.fill(buf.data(), 2 * m);
-    const uint32_t* b = buf.data();
-    uint32_t* o = out + (i0 >> 5);
-    const uint64_t nw = (m + 31) / 32;
-    for (uint64_t w = 0; w < nw; ++w) {
-      uint32_t acc = 0;
-      const uint64_t lim = std::min<uint64_t>(32, m - 32 * w);
-      for (uint64_t j = 0; j < lim; ++j) {
-        const uint64_t e = 32 * w + j;
-        const uint64_t v = (((uint64_t)b[2 * e] << 32) | b[2 * e + 1]) & mask53;
-        acc |= (uint32_t)(v < thr) << j;
-      }
-      o[w] = acc;
-    }
-  }
-}
-
-int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim, double keep,
-                       uint32_t* out) {
-  if (!ts || tlen < 24 + 624 * 8 || n_steps < 0 || dim <= 0 || (n_steps > 0 && (!rows || !out))) return KP_EINVAL;
-  Mt mt;
-  mt.load(ts);
-  std::vector<uint32_t> buf;
-  size_t w0 = 0;
-  for (int st = 0; st < n_steps; ++st) {
-    const uint64_t n = (uint64_t)rows[st] * (uint64_t)dim;
-    bernoulli_words(mt, n, keep, out + w0, buf);  // each step's mask starts on a word
-    w0 += (size_t)((n + 31) / 32);
-  }
-  mt.store(ts);
-  return KP_OK;
-}
-
-int kp_rng_bernoulli_bits(uint8_t* st, size_t len, uint64_t n, double p, uint32_t* out) {
-  if (!st || len < 24 + 624 * 8 || (n > 0 && !out)) return KP_EINVAL;
-  Mt mt;
-  mt.load(st);
-  std::vector<uint32_t> buf;
-  bernoulli_words(mt, n, p, out, buf);
-  mt.store(st);
-  return KP_OK;
-}
-
-int kp_mt19937_discard(uint8_t* st, size_t len, uint64_t n) {
-  if (!st || len < 24 + 624 * 8) return KP_EINVAL;
-  Mt mt;
-  mt.load(st);
-  mt.skip(n);
-  mt.store(st);
-  return KP_OK;
-}
+// The host RNG protocol entry points (kp_rng_*, kp_mt19937_discard) are in kp_rng.cpp.
 
 int kp_last_timing(const kp_ctx* c, double* dev_s, double* hot_s, int64_t* hot_n, double* hot_w) {
   if (!c) return KP_EINVAL;

@@ -1,0 +1,399 @@
+// kp_rng.cpp -- host C++ of the reference's random-draw protocol (SURVEY.md
+// Appendix B), behind the kp_rng_* / kp_mt19937_discard entry points of
+// include/kelpie_hip.h.
+//
+// The reference draws from two MT19937 generators while it post-trains one
+// candidate after another:
+//   * torch's CPU generator (aten/src/ATen/core/MT19937RNGEngine.h): the
+//     per-epoch torch.randint negatives of KelpiePairwiseRankingOptimizer
+//     (src/link_prediction/optimization/pairwise_ranking_optimizer.py:171-172),
+//     the ConvE dropout bernoulli_ masks, and draws that only advance the state;
+//   * numpy's global RandomState (numpy/random/src/mt19937): the per-epoch
+//     np.random.shuffle of the TransE rows (pairwise_ranking_optimizer.py:166).
+// The engine ships the draws to the kernels, so they are generated here from the
+// generators' own state blobs, bit for bit, and the states are advanced in place.
+//
+// Speed matters because the TransE protocol is on the critical path of every
+// engine batch (about 84k generator outputs per slot at FB15k-237 sizes):
+//   * the two generators are independent streams, so a slot's numpy shuffles run
+//     on a persistent helper thread while the calling thread produces the torch
+//     draws;
+//   * numpy outputs are tempered block-wise after each regeneration (vectorised)
+//     and the shuffle works on a local copy of the state (no aliasing with the
+//     output array);
+//   * of the ratio*R torch.randint draws per epoch only the first R are stepped
+//     (SURVEY A-Q2): the others are skipped by twisting, without tempering.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include <unistd.h>
+
+#include "kelpie_hip.h"
+
+namespace {
+
+constexpr int kN = 624, kM = 397;
+
+inline void mt_twist(uint32_t* s) {
+  // three dependency-free spans (distance >= N-M), vectorised by the compiler
+  for (int i = 0; i < kN - kM; ++i) {
+    const uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
+    s[i] = s[i + kM] ^ (y >> 1) ^ ((0u - (s[i + 1] & 1u)) & 0x9908b0dfu);
+  }
+  for (int i = kN - kM; i < kN - 1; ++i) {
+    const uint32_t y = (s[i] & 0x80000000u) | (s[i + 1] & 0x7fffffffu);
+    s[i] = s[i + kM - kN] ^ (y >> 1) ^ ((0u - (s[i + 1] & 1u)) & 0x9908b0dfu);
+  }
+  const uint32_t y = (s[kN - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
+  s[kN - 1] = s[kM - 1] ^ (y >> 1) ^ ((0u - (s[0] & 1u)) & 0x9908b0dfu);
+}
+
+inline uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+// ATen's mt19937 over the CPU-generator state blob of torch.get_rng_state():
+//   { u64 seed; i32 left; i32 seeded; u64 next; u64 state[624]; ... }.
+// operator(): if (--left == 0) twist (left = 624, next = 0); return temper(state[next++]).
+struct TorchMt {
+  int32_t left;
+  uint64_t next;
+  uint32_t s[kN];
+  void load(const uint8_t* st) {
+    std::memcpy(&left, st + 8, 4);
+    std::memcpy(&next, st + 16, 8);
+    for (int i = 0; i < kN; ++i) {
+      uint64_t v;
+      std::memcpy(&v, st + 24 + 8 * i, 8);
+      s[i] = (uint32_t)v;
+    }
+  }
+  void store(uint8_t* st) const {
+    std::memcpy(st + 8, &left, 4);
+    std::memcpy(st + 16, &next, 8);
+    for (int i = 0; i < kN; ++i) {
+      const uint64_t v = s[i];
+      std::memcpy(st + 24 + 8 * i, &v, 8);
+    }
+  }
+  // advance by n outputs (operator() semantics, nothing tempered)
+  void skip(uint64_t n) {
+    while (n > 0) {
+      const uint64_t k = std::min<uint64_t>(n, (uint64_t)(left - 1));
+      left -= (int32_t)k;
+      next += k;
+      n -= k;
+      if (n > 0) {
+        mt_twist(s);
+        left = kN;
+        next = 1;
+        n -= 1;
+      }
+    }
+  }
+  // the next n outputs, in order, tempered as they are taken
+  void fill(uint32_t* out, size_t n) {
+    size_t k = 0;
+    while (k < n) {
+      if (left <= 1) {  // the next operator() call twists
+        mt_twist(s);
+        left = kN + 1;
+        next = 0;
+      }
+      const size_t m = std::min<size_t>(n - k, (size_t)(left - 1));
+      const uint32_t* src = s + next;
+      for (size_t j = 0; j < m; ++j) out[k + j] = mt_temper(src[j]);
+      k += m;
+      next += m;
+      left -= (int32_t)m;
+    }
+  }
+};
+
+// numpy's legacy MT19937 (numpy/random/src/mt19937/mt19937.h: {uint32 key[624]; int pos}):
+// regenerate when pos reaches 624.  Works on a local copy; the current block is kept
+// tempered (tb) so a draw is one load.
+struct NumpyMt {
+  uint32_t key[kN];
+  uint32_t tb[kN];
+  int pos;
+  void temper_all() {
+    for (int i = 0; i < kN; ++i) tb[i] = mt_temper(key[i]);
+  }
+  void load(const uint32_t* k, const int32_t* p) {
+    std::memcpy(key, k, sizeof(key));
+    pos = *p;
+    temper_all();
+  }
+  void store(uint32_t* k, int32_t* p) const {
+    std::memcpy(k, key, sizeof(key));
+    *p = pos;
+  }
+  inline uint32_t next32() {
+    if (pos >= kN) {
+      mt_twist(key);
+      temper_all();
+      pos = 0;
+    }
+    return tb[pos++];
+  }
+  // numpy/random/src/distributions: random_interval(max), max < 2^32 (masked rejection)
+  inline uint32_t interval(uint32_t max) {
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (next32() & mask)) > max) {
+    }
+    return v;
+  }
+};
+
+// a % d for 32-bit a, d >= 1 (Lemire, Kaser & Kurz 2019), fm = 2^64 / d rounded up
+inline uint32_t fastmod_u32(uint32_t a, uint64_t fm, uint32_t d) {
+  const uint64_t lowbits = fm * a;
+  return (uint32_t)(((__uint128_t)lowbits * d) >> 64);
+}
+
+// One persistent helper thread that runs one task at a time for a caller that waits
+// for it.  It spins briefly between tasks (a scheduling pass calls every few tens of
+// microseconds) and then sleeps on a condition variable.  Re-created after a fork.
+class Helper {
+ public:
+  static Helper& get() {
+    static Helper* h = new Helper();  // never destroyed: no join at process exit
+    return *h;
+  }
+  // run a() here and b() on the helper (inline if the helper is busy or unusable)
+  void run2(const std::function<void()>& a, const std::function<void()>& b) {
+    std::unique_lock<std::mutex> owner(own_, std::try_to_lock);
+    if (!owner.owns_lock() || !ensure()) {
+      b();
+      a();
+      return;
+    }
+    task_ = &b;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      state_.store(1, std::memory_order_release);
+    }
+    cv_.notify_one();
+    bool a_failed = false;
+    try {
+      a();
+    } catch (...) {
+      a_failed = true;  // b() still references the caller's frame: wait for it first
+    }
+    // if the helper has not claimed the task yet (descheduled on a busy host), take it back
+    int posted = 1;
+    const bool claimed = !state_.compare_exchange_strong(posted, 0, std::memory_order_acq_rel);
+    if (!claimed) {
+      try {
+        b();
+      } catch (...) {
+        a_failed = true;
+      }
+    } else {
+      while (state_.load(std::memory_order_acquire) != 2) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+      state_.store(0, std::memory_order_relaxed);
+    }
+    if (a_failed || (claimed && failed_)) throw std::bad_alloc();
+  }
+
+ private:
+  bool ensure() {
+    const pid_t me = getpid();
+    if (pid_ == me) return true;
+    try {
+      state_.store(0);
+      std::thread([this] { loop(); }).detach();
+      pid_ = me;
+      return true;
+    } catch (...) {
+      return false;
+    }
+  }
+  // states: 0 idle, 1 posted, 3 claimed by the helper, 2 done
+  void loop() {
+    for (;;) {
+      int spins = 0;
+      for (;;) {
+        int posted = 1;
+        if (state_.compare_exchange_weak(posted, 3, std::memory_order_acq_rel)) break;
+        if (++spins < 200000) {
+#if defined(__x86_64__)
+          __builtin_ia32_pause();
+#endif
+          continue;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return state_.load(std::memory_order_acquire) == 1; });
+      }
+      try {
+        (*task_)();
+        failed_ = false;
+      } catch (...) {
+        failed_ = true;
+      }
+      state_.store(2, std::memory_order_release);
+    }
+  }
+  std::mutex own_, mu_;
+  std::condition_variable cv_;
+  std::atomic<int> state_{0};
+  const std::function<void()>* task_ = nullptr;
+  pid_t pid_ = 0;
+  bool failed_ = false;
+};
+
+// ATen's bernoulli_(p) on a float tensor draws u = random64() * 2^-53 (hi word first)
+// per element and keeps it when u < p.  u is exact, so u < p <=> m < ceil(p * 2^53)
+// for the 53-bit integer m: the test runs on integers, block-wise over bulk draws.
+void bernoulli_words(TorchMt& mt, uint64_t n, double p, uint32_t* out, std::vector<uint32_t>& buf) {
+  const uint64_t mask53 = (1ULL << 53) - 1;
+  const uint64_t thr = (uint64_t)std::ceil(std::ldexp(std::min(std::max(p, 0.0), 1.0), 53));
+  constexpr uint64_t CH = 1u << 14;  // elements per chunk (multiple of 32)
+  buf.resize(2 * CH);
+  for (uint64_t i0 = 0; i0 < n; i0 += CH) {
+    const uint64_t m = std::min<uint64_t>(CH, n - i0);
+    mt.fill(buf.data(), 2 * m);
+    const uint32_t* b = buf.data();
+    uint32_t* o = out + (i0 >> 5);
+    const uint64_t nw = (m + 31) / 32;
+    for (uint64_t w = 0; w < nw; ++w) {
+      uint32_t acc = 0;
+      const uint64_t lim = std::min<uint64_t>(32, m - 32 * w);
+      for (uint64_t j = 0; j < lim; ++j) {
+        const uint64_t e = 32 * w + j;
+        const uint64_t v = (((uint64_t)b[2 * e] << 32) | b[2 * e + 1]) & mask53;
+        acc |= (uint32_t)(v < thr) << j;
+      }
+      o[w] = acc;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs,
+                         int32_t ratio, int64_t n_entities, int32_t* out) {
+  if (!ts || tlen < 24 + kN * 8 || !np_key || !np_pos || R < 0 || epochs < 0 || ratio < 1 || n_entities < 1 ||
+      n_entities >= (1LL << 32) || (R > 0 && epochs > 0 && !out))
+    return KP_EINVAL;
+  if (*np_pos < 0 || *np_pos > kN) return KP_EINVAL;
+  try {
+    // numpy stream: per epoch np.random.shuffle(rows) in place; the row order composes
+    auto shuffles = [&] {
+      NumpyMt np;
+      np.load(np_key, np_pos);
+      std::vector<int32_t> idx(R);
+      for (int i = 0; i < R; ++i) idx[i] = i;
+      for (int e = 0; e < epochs; ++e) {
+        for (int i = R - 1; i >= 1; --i) {  // for i in reversed(range(1, n)): j = interval(i)
+          const uint32_t j = np.interval((uint32_t)i);
+          std::swap(idx[i], idx[j]);
+        }
+        std::memcpy(out + (size_t)e * 3 * R, idx.data(), sizeof(int32_t) * R);
+      }
+      np.store(np_key, np_pos);
+    };
+    // torch stream: randint(high=N) = random() % N and randint(high=2), ratio*R each;
+    // only the first R of each are stepped
+    auto randints = [&] {
+      TorchMt mt;
+      mt.load(ts);
+      const uint64_t n = (uint64_t)ratio * (uint64_t)R;
+      const uint32_t nent = (uint32_t)n_entities;
+      const uint64_t fm = UINT64_C(0xFFFFFFFFFFFFFFFF) / nent + 1;
+      std::vector<uint32_t> draw(std::max(R, 1));
+      for (int e = 0; e < epochs; ++e) {
+        int32_t* o = out + (size_t)e * 3 * R;
+        mt.fill(draw.data(), R);
+        for (int k = 0; k < R; ++k) o[R + k] = (int32_t)fastmod_u32(draw[k], fm, nent);
+        mt.skip(n - (uint64_t)R);
+        mt.fill(draw.data(), R);
+        for (int k = 0; k < R; ++k) o[2 * R + k] = (int32_t)(draw[k] & 1u);
+        mt.skip(n - (uint64_t)R);
+      }
+      mt.store(ts);
+    };
+    if (R >= 16 && epochs >= 4) {
+      const std::function<void()> a = randints, b = shuffles;
+      Helper::get().run2(a, b);
+    } else {
+      shuffles();
+      randints();
+    }
+  } catch (...) {
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim, double keep,
+                       uint32_t* out) {
+  if (!ts || tlen < 24 + kN * 8 || n_steps < 0 || dim <= 0 || (n_steps > 0 && (!rows || !out))) return KP_EINVAL;
+  try {
+    TorchMt mt;
+    mt.load(ts);
+    std::vector<uint32_t> buf;
+    size_t w0 = 0;
+    for (int st = 0; st < n_steps; ++st) {
+      const uint64_t n = (uint64_t)rows[st] * (uint64_t)dim;
+      bernoulli_words(mt, n, keep, out + w0, buf);  // each step's mask starts on a word
+      w0 += (size_t)((n + 31) / 32);
+    }
+    mt.store(ts);
+  } catch (...) {
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+int kp_rng_bernoulli_bits(uint8_t* st, size_t len, uint64_t n, double p, uint32_t* out) {
+  if (!st || len < 24 + kN * 8 || (n > 0 && !out)) return KP_EINVAL;
+  try {
+    TorchMt mt;
+    mt.load(st);
+    std::vector<uint32_t> buf;
+    bernoulli_words(mt, n, p, out, buf);
+    mt.store(st);
+  } catch (...) {
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+int kp_mt19937_discard(uint8_t* st, size_t len, uint64_t n) {
+  if (!st || len < 24 + kN * 8) return KP_EINVAL;
+  TorchMt mt;
+  mt.load(st);
+  mt.skip(n);
+  mt.store(st);
+  return KP_OK;
+}
+
+}  // extern "C"

@@ -217,13 +217,19 @@ class KelpieView:
             if b == k:
                 self.filter[p + R][a] += 1
         self.index = {t: i for i, t in enumerate(self.base_triples)}
-        self.base_rows = self._rows(self.base_triples)
+        self.base_arr = np.asarray(self.base_triples, dtype=np.int32).reshape(-1, 3)
+        self.base_rows = self._rows(self.base_arr)
 
-    def _rows(self, triples):
-        t = np.asarray(triples, dtype=np.int32).reshape(-1, 3)
-        inv = t[:, [2, 1, 0]].copy()
-        inv[:, 1] += self.dataset.num_relations
-        return np.ascontiguousarray(np.vstack([t, inv]))
+    def _rows(self, t):
+        """Kelpie rows followed by their inverses (o, p + |R|, s), the optimizers' order
+        (pairwise_ranking_optimizer.py:64-65, multiclass_nll_optimizer.py:66-67)."""
+        n = len(t)
+        out = np.empty((2 * n, 3), np.int32)
+        out[:n] = t
+        out[n:, 0] = t[:, 2]
+        out[n:, 1] = t[:, 1] + self.dataset.num_relations
+        out[n:, 2] = t[:, 0]
+        return out
 
     def as_kelpie_triple(self, triple):
         if self.original_entity not in tuple(triple):
@@ -259,7 +265,7 @@ class KelpieView:
         idx = [self.index[x] for x in conv]  # KeyError for a foreign triple, like the reference
         keep = np.ones(len(self.base_triples), dtype=bool)
         keep[idx] = False
-        kept = [t for t, f in zip(self.base_triples, keep) if f]
+        kept = self.base_arr[keep]
         delta = self._delta(conv, -1)
         for rel, cnt in delta.items():
             cur = self.filter.get(rel, Counter())
@@ -274,4 +280,5 @@ class KelpieView:
             assert self.original_entity == s or self.original_entity == o
         conv = [Dataset.replace_entity_in_triple(tuple(t), self.original_entity, self.kelpie_entity)
                 for t in triples]
-        return self._rows(list(self.base_triples) + conv), self._delta(conv, +1)
+        rows = np.concatenate([self.base_arr, np.asarray(conv, dtype=np.int32).reshape(-1, 3)])
+        return self._rows(rows), self._delta(conv, +1)

@@ -228,3 +228,64 @@ def test_batch_equals_sequential_and_is_deterministic_fb15k_shape():
     n = ds.num_entities + 1
     for pt, b in eng.last_results:
         assert 0 <= pt["target_rank"] <= n and 0 <= b["target_rank"] <= n
+
+
+@pytest.fixture(scope="module")
+def db100k():
+    """BASELINE.json configs[3] shape: 99,604 entities, 470 relations, D = 400."""
+    from kelpie_amd import synth
+    g = synth.make_graph("DB100K", seed=0)
+    ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    return g, ds
+
+
+DB_HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 83, "lr": 0.0814, "decay1": 0.9,
+         "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0}  # ComplEx_DB100K_explanation.json
+
+
+def test_complex_db100k_necessary_vs_oracle(db100k):
+    """ComplEx at the DB100K size (N = 99,605 rows in the rank, 83 Adagrad epochs) against
+    the oracle, on weights with a trained-like spread (ranks exact, scores within 1e-4)."""
+    from cpu_backend import OracleBackedContext
+    from kelpie_amd import synth
+    g, ds = db100k
+    w = synth.make_weights("ComplEx", g.num_entities, g.num_relations, 200, seed=4, trained_scale=0.3)
+    pred = next(tuple(int(v) for v in t) for t in g.test if 10 <= ds.entity_to_degree.get(int(t[0]), 0) <= 30)
+    cands = sorted(ds.entity_to_training_triples[pred[0]])[:2]
+    out = {}
+    for backend in ("gpu", "cpu"):
+        model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"])
+        if backend == "cpu":
+            model._ctx = OracleBackedContext(model)
+        seed_all(42)
+        eng = ka.NecessaryPostTrainingEngine(model, ds, DB_HP)
+        rels = eng.compute_relevance_batch(pred, [[c] for c in cands])
+        out[backend] = (rels, [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+                               for pt, b in eng.last_results])
+    for a, b in zip(out["gpu"][1], out["cpu"][1]):
+        assert a[0] == b[0] and a[2] == b[2], (a, b)
+        assert abs(a[1] - b[1]) <= 1e-4 * max(1.0, abs(b[1])) and abs(a[3] - b[3]) <= 1e-4 * max(1.0, abs(b[3]))
+    assert np.allclose(out["gpu"][0], out["cpu"][0], atol=1e-4)
+
+
+def test_complex_db100k_sufficient_batch_equals_sequential(db100k):
+    """Sufficient mode at the DB100K size with the reference random init: one batch over
+    all conversion entities returns exactly the sequential calls, and reruns are bitwise equal."""
+    from kelpie_amd import synth
+    g, ds = db100k
+    w = synth.make_weights("ComplEx", g.num_entities, g.num_relations, 200, seed=0)
+    model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"])
+    pred = next(tuple(int(v) for v in t) for t in g.test if 10 <= ds.entity_to_degree.get(int(t[0]), 0) <= 30)
+    cands = sorted(ds.entity_to_training_triples[pred[0]])[:4]
+    runs = []
+    for mode in ("batch", "batch", "seq"):
+        seed_all(42)
+        eng = ka.SufficientPostTrainingEngine(model, ds, DB_HP)
+        ents = eng.select_entities_to_convert(pred, 10, 200)
+        assert len(ents) == 10
+        if mode == "batch":
+            runs.append(eng.compute_relevance_batch(pred, [[c] for c in cands]))
+        else:
+            runs.append([eng.compute_relevance(pred, [c]) for c in cands])
+    assert runs[0] == runs[1]
+    assert np.allclose(runs[0], runs[2], atol=1e-6)

@@ -1,5 +1,6 @@
 """The host RNG protocol's shortcuts consume exactly what the reference's calls consume."""
 import numpy as np
+import pytest
 import torch
 
 from kelpie_amd import _lib
@@ -57,12 +58,16 @@ def test_complex_epochs_skip_is_equivalent():
     assert torch.equal(a, b)
 
 
-def test_transe_epochs_match_reference_calls():
-    R, E, ratio, N = 9, 5, 5, 301
+@pytest.mark.parametrize("R,E", [(9, 5), (150, 7), (700, 4)])
+def test_transe_epochs_match_reference_calls(R, E):
+    """R >= 16 runs the numpy shuffles on the helper thread; 700 rows cross numpy
+    regenerations inside one epoch's shuffle."""
+    ratio, N = 5, 301
     torch.manual_seed(2)
     np.random.seed(2)
     blob = ReferenceRNG().transe_epochs(R, E, ratio, N).reshape(E, 3, R)
     after = torch.rand(2)
+    np_after = np.random.randint(0, 1 << 30, 8)
     torch.manual_seed(2)
     np.random.seed(2)
     rows = np.arange(R * 3).reshape(R, 3)
@@ -74,6 +79,7 @@ def test_transe_epochs_match_reference_calls():
         assert np.array_equal(ents[:R].numpy(), blob[e, 1])
         assert np.array_equal(hot[:R].numpy(), blob[e, 2])
     assert torch.equal(torch.rand(2), after)
+    assert np.array_equal(np.random.randint(0, 1 << 30, 8), np_after)
 
 
 def test_conve_masks_match_torch_dropout_sequence():
