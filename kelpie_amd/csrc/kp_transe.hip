@@ -19,6 +19,7 @@
 // Memory-bound: every pair gathers up to 4 entity rows and a relation row
 // from the L2 / Infinity Cache.
 #include <cmath>
+#include <cstdlib>
 
 #include "kp_common.hpp"
 
@@ -36,226 +37,232 @@ struct TeHp {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-constexpr int TE_CH = 256;
-constexpr int TE_PPG = 2;  // pairs in flight per 16-lane group (all their row loads issued before the math)
-
 #ifdef KP_TE_STAMPS
-// diagnostic build only: per-phase cycles of kp_te_posttrain summed over wave 0 of
-// every workgroup: [staging, pairs, chunk sync, reduce + Adam]
-__device__ unsigned long long g_te_stamps[8];
-#define TE_STAMP(k) te_ts[k] = __builtin_amdgcn_s_memtime()
-#else
-#define TE_STAMP(k) (void)0
-#endif  // stepped pairs whose descriptors are staged in LDS at a time
-
-// one (positive, negative) pair: the two difference vectors of 16 lanes x VPL float4
-template <int VPL>
-struct TePair {
-  float4 vp[VPL], vn[VPL];
-  float sp, sn;
-};
-
-// Row loads of one pair.  Frozen rows come from global memory (global_load, the
-// kelpie id K replaced by row 0) and the kelpie row from LDS, selected per value:
-// one flat load per row would let a 16-lane group's pointer alias either space.
-template <int VPL>
-__device__ __forceinline__ void te_load(TePair<VPL>& P, const float* __restrict__ E,
-                                        const float* __restrict__ Rt, const float* xs, int dp, int K, int4 dsc,
-                                        int tn, int l16, int NF4) {
-  const int h = dsc.x, r = dsc.y, t = dsc.z, hn = dsc.w;
-  const float* Lp = E + (size_t)(h == K ? 0 : h) * dp;
-  const float* Rp = E + (size_t)(t == K ? 0 : t) * dp;
-  const float* Ln = E + (size_t)(hn == K ? 0 : hn) * dp;
-  const float* Rn = E + (size_t)(tn == K ? 0 : tn) * dp;
-  const float* rel = Rt + (size_t)r * dp;
-  P.sp = 0.f;
-  P.sn = 0.f;
-  // branch-free: lanes past the row end load a clamped duplicate and are zeroed, so
-  // every pair's loads sit in one basic block and can all be in flight together
-#pragma unroll
-  for (int u = 0; u < VPL; ++u) {
-    const int f0 = l16 + 16 * u;
-    const bool on = f0 < NF4;
-    const int f = on ? f0 : NF4 - 1;
-    const float4 xk = ld4(xs + 4 * f);
-    float4 a = ld4(Lp + 4 * f), c = ld4(Rp + 4 * f), a2 = ld4(Ln + 4 * f), c2 = ld4(Rn + 4 * f);
-    const float4 b = ld4(rel + 4 * f);
-    if (h == K) a = xk;
-    if (t == K) c = xk;
-    if (hn == K) a2 = xk;
-    if (tn == K) c2 = xk;
-    const float4 vp = make_float4((a.x + b.x) - c.x, (a.y + b.y) - c.y, (a.z + b.z) - c.z, (a.w + b.w) - c.w);
-    const float4 vn = make_float4((a2.x + b.x) - c2.x, (a2.y + b.y) - c2.y, (a2.z + b.z) - c2.z, (a2.w + b.w) - c2.w);
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    P.vp[u] = on ? vp : z;
-    P.vn[u] = on ? vn : z;
-  }
-}
-
-template <int VPL>
-__device__ __forceinline__ void te_accum(TePair<VPL>& P, const int4 dsc, int tn, int K, float margin, float4* g,
-                                         int& cnt) {
-#pragma unroll
-  for (int u = 0; u < VPL; ++u) {
-    P.sp += P.vp[u].x * P.vp[u].x + P.vp[u].y * P.vp[u].y + P.vp[u].z * P.vp[u].z + P.vp[u].w * P.vp[u].w;
-    P.sn += P.vn[u].x * P.vn[u].x + P.vn[u].y * P.vn[u].y + P.vn[u].z * P.vn[u].z + P.vn[u].w * P.vn[u].w;
-  }
-  P.sp = row16_sum(P.sp);
-  P.sn = row16_sum(P.sn);
-  const int h = dsc.x, t = dsc.z, hn = dsc.w;
-  const float fp = sqrtf(P.sp), fn = sqrtf(P.sn);
-  const float z = (fp - fn) + margin;
-  const bool act = z >= 0.f;  // clamp_min backward passes grad where self >= min
-  const float sgn_p = (float)((h == K) - (t == K));
-  const float sgn_n = (float)((hn == K) - (tn == K));
-  const float cp = (act && fp > 0.f) ? sgn_p / fp : 0.f;
-  const float cn = (act && fn > 0.f) ? -sgn_n / fn : 0.f;
-#pragma unroll
-  for (int u = 0; u < VPL; ++u) {
-    g[u].x += cp * P.vp[u].x + cn * P.vn[u].x;
-    g[u].y += cp * P.vp[u].y + cn * P.vn[u].y;
-    g[u].z += cp * P.vp[u].z + cn * P.vn[u].z;
-    g[u].w += cp * P.vp[u].w + cn * P.vn[u].w;
-  }
-  cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
-}
-
-template <int VPL>  // float4 per lane (16 lanes per row): DP <= 64 * VPL
-__global__ __launch_bounds__(256, 2) void kp_te_posttrain(int n_ent, int dp, int d, const float* __restrict__ E,
-                                                       const float* __restrict__ R,
-                                                       const TeSlot* __restrict__ slots,
-                                                       const int32_t* __restrict__ rows,
-                                                       const int32_t* __restrict__ rng, TeHp hp,
-                                                       float* __restrict__ X) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* xs = sm;                                            // [dp]
-  float* red = sm + dp;                                      // [16][dp] per-group gradient partials
-  int4* dsc = reinterpret_cast<int4*>(sm + 17 * dp);         // [TE_CH] (h, r, t, h_neg)
-  int* dtn = reinterpret_cast<int*>(dsc + TE_CH);            // [TE_CH] t_neg
-  __shared__ int cnt_s[16];
-  const int tid = threadIdx.x;
-  const int grp = tid >> 4, l16 = tid & 15;
-  const TeSlot S = slots[blockIdx.x];
-  const int K = n_ent;
-  float* x = X + (size_t)blockIdx.x * dp;
-  for (int i = tid; i < dp; i += 256) xs[i] = x[i];
-  // Adam moments: thread i owns element i (and i+256)
-  float m1[2] = {0.f, 0.f}, v2[2] = {0.f, 0.f};
-  __syncthreads();
-  const int32_t* rw = rows + 3 * (size_t)S.row_off;
-  const int NF4 = dp / 4;
-  double b1t = 1.0, b2t = 1.0;
-#ifdef KP_TE_STAMPS
-  unsigned long long te_ts[5] = {0, 0, 0, 0, 0}, te_acc[4] = {0, 0, 0, 0}, te_wait = 0, te_rounds = 0;
+// diagnostic build only (make stamps): per workgroup [slot, R, start, end] in wall_clock64 ticks (100 MHz)
+__device__ long long g_te_times[4 * 8192];
 #endif
+
+constexpr int TE_NB = 5;  // negatives per bundle held in registers (the reference's ratio; larger ratios loop)
+
+// sum over the 64 lanes, returned wave-uniform: 16-lane DPP sums, then row_bcast15 /
+// row_bcast31 fold the four rows into lane 63
+__device__ __forceinline__ float wave_sum_u(float v) {
+  v = row16_sum(v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
+// One workgroup per slot (slots issued longest first) runs every epoch on chip: x in
+// LDS, its Adam moments in registers.
+//
+// Work unit = one wave-uniform *bundle*: the stepped positions j = m*ratio .. m*ratio +
+// ratio - 1 share the positive row order[m] (np.repeat of the shuffled rows, A-Q2), so
+// a wave loads the positive's frozen side (h or t; the other is the kelpie row x) and
+// the relation ONCE, plus one fresh entity row per negative (a negative keeps the
+// positive's uncorrupted side).  Descriptors are wave-uniform scalar loads; rows are
+// float4 per lane (64 lanes per row).  The kelpie id K in any position selects x
+// (loads stay branch-free: K reads row 0).  Squared norms are wave reductions; the
+// single-row gradient (TransE) accumulates in registers; per step the
+// 16 wave partials are summed in a fixed order in LDS and Adam updates x.
+//
+// Cost model: per stepped pair one fresh 4*d-byte negative row; the
+// positive side and relation once per bundle.  A slot's epochs are one dependent chain,
+// so its time is the latency of that chain: the slot's rows are staged in LDS once and
+// each epoch's draws are loaded into registers during the previous epoch and stored to
+// the other half of a double buffer in LDS (they do not depend on x), which leaves one
+// row-gather round per bundle, two barriers and the Adam step per epoch.  NT = 1024
+// threads per workgroup (1024: one per CU; 512 for diagnostics).
+// STAGED = false (slots too long for the LDS buffers) reads the descriptors from memory.
+template <int VPL, int NT, bool STAGED>  // VPL float4 per lane: dp <= 256 * VPL
+__global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, const float* __restrict__ E,
+                                                          const float* __restrict__ Rt,
+                                                          const TeSlot* __restrict__ slots,
+                                                          const int32_t* __restrict__ slot_of_block,
+                                                          const int32_t* __restrict__ rows,
+                                                          const int32_t* __restrict__ rng, TeHp hp,
+                                                          float* __restrict__ X) {
+  constexpr int TE_NW = NT / 64;  // waves
+  constexpr int PF = 4;           // prefetched draw words per thread (STAGED: 3 R <= PF * NT)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xs = sm;        // [dp]
+  float* red = sm + dp;  // [TE_NW][dp] per-wave gradient partials
+  int* rws = reinterpret_cast<int*>(red + TE_NW * dp);  // STAGED: [3 R] the slot's rows
+  int* drw = rws + 3 * (STAGED ? slots[slot_of_block[blockIdx.x]].R : 0);  // STAGED: [2][3 R] draws
+  __shared__ int cnt_s[TE_NW];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int slot = slot_of_block[blockIdx.x];
+  const TeSlot S = slots[slot];
+  const int K = n_ent;
+  float* x = X + (size_t)slot * dp;
+#ifdef KP_TE_STAMPS
+  const long long t_start = wall_clock64();
+#endif
+  for (int i = tid; i < dp; i += NT) xs[i] = x[i];
+  float m1 = 0.f, v2 = 0.f;  // Adam moments of element tid (tid < dp)
+  const int32_t* rwg = rows + 3 * (size_t)S.row_off;
+  const int32_t* rngs = rng + S.rng_off;
+  const int R3 = 3 * S.R;
+  int pf[PF];
+  if (STAGED) {
+    for (int i = tid; i < R3; i += NT) {
+      rws[i] = rwg[i];
+      if (hp.epochs > 0) drw[i] = rngs[i];
+    }
+  }
+  __syncthreads();
+  const int32_t* rw = STAGED ? rws : rwg;
+  const int NF4 = dp / 4;
+  const int ratio = hp.ratio;
+  double b1t = 1.0, b2t = 1.0;
   for (int e = 0; e < hp.epochs; ++e) {
-    const int32_t* order = rng + S.rng_off + (long long)e * 3 * S.R;
+    const int32_t* order = STAGED ? drw + (e & 1) * R3 : rngs + (long long)e * R3;
     const int32_t* ents = order + S.R;
     const int32_t* hot = order + 2 * S.R;
+    if (STAGED && e + 1 < hp.epochs) {  // next epoch's draws, landed during this epoch
+      const int32_t* nx = rngs + (long long)(e + 1) * R3;
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const int i = tid + k * NT;
+        pf[k] = i < R3 ? nx[i] : 0;
+      }
+    }
     for (int st = 0; st < S.R; st += hp.bs) {
       const int B = min(hp.bs, S.R - st);
       float4 g[VPL];
 #pragma unroll
       for (int u = 0; u < VPL; ++u) g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       int cnt = 0;
-      for (int c0 = st; c0 < st + B; c0 += TE_CH) {
-        TE_STAMP(0);
-        const int n = min(TE_CH, st + B - c0);
-        // ---- stage the chunk's pair descriptors (coalesced draws, row gathers from L2)
-        for (int k = tid; k < n; k += 256) {
-          const int j = c0 + k;
-          const int ri = order[j / hp.ratio];
-          const int h = rw[3 * ri], r = rw[3 * ri + 1], t = rw[3 * ri + 2];
-          const int ent = ents[j];
-          const bool corrupt_head = hot[j] == 1;
-          dsc[k] = make_int4(h, r, t, corrupt_head ? ent : h);
-          dtn[k] = corrupt_head ? t : ent;
-        }
-        __syncthreads();
-        TE_STAMP(1);
-        // ---- TE_PPG pairs per group in flight: all their row loads issued before the math
-        for (int k0 = grp; k0 < n; k0 += 16 * TE_PPG) {
-          TePair<VPL> P[TE_PPG];
-          int4 dd[TE_PPG];
-          int tt[TE_PPG];
+      // bundles overlapping the step's positions [st, st + B)
+      for (int m = st / ratio + wave; m * ratio < st + B; m += TE_NW) {
+        const int ri = __builtin_amdgcn_readfirstlane(order[m]);
+        const int h = __builtin_amdgcn_readfirstlane(rw[3 * ri]);
+        const int r = __builtin_amdgcn_readfirstlane(rw[3 * ri + 1]);
+        const int t = __builtin_amdgcn_readfirstlane(rw[3 * ri + 2]);
+        const int fz = (h == K) ? t : h;  // the positive's frozen side (K too for a self loop)
+        const float* A = E + (size_t)(fz == K ? 0 : fz) * dp;
+        const float* rel = Rt + (size_t)r * dp;
+        const int jlo = max(m * ratio, st), jhi = min(m * ratio + ratio, st + B);
+        for (int j0 = jlo; j0 < jhi; j0 += TE_NB) {
+          const int nb = min(TE_NB, jhi - j0);
+          int ent[TE_NB];
+          bool ch[TE_NB];
 #pragma unroll
-          for (int u = 0; u < TE_PPG; ++u) {
-            const int k = min(k0 + 16 * u, n - 1);  // past the chunk: reload a valid pair, not accumulated
-            dd[u] = dsc[k];
-            tt[u] = dtn[k];
-            te_load<VPL>(P[u], E, R, xs, dp, K, dd[u], tt[u], l16, NF4);
+          for (int q = 0; q < TE_NB; ++q) {
+            const int jj = j0 + min(q, nb - 1);
+            ent[q] = __builtin_amdgcn_readfirstlane(ents[jj]);
+            ch[q] = __builtin_amdgcn_readfirstlane(hot[jj]) == 1;
           }
-#ifdef KP_TE_STAMPS
-          const unsigned long long r0 = __builtin_amdgcn_s_memtime();
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          const unsigned long long r1 = __builtin_amdgcn_s_memtime();
-          te_wait += r1 - r0;
-#endif
+          float4 lp[VPL], rp[VPL], bb[VPL], bn[TE_NB][VPL];
 #pragma unroll
-          for (int u = 0; u < TE_PPG; ++u)
-            if (k0 + 16 * u < n) te_accum<VPL>(P[u], dd[u], tt[u], K, hp.margin, g, cnt);
-#ifdef KP_TE_STAMPS
-          te_rounds += 1;
-#endif
+          for (int u = 0; u < VPL; ++u) {
+            const int f0 = lane + 64 * u;
+            const int f = f0 < NF4 ? f0 : NF4 - 1;
+            const float4 xk = ld4(xs + 4 * f);
+            float4 av = ld4(A + 4 * f);
+            bb[u] = ld4(rel + 4 * f);
+#pragma unroll
+            for (int q = 0; q < TE_NB; ++q) bn[q][u] = ld4(E + (size_t)(ent[q] == K ? 0 : ent[q]) * dp + 4 * f);
+            if (fz == K) av = xk;
+#pragma unroll
+            for (int q = 0; q < TE_NB; ++q)
+              if (ent[q] == K) bn[q][u] = xk;
+            lp[u] = (h == K) ? xk : av;
+            rp[u] = (t == K) ? xk : av;
+          }
+          // positive: v+ = (lhs + rel) - rhs, zero past the row end
+          float4 vp[VPL];
+          float sp = 0.f;
+#pragma unroll
+          for (int u = 0; u < VPL; ++u) {
+            const bool on = lane + 64 * u < NF4;
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            vp[u] = on ? make_float4((lp[u].x + bb[u].x) - rp[u].x, (lp[u].y + bb[u].y) - rp[u].y,
+                                     (lp[u].z + bb[u].z) - rp[u].z, (lp[u].w + bb[u].w) - rp[u].w)
+                       : z;
+            sp += vp[u].x * vp[u].x + vp[u].y * vp[u].y + vp[u].z * vp[u].z + vp[u].w * vp[u].w;
+          }
+          const float fp = sqrtf(wave_sum_u(sp));
+          const float sgn_p = (float)((h == K) - (t == K));
+#pragma unroll
+          for (int q = 0; q < TE_NB; ++q) {
+            if (q >= nb) break;
+            const int hn = ch[q] ? ent[q] : h, tn = ch[q] ? t : ent[q];
+            float4 vn[VPL];
+            float sn = 0.f;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+              const bool on = lane + 64 * u < NF4;
+              const float4 ln = ch[q] ? bn[q][u] : lp[u], rn = ch[q] ? rp[u] : bn[q][u];
+              const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+              vn[u] = on ? make_float4((ln.x + bb[u].x) - rn.x, (ln.y + bb[u].y) - rn.y, (ln.z + bb[u].z) - rn.z,
+                                       (ln.w + bb[u].w) - rn.w)
+                         : z;
+              sn += vn[u].x * vn[u].x + vn[u].y * vn[u].y + vn[u].z * vn[u].z + vn[u].w * vn[u].w;
+            }
+            const float fn = sqrtf(wave_sum_u(sn));
+            const float zz = (fp - fn) + hp.margin;
+            const bool act = zz >= 0.f;  // clamp_min backward passes grad where self >= min
+            const float sgn_n = (float)((hn == K) - (tn == K));
+            const float cp = (act && fp > 0.f) ? sgn_p / fp : 0.f;
+            const float cn = (act && fn > 0.f) ? -sgn_n / fn : 0.f;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+              g[u].x += cp * vp[u].x + cn * vn[u].x;
+              g[u].y += cp * vp[u].y + cn * vn[u].y;
+              g[u].z += cp * vp[u].z + cn * vn[u].z;
+              g[u].w += cp * vp[u].w + cn * vn[u].w;
+            }
+            cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
+          }
         }
-        TE_STAMP(2);
-        __syncthreads();  // the next chunk overwrites the descriptors
       }
-      TE_STAMP(3);
-      // ---- reduce the 16 group partials
+      if (STAGED && e + 1 < hp.epochs && st + hp.bs >= S.R) {  // last step of the epoch
+        int* nb_ = drw + ((e + 1) & 1) * R3;
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+          const int i = tid + k * NT;
+          if (i < R3) nb_[i] = pf[k];
+        }
+      }
+      // ---- sum the wave partials in a fixed order, then Adam on x
 #pragma unroll
       for (int u = 0; u < VPL; ++u) {
-        const int f = l16 + 16 * u;
-        if (f < NF4) *reinterpret_cast<float4*>(red + grp * dp + 4 * f) = g[u];
+        const int f = lane + 64 * u;
+        if (f < NF4) *reinterpret_cast<float4*>(red + wave * dp + 4 * f) = g[u];
       }
-      if (l16 == 0) cnt_s[grp] = cnt;
+      if (lane == 0) cnt_s[wave] = cnt;
       __syncthreads();
-      int ctot = 0;
-      for (int k = 0; k < 16; ++k) ctot += cnt_s[k];
-      const float invB = 1.0f / (float)B;
-      const float regc = hp.lam / (3.0f * (float)B * (float)d) * (float)ctot;
       b1t *= (double)hp.b1;
       b2t *= (double)hp.b2;
-      const float step_size = (float)((double)hp.lr / (1.0 - b1t));
-      const float bc2s = (float)sqrt(1.0 - b2t);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int i = tid + 256 * u;
-        if (i < dp) {
-          float gs = 0.f;
-          for (int k = 0; k < 16; ++k) gs += red[k * dp + i];
-          const float xi = xs[i];
-          const float gi = gs * invB + regc * xi;
-          m1[u] = m1[u] + hp.one_minus_b1 * (gi - m1[u]);
-          v2[u] = v2[u] * hp.b2;
-          v2[u] = v2[u] + (hp.one_minus_b2 * gi) * gi;
-          const float den = sqrtf(v2[u]) / bc2s + hp.eps;
-          const float xn = (i < d) ? xi + (-step_size * m1[u]) / den : 0.f;
-          red[i] = xn;  // stage (group 0's slot is consumed already)
-        }
+      if (tid < dp) {
+        int ctot = 0;
+        for (int k = 0; k < TE_NW; ++k) ctot += cnt_s[k];
+        const float invB = 1.0f / (float)B;
+        const float regc = hp.lam / (3.0f * (float)B * (float)d) * (float)ctot;
+        const float step_size = (float)((double)hp.lr / (1.0 - b1t));
+        const float bc2s = (float)sqrt(1.0 - b2t);
+        float gs = 0.f;
+        for (int k = 0; k < TE_NW; ++k) gs += red[k * dp + tid];
+        const float xi = xs[tid];
+        const float gi = gs * invB + regc * xi;
+        m1 = m1 + hp.one_minus_b1 * (gi - m1);
+        v2 = v2 * hp.b2;
+        v2 = v2 + (hp.one_minus_b2 * gi) * gi;
+        const float den = sqrtf(v2) / bc2s + hp.eps;
+        xs[tid] = (tid < d) ? xi + (-step_size * m1) / den : 0.f;
       }
       __syncthreads();
-      for (int i = tid; i < dp; i += 256) xs[i] = red[i];
-      __syncthreads();
-      TE_STAMP(4);
-#ifdef KP_TE_STAMPS
-      te_acc[0] += te_ts[1] - te_ts[0];
-      te_acc[1] += te_ts[2] - te_ts[1];
-      te_acc[2] += te_ts[3] - te_ts[2];
-      te_acc[3] += te_ts[4] - te_ts[3];
-#endif
     }
   }
-  for (int i = tid; i < dp; i += 256) x[i] = xs[i];
+  for (int i = tid; i < dp; i += NT) x[i] = xs[i];
 #ifdef KP_TE_STAMPS
-  if (tid == 0) {
-    for (int k = 0; k < 2; ++k) atomicAdd(&g_te_stamps[k], te_acc[k]);
-    atomicAdd(&g_te_stamps[4], 1ull);
-    atomicAdd(&g_te_stamps[5], (unsigned long long)S.R);
-    atomicMax(&g_te_stamps[6], te_acc[0] + te_acc[1] + te_acc[2] + te_acc[3]);
-    atomicMax(&g_te_stamps[7], (unsigned long long)S.R);
-    atomicAdd(&g_te_stamps[2], te_wait);    // (reuses the chunk-sync slot: load wait inside the pair loop)
-    atomicAdd(&g_te_stamps[3], te_rounds);  // (reuses the reduce slot: rounds)
+  if (tid == 0 && blockIdx.x < 8192) {
+    g_te_times[4 * blockIdx.x] = slot;
+    g_te_times[4 * blockIdx.x + 1] = S.R;
+    g_te_times[4 * blockIdx.x + 2] = t_start;
+    g_te_times[4 * blockIdx.x + 3] = wall_clock64();
   }
 #endif
 }
@@ -364,29 +371,50 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   h.one_minus_b1 = (float)(1.0 - (double)hp->beta1);
   h.one_minus_b2 = (float)(1.0 - (double)hp->beta2);
 
+  // longest slots first: a slot's epochs are one dependent chain on one CU
+  std::vector<int32_t> order(ns);
+  for (int s = 0; s < ns; ++s) order[s] = s;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return slots[a].R > slots[b].R; });
+  int32_t* dOrder = upload(c, c->ws[12], order.data(), order.size());
+  KP_REQUIRE(DP <= 512, "TransE: dimension > 512 not supported");
+  int max_r = 0;
+  for (int s = 0; s < ns; ++s) max_r = std::max(max_r, slots[s].R);
+  // one 1024-thread workgroup per CU: a long slot is bound by the row gathers one CU keeps
+  // in flight (measured: 18.6 us per epoch at R 200-400 vs 23.6 with two 512-thread
+  // workgroups per CU sharing it, tools/te_times.py); short slots queue behind
+  int nt = 1024;
+  if (const char* env = std::getenv("KELPIE_TE_NT")) nt = std::atoi(env) == 1024 ? 1024 : 512;  // diagnostics
+  const bool staged = 3 * max_r <= 4 * nt && (size_t)9 * max_r * sizeof(int) <= 48 * 1024;
+  const int nw = nt / 64;
+  const size_t shm = sizeof(float) * (size_t)(1 + nw) * DP + (staged ? sizeof(int) * (size_t)9 * max_r : 0);
+
   KP_HIP(hipEventRecord(c->ev0, c->stream));
   hipEvent_t ea = c->event(0), eb = c->event(1);
   KP_HIP(hipEventRecord(ea, c->stream));
-  const size_t shm = sizeof(float) * (size_t)17 * DP + sizeof(int4) * TE_CH + sizeof(int) * TE_CH;
-  const int vpl = (DP + 63) / 64;
-  switch (vpl) {
-#define TE_CASE(V)                                                                                              \
-  case V:                                                                                                       \
-    hipLaunchKernelGGL(kp_te_posttrain<V>, dim3(ns), dim3(256), shm, c->stream, c->n_ent, DP, c->dim, c->dE, c->dR, \
-                       dSlots, dRows, dRng, h, dX);                                                             \
-    break;
-    TE_CASE(1)
-    TE_CASE(2)
-    TE_CASE(3)
-    TE_CASE(4)
-    TE_CASE(5)
-    TE_CASE(6)
-    TE_CASE(7)
-    TE_CASE(8)
-#undef TE_CASE
-    default:
-      throw KpError{KP_ENOTSUP, "TransE: dimension > 512 not supported"};
+  const int vpl = (DP + 255) / 256;
+#define TE_LAUNCH(V, T, ST)                                                                                    \
+  hipLaunchKernelGGL((kp_te_posttrain<V, T, ST>), dim3(ns), dim3(T), shm, c->stream, c->n_ent, DP, c->dim, c->dE, \
+                     c->dR, dSlots, dOrder, dRows, dRng, h, dX)
+#define TE_STAGE(V, T) \
+  if (staged)          \
+    TE_LAUNCH(V, T, true); \
+  else                 \
+    TE_LAUNCH(V, T, false)
+  if (vpl == 1) {
+    if (nt == 1024) {
+      TE_STAGE(1, 1024);
+    } else {
+      TE_STAGE(1, 512);
+    }
+  } else {
+    if (nt == 1024) {
+      TE_STAGE(2, 1024);
+    } else {
+      TE_STAGE(2, 512);
+    }
   }
+#undef TE_STAGE
+#undef TE_LAUNCH
   KP_HIP(hipGetLastError());
   KP_HIP(hipEventRecord(eb, c->stream));
 
@@ -444,12 +472,8 @@ void transe_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* re
 }
 
 #ifdef KP_TE_STAMPS
-extern "C" int kp_debug_te_stamps(unsigned long long* out, int reset) {
-  KP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_te_stamps), sizeof(unsigned long long) * 8));
-  if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    KP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_te_stamps), z, sizeof(z)));
-  }
+extern "C" int kp_debug_te_times(long long* out, int n) {
+  KP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_te_times), sizeof(long long) * 4 * (size_t)std::min(n, 8192)));
   return 0;
 }
 #endif

@@ -164,12 +164,14 @@ def main():
         out["runs"]["oracle"] = {"relevances": rels, "rank_deltas": deltas}
         print(f"oracle: {rels} deltas {deltas}", flush=True)
     names = list(out["runs"])
-    rates = {}
+    rates, diffs = {}, {}
     for i, a in enumerate(names):
         for b in names[i + 1:]:
             da, db = out["runs"][a]["rank_deltas"], out["runs"][b]["rank_deltas"]
             rates[f"{a} vs {b}"] = float(np.mean([x == y for x, y in zip(da, db)])) if da else None
+            diffs[f"{a} vs {b}"] = int(max(abs(x - y) for x, y in zip(da, db))) if da else None
     out["rank_delta_match_rates"] = rates
+    out["rank_delta_max_abs_diff"] = diffs
     print(json.dumps(rates, indent=1))
     with open(os.path.join(ROOT, "profiles", f"noise_floor_{args.workload}.json"), "w") as f:
         json.dump(out, f, indent=1)
