@@ -37,20 +37,158 @@ struct TeHp {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// component-wise select: a ternary on float4 aggregates can be lowered to a select of
+// addresses, which sends both operands through scratch memory
+__device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {
+  return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
 #ifdef KP_TE_STAMPS
-// diagnostic build only (make stamps): per workgroup [slot, R, start, end] in wall_clock64 ticks (100 MHz)
-__device__ long long g_te_times[4 * 8192];
+// diagnostic build only (make stamps): per workgroup [slot, R, start, end] in wall_clock64 ticks (100 MHz),
+// then s_memtime cycles [wave 0 fetch + load wait, wave 0 compute, sum over steps of the slowest wave's
+// item loop, sum over steps of the whole step (wave 0)]
+__device__ long long g_te_times[8 * 8192];
 #endif
 
 constexpr int TE_NB = 5;  // negatives per bundle held in registers (the reference's ratio; larger ratios loop)
 
-// sum over the 64 lanes, returned wave-uniform: 16-lane DPP sums, then row_bcast15 /
+// sum over the 64 lanes of 16-lane sums (row16_sum), returned wave-uniform: row_bcast15 /
 // row_bcast31 fold the four rows into lane 63
-__device__ __forceinline__ float wave_sum_u(float v) {
-  v = row16_sum(v);
+__device__ __forceinline__ float wave_fold_u(float v) {  // v: 16-lane sums (row16_sum)
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false));
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
+// one work item of kp_te_posttrain: a positive row and up to TE_NB of its negatives
+template <int VPL>
+struct TeItem {
+  int h, t, fz, nb;
+  int ent[TE_NB];
+  bool ch[TE_NB];
+  float4 av[VPL], bb[VPL], bn[TE_NB][VPL];
+};
+
+template <int VPL>
+__device__ __forceinline__ void te_fetch(TeItem<VPL>& I, int it, int cpb, int mb, int ratio, int st, int B,
+                                         const int32_t* order, const int32_t* ents, const int32_t* hot,
+                                         const int32_t* rw, const float* __restrict__ E,
+                                         const float* __restrict__ Rt, int dp, int K, int lane, int NF4) {
+  const int m = mb + it / cpb, c = it - (it / cpb) * cpb;
+  const int ri = __builtin_amdgcn_readfirstlane(order[m]);
+  I.h = __builtin_amdgcn_readfirstlane(rw[3 * ri]);
+  const int r = __builtin_amdgcn_readfirstlane(rw[3 * ri + 1]);
+  I.t = __builtin_amdgcn_readfirstlane(rw[3 * ri + 2]);
+  I.fz = (I.h == K) ? I.t : I.h;  // the positive's frozen side (K too for a self loop)
+  const int j0 = max(m * ratio, st) + c * TE_NB;
+  const int jhi = min(m * ratio + ratio, st + B);
+  I.nb = max(0, min(TE_NB, jhi - j0));
+#pragma unroll
+  for (int q = 0; q < TE_NB; ++q) {
+    const int jj = min(j0 + q, jhi - 1);
+    I.ent[q] = __builtin_amdgcn_readfirstlane(ents[jj]);
+    I.ch[q] = __builtin_amdgcn_readfirstlane(hot[jj]) == 1;
+  }
+  const float* A = E + (size_t)(I.fz == K ? 0 : I.fz) * dp;
+  const float* rel = Rt + (size_t)r * dp;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int f0 = lane + 64 * u;
+    const int f = f0 < NF4 ? f0 : NF4 - 1;
+    I.av[u] = ld4(A + 4 * f);
+    I.bb[u] = ld4(rel + 4 * f);
+#pragma unroll
+    for (int q = 0; q < TE_NB; ++q) I.bn[q][u] = ld4(E + (size_t)(I.ent[q] == K ? 0 : I.ent[q]) * dp + 4 * f);
+  }
+}
+
+// VALU-lean pair math (the kernel is VALU-bound per CU, tools/te_times.py): lhs + rel
+// of the positive is shared by every tail-corrupted negative, squared norms are FMA
+// chains, the item's TE_NB norm reductions run interleaved, negatives without the
+// kelpie entity (zero gradient, the hinge only) skip the gradient FMAs, and the
+// positive's gradient is applied once with the summed coefficient.
+template <int VPL>
+__device__ __forceinline__ void te_compute(const TeItem<VPL>& I, const float* xs, int K, int lane, int NF4,
+                                           float margin, float4* g, int& cnt) {
+  const int h = I.h, t = I.t;
+  float4 rp[VPL], lb[VPL], vp[VPL];
+  float sp = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int f0 = lane + 64 * u;
+    const bool on = f0 < NF4;
+    const float4 xk = ld4(xs + 4 * (on ? f0 : NF4 - 1));
+    const float4 av = sel4(I.fz == K, xk, I.av[u]);
+    const float4 lp = sel4(h == K, xk, av);
+    rp[u] = sel4(t == K, xk, av);
+    const float4 b = I.bb[u];
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    lb[u] = make_float4(lp.x + b.x, lp.y + b.y, lp.z + b.z, lp.w + b.w);
+    // positive: v+ = (lhs + rel) - rhs, zero past the row end
+    vp[u] = sel4(on, make_float4(lb[u].x - rp[u].x, lb[u].y - rp[u].y, lb[u].z - rp[u].z, lb[u].w - rp[u].w), z);
+    sp = fmaf(vp[u].x, vp[u].x, fmaf(vp[u].y, vp[u].y, fmaf(vp[u].z, vp[u].z, fmaf(vp[u].w, vp[u].w, sp))));
+  }
+  float4 vn[TE_NB][VPL];
+  float sn[TE_NB];
+#pragma unroll
+  for (int q = 0; q < TE_NB; ++q) {
+    const bool ch = I.ch[q];
+    sn[q] = 0.f;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      const int f0 = lane + 64 * u;
+      const bool on = f0 < NF4;
+      const float4 bq = sel4(I.ent[q] == K, ld4(xs + 4 * (on ? f0 : NF4 - 1)), I.bn[q][u]);
+      const float4 b = I.bb[u];
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      // corrupted head: (e_n + rel) - rhs; corrupted tail: (lhs + rel) - e_n
+      const float4 vh = make_float4((bq.x + b.x) - rp[u].x, (bq.y + b.y) - rp[u].y, (bq.z + b.z) - rp[u].z,
+                                    (bq.w + b.w) - rp[u].w);
+      const float4 vt = make_float4(lb[u].x - bq.x, lb[u].y - bq.y, lb[u].z - bq.z, lb[u].w - bq.w);
+      const float4 v = sel4(ch, vh, vt);
+      vn[q][u] = sel4(on, v, z);
+      sn[q] = fmaf(vn[q][u].x, vn[q][u].x,
+                   fmaf(vn[q][u].y, vn[q][u].y, fmaf(vn[q][u].z, vn[q][u].z, fmaf(vn[q][u].w, vn[q][u].w, sn[q]))));
+    }
+  }
+  // TE_NB + 1 independent wave reductions, interleaved
+  sp = row16_sum(sp);
+#pragma unroll
+  for (int q = 0; q < TE_NB; ++q) sn[q] = row16_sum(sn[q]);
+  const float fp = sqrtf(wave_fold_u(sp));
+  const float sgn_p = (float)((h == K) - (t == K));
+  float cps = 0.f;
+#pragma unroll
+  for (int q = 0; q < TE_NB; ++q) {
+    const float fn = sqrtf(wave_fold_u(sn[q]));
+    if (q >= I.nb) continue;
+    const bool ch = I.ch[q];
+    const int ent = I.ent[q];
+    const int hn = ch ? ent : h, tn = ch ? t : ent;
+    const bool act = (fp - fn) + margin >= 0.f;  // clamp_min backward passes grad where self >= min
+    const float sgn_n = (float)((hn == K) - (tn == K));
+    cps += (act && fp > 0.f) ? sgn_p / fp : 0.f;
+    const float cn = (act && fn > 0.f) ? -sgn_n / fn : 0.f;
+    if (cn != 0.f) {
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) {
+        g[u].x = fmaf(cn, vn[q][u].x, g[u].x);
+        g[u].y = fmaf(cn, vn[q][u].y, g[u].y);
+        g[u].z = fmaf(cn, vn[q][u].z, g[u].z);
+        g[u].w = fmaf(cn, vn[q][u].w, g[u].w);
+      }
+    }
+    cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
+  }
+  if (cps != 0.f) {
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+      g[u].x = fmaf(cps, vp[u].x, g[u].x);
+      g[u].y = fmaf(cps, vp[u].y, g[u].y);
+      g[u].z = fmaf(cps, vp[u].z, g[u].z);
+      g[u].w = fmaf(cps, vp[u].w, g[u].w);
+    }
+  }
 }
 
 // One workgroup per slot (slots issued longest first) runs every epoch on chip: x in
@@ -98,6 +236,9 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
   float* x = X + (size_t)slot * dp;
 #ifdef KP_TE_STAMPS
   const long long t_start = wall_clock64();
+  long long st_fetch = 0, st_comp = 0, st_red = 0, st_items = 0;
+  __shared__ unsigned long long loop_max_s;
+  if (tid == 0) loop_max_s = 0;
 #endif
   for (int i = tid; i < dp; i += NT) xs[i] = x[i];
   float m1 = 0.f, v2 = 0.f;  // Adam moments of element tid (tid < dp)
@@ -134,90 +275,36 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
 #pragma unroll
       for (int u = 0; u < VPL; ++u) g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       int cnt = 0;
-      // bundles overlapping the step's positions [st, st + B)
-      for (int m = st / ratio + wave; m * ratio < st + B; m += TE_NW) {
-        const int ri = __builtin_amdgcn_readfirstlane(order[m]);
-        const int h = __builtin_amdgcn_readfirstlane(rw[3 * ri]);
-        const int r = __builtin_amdgcn_readfirstlane(rw[3 * ri + 1]);
-        const int t = __builtin_amdgcn_readfirstlane(rw[3 * ri + 2]);
-        const int fz = (h == K) ? t : h;  // the positive's frozen side (K too for a self loop)
-        const float* A = E + (size_t)(fz == K ? 0 : fz) * dp;
-        const float* rel = Rt + (size_t)r * dp;
-        const int jlo = max(m * ratio, st), jhi = min(m * ratio + ratio, st + B);
-        for (int j0 = jlo; j0 < jhi; j0 += TE_NB) {
-          const int nb = min(TE_NB, jhi - j0);
-          int ent[TE_NB];
-          bool ch[TE_NB];
-#pragma unroll
-          for (int q = 0; q < TE_NB; ++q) {
-            const int jj = j0 + min(q, nb - 1);
-            ent[q] = __builtin_amdgcn_readfirstlane(ents[jj]);
-            ch[q] = __builtin_amdgcn_readfirstlane(hot[jj]) == 1;
-          }
-          float4 lp[VPL], rp[VPL], bb[VPL], bn[TE_NB][VPL];
-#pragma unroll
-          for (int u = 0; u < VPL; ++u) {
-            const int f0 = lane + 64 * u;
-            const int f = f0 < NF4 ? f0 : NF4 - 1;
-            const float4 xk = ld4(xs + 4 * f);
-            float4 av = ld4(A + 4 * f);
-            bb[u] = ld4(rel + 4 * f);
-#pragma unroll
-            for (int q = 0; q < TE_NB; ++q) bn[q][u] = ld4(E + (size_t)(ent[q] == K ? 0 : ent[q]) * dp + 4 * f);
-            if (fz == K) av = xk;
-#pragma unroll
-            for (int q = 0; q < TE_NB; ++q)
-              if (ent[q] == K) bn[q][u] = xk;
-            lp[u] = (h == K) ? xk : av;
-            rp[u] = (t == K) ? xk : av;
-          }
-          // positive: v+ = (lhs + rel) - rhs, zero past the row end
-          float4 vp[VPL];
-          float sp = 0.f;
-#pragma unroll
-          for (int u = 0; u < VPL; ++u) {
-            const bool on = lane + 64 * u < NF4;
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            vp[u] = on ? make_float4((lp[u].x + bb[u].x) - rp[u].x, (lp[u].y + bb[u].y) - rp[u].y,
-                                     (lp[u].z + bb[u].z) - rp[u].z, (lp[u].w + bb[u].w) - rp[u].w)
-                       : z;
-            sp += vp[u].x * vp[u].x + vp[u].y * vp[u].y + vp[u].z * vp[u].z + vp[u].w * vp[u].w;
-          }
-          const float fp = sqrtf(wave_sum_u(sp));
-          const float sgn_p = (float)((h == K) - (t == K));
-#pragma unroll
-          for (int q = 0; q < TE_NB; ++q) {
-            if (q >= nb) break;
-            const int hn = ch[q] ? ent[q] : h, tn = ch[q] ? t : ent[q];
-            float4 vn[VPL];
-            float sn = 0.f;
-#pragma unroll
-            for (int u = 0; u < VPL; ++u) {
-              const bool on = lane + 64 * u < NF4;
-              const float4 ln = ch[q] ? bn[q][u] : lp[u], rn = ch[q] ? rp[u] : bn[q][u];
-              const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-              vn[u] = on ? make_float4((ln.x + bb[u].x) - rn.x, (ln.y + bb[u].y) - rn.y, (ln.z + bb[u].z) - rn.z,
-                                       (ln.w + bb[u].w) - rn.w)
-                         : z;
-              sn += vn[u].x * vn[u].x + vn[u].y * vn[u].y + vn[u].z * vn[u].z + vn[u].w * vn[u].w;
-            }
-            const float fn = sqrtf(wave_sum_u(sn));
-            const float zz = (fp - fn) + hp.margin;
-            const bool act = zz >= 0.f;  // clamp_min backward passes grad where self >= min
-            const float sgn_n = (float)((hn == K) - (tn == K));
-            const float cp = (act && fp > 0.f) ? sgn_p / fp : 0.f;
-            const float cn = (act && fn > 0.f) ? -sgn_n / fn : 0.f;
-#pragma unroll
-            for (int u = 0; u < VPL; ++u) {
-              g[u].x += cp * vp[u].x + cn * vn[u].x;
-              g[u].y += cp * vp[u].y + cn * vn[u].y;
-              g[u].z += cp * vp[u].z + cn * vn[u].z;
-              g[u].w += cp * vp[u].w + cn * vn[u].w;
-            }
-            cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
-          }
-        }
+      // work items: (bundle m, chunk of <= TE_NB of its negatives) over the bundles that
+      // overlap the step's positions [st, st + B), strided over the waves
+      const int cpb = (ratio + TE_NB - 1) / TE_NB;
+      const int mb = st / ratio;
+      const int n_items = ((st + B - 1) / ratio - mb + 1) * cpb;
+#ifdef KP_TE_STAMPS
+      const long long c_step = __builtin_amdgcn_s_memtime();
+#endif
+      for (int it = wave; it < n_items; it += TE_NW) {
+        TeItem<VPL> I;
+#ifdef KP_TE_STAMPS
+        const long long c0 = __builtin_amdgcn_s_memtime();
+#endif
+        te_fetch<VPL>(I, it, cpb, mb, ratio, st, B, order, ents, hot, rw, E, Rt, dp, K, lane, NF4);
+#ifdef KP_TE_STAMPS
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const long long c1 = __builtin_amdgcn_s_memtime();
+#endif
+        te_compute<VPL>(I, xs, K, lane, NF4, hp.margin, g, cnt);
+#ifdef KP_TE_STAMPS
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const long long c2 = __builtin_amdgcn_s_memtime();
+        st_fetch += c1 - c0;
+        st_comp += c2 - c1;
+#endif
       }
+#ifdef KP_TE_STAMPS
+      const long long c3 = __builtin_amdgcn_s_memtime();
+      if (lane == 0) atomicMax(&loop_max_s, (unsigned long long)(c3 - c_step));
+#endif
       if (STAGED && e + 1 < hp.epochs && st + hp.bs >= S.R) {  // last step of the epoch
         int* nb_ = drw + ((e + 1) & 1) * R3;
 #pragma unroll
@@ -254,15 +341,26 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
         xs[tid] = (tid < d) ? xi + (-step_size * m1) / den : 0.f;
       }
       __syncthreads();
+#ifdef KP_TE_STAMPS
+      st_red += __builtin_amdgcn_s_memtime() - c_step;
+      st_items += (long long)loop_max_s;
+      __syncthreads();
+      if (tid == 0) loop_max_s = 0;
+#endif
     }
   }
   for (int i = tid; i < dp; i += NT) x[i] = xs[i];
 #ifdef KP_TE_STAMPS
   if (tid == 0 && blockIdx.x < 8192) {
-    g_te_times[4 * blockIdx.x] = slot;
-    g_te_times[4 * blockIdx.x + 1] = S.R;
-    g_te_times[4 * blockIdx.x + 2] = t_start;
-    g_te_times[4 * blockIdx.x + 3] = wall_clock64();
+    long long* o = g_te_times + 8 * blockIdx.x;
+    o[0] = slot;
+    o[1] = S.R;
+    o[2] = t_start;
+    o[3] = wall_clock64();
+    o[4] = st_fetch;
+    o[5] = st_comp;
+    o[6] = st_red;
+    o[7] = st_items;
   }
 #endif
 }
@@ -382,7 +480,7 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   // one 1024-thread workgroup per CU: a long slot is bound by the row gathers one CU keeps
   // in flight (measured: 18.6 us per epoch at R 200-400 vs 23.6 with two 512-thread
   // workgroups per CU sharing it, tools/te_times.py); short slots queue behind
-  int nt = 1024;
+  int nt = DP > 256 ? 512 : 1024;  // two float4 per lane need > 128 VGPRs: 8 waves per workgroup
   if (const char* env = std::getenv("KELPIE_TE_NT")) nt = std::atoi(env) == 1024 ? 1024 : 512;  // diagnostics
   const bool staged = 3 * max_r <= 4 * nt && (size_t)9 * max_r * sizeof(int) <= 48 * 1024;
   const int nw = nt / 64;
@@ -407,11 +505,7 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       TE_STAGE(1, 512);
     }
   } else {
-    if (nt == 1024) {
-      TE_STAGE(2, 1024);
-    } else {
-      TE_STAGE(2, 512);
-    }
+    TE_STAGE(2, 512);
   }
 #undef TE_STAGE
 #undef TE_LAUNCH
@@ -473,7 +567,7 @@ void transe_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* re
 
 #ifdef KP_TE_STAMPS
 extern "C" int kp_debug_te_times(long long* out, int n) {
-  KP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_te_times), sizeof(long long) * 4 * (size_t)std::min(n, 8192)));
+  KP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_te_times), sizeof(long long) * 8 * (size_t)std::min(n, 8192)));
   return 0;
 }
 #endif

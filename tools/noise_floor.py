@@ -132,7 +132,8 @@ def main():
         from src.relevance_engines import SufficientPostTrainingEngine
         ref_harness.seed_all(42)
         se = SufficientPostTrainingEngine(model, dataset, wl["hp"])
-        ents = [int(e) for e in se.select_entities_to_convert(pred, wl["convert"], 200)]
+        se.select_entities_to_convert(pred, wl["convert"], 200)  # sets entities_to_convert (engine.py:125)
+        ents = [int(e) for e in se.entities_to_convert]
     out = {"workload": args.workload, "pred": list(pred), "candidates": [list(c) for c in cands],
            "entities_to_convert": ents, "runs": {}}
     for t in args.threads:

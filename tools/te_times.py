@@ -33,9 +33,9 @@ for i in range(2):
     eng.compute_relevance_multi([(p, [[c] for c in bench.candidates_of(ds, p, wl["candidates"])])
                                  for p in preds[i * k:(i + 1) * k]])
     n = eng.last_batch_stats["slots"]
-    buf = np.zeros(4 * n, np.int64)
+    buf = np.zeros(8 * n, np.int64)
     L.kp_debug_te_times(buf.ctypes.data, n)
-    t = buf.reshape(n, 4)
+    t = buf.reshape(n, 8)
     t0 = t[:, 2].min()
     dur = (t[:, 3] - t[:, 2]) / 100.0  # us
     print(f"batch {i}: {n} slots, launch span {(t[:, 3].max() - t0) / 100:.0f} us, "
@@ -46,3 +46,6 @@ for i in range(2):
         if sel.any():
             print(f"  R in [{lo},{hi}): {sel.sum():4d} slots, dur mean {dur[sel].mean():7.0f} us max {dur[sel].max():7.0f}"
                   f", per epoch {dur[sel].mean() / ep:6.2f} us, start max {(t[sel, 2].max() - t0) / 100:6.0f} us")
+            print(f"     cycles per epoch: wave 0 fetch+wait {np.mean(t[sel, 4]) / ep:7.0f}, wave 0 compute "
+                  f"{np.mean(t[sel, 5]) / ep:7.0f}, slowest wave's item loop {np.mean(t[sel, 7]) / ep:7.0f}, "
+                  f"whole step {np.mean(t[sel, 6]) / ep:7.0f}")
