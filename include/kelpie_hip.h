@@ -164,6 +164,28 @@ int kp_convertible(kp_ctx* ctx, int32_t n, const int32_t* heads, int32_t rel, in
 int kp_predict_tails(kp_ctx* ctx, int32_t n, const int32_t* triples, const int32_t* filt_off, const int32_t* filt,
                      float* out_score, int64_t* out_rank);
 
+/* Data-poisoning relevance, ComplEx (src/relevance_engines/data_poisoning_engine.py:
+ * DPEngine.get_gradient :21-49, NecessaryDPEngine.compute_relevance :52-94,
+ * SufficientDPEngine.compute_individual_relevance :97-137; the other models have no
+ * score_embeddings and raise in the reference).  items[n][7] = (pred s, p, o,
+ * perspective entity e, triple h, r, t).  Per item: g = d score(s, p, o) / d emb(e)
+ * (the lhs when e == s, else the rhs), e' = emb(e) + step_sign * (epsilon * g), the
+ * triple's score with e' in its head when h == e (else in its tail), and
+ * out[i] = rel_sign * (score - lambd * perturbed score). */
+int kp_dp_relevance(kp_ctx* ctx, int32_t n, const int32_t* items, float epsilon, float lambd, int32_t step_sign,
+                    int32_t rel_sign, float* out);
+
+/* CRIAGE score variation (src/relevance_engines/criage_engine.py: compute_hessian
+ * :74-104, estimate_score_variation :107-134 / :158-177), ComplEx and ConvE.
+ * items[n][5] = (z_pred s, p, z_triple s, p, entity slot); z = criage_first_step
+ * (complex.py:131, conve.py:102-124).  Entity slot k is ent_ids[k] with tail
+ * triples (h, r) = tails[tails_off[k] .. tails_off[k+1]) in training order.
+ * out[i] = z_pred . ((1 - sig) z_triple A^{-1}), A = H_e + sig (1 - sig) z^T z,
+ * sig = sigmoid(e . z_triple), in float64 (the necessary engine negates it);
+ * status[i] = 1 when A is exactly singular (numpy.linalg.inv raises). */
+int kp_criage_relevance(kp_ctx* ctx, int32_t n, const int32_t* items, int32_t n_ents, const int32_t* ent_ids,
+                        const int32_t* tails_off, const int32_t* tails, double* out, int32_t* status);
+
 /* Advance a torch CPU generator state (the 5056-byte torch.get_rng_state()
  * blob) by n 32-bit mt19937 outputs, in place.  Used by the host RNG protocol
  * to replay the draws of reset_parameters() that each KelpieConvE

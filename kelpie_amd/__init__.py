@@ -10,6 +10,8 @@ from .engine import NecessaryPostTrainingEngine, PostTrainingEngine, SufficientP
 from .models import MODEL_REGISTRY, ComplEx, ConvE, TransE, from_state_dict  # noqa: F401
 from .builder import StochasticBuilder  # noqa: F401
 from .prefilters import NoPreFilter, TopologyPreFilter, WeightedTopologyPreFilter  # noqa: F401
+from .baselines import (CriagePreFilter, NecessaryCriageEngine, NecessaryDPEngine, SufficientCriageEngine,  # noqa: F401
+                        SufficientDPEngine)
 from .pipeline import NecessaryPipeline, SufficientPipeline, build_pipeline, explain_preds, read_preds  # noqa: F401
 
 __version__ = "0.1.0"

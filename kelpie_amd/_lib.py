@@ -21,7 +21,7 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
            "kp_rng_transe_epochs", "kp_rng_conve_masks", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
-           "kp_predict_tails"]
+           "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance"]
 
 
 class ModelDesc(C.Structure):
@@ -68,6 +68,10 @@ def lib():
         L.kp_mt19937_discard.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         L.kp_predict_tails.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p]
+        L.kp_dp_relevance.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_float, C.c_float, C.c_int32, C.c_int32,
+                                       C.c_void_p]
+        L.kp_criage_relevance.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_graph_create.argtypes = [C.c_int32, C.c_int64, C.c_void_p, C.POINTER(C.c_void_p)]
         L.kp_graph_destroy.argtypes = [C.c_void_p]
         L.kp_graph_destroy.restype = None
@@ -213,6 +217,27 @@ class Context:
         check(lib().kp_predict_tails(self.h, len(t), _ptr(t), _ptr(filt_off), _ptr(filt), _ptr(score), _ptr(rank)),
               self.h)
         return score, rank
+
+    def dp_relevance(self, items, epsilon, lambd, step_sign, rel_sign):
+        """kp_dp_relevance: items int [n, 7] -> float32 [n]."""
+        it = np.ascontiguousarray(np.asarray(items, dtype=np.int32).reshape(-1, 7))
+        out = np.zeros(len(it), np.float32)
+        check(lib().kp_dp_relevance(self.h, len(it), _ptr(it), float(epsilon), float(lambd), int(step_sign),
+                                    int(rel_sign), _ptr(out)), self.h)
+        return out
+
+    def criage_relevance(self, items, ent_ids, tails_off, tails):
+        """kp_criage_relevance: items int [n, 5] -> (float64 [n], status int32 [n])."""
+        it = np.ascontiguousarray(np.asarray(items, dtype=np.int32).reshape(-1, 5))
+        ents = np.ascontiguousarray(ent_ids, dtype=np.int32)
+        off = np.ascontiguousarray(tails_off, dtype=np.int32)
+        tl = np.ascontiguousarray(np.asarray(tails, dtype=np.int32).reshape(-1, 2)) if len(tails) \
+            else np.zeros((1, 2), np.int32)
+        out = np.zeros(len(it), np.float64)
+        status = np.zeros(len(it), np.int32)
+        check(lib().kp_criage_relevance(self.h, len(it), _ptr(it), len(ents), _ptr(ents), _ptr(off), _ptr(tl),
+                                        _ptr(out), _ptr(status)), self.h)
+        return out, status
 
     def last_timing(self):
         a, b, n, w = C.c_double(), C.c_double(), C.c_int64(), C.c_double()

@@ -232,6 +232,30 @@ int kp_predict_tails(kp_ctx* c, int32_t n, const int32_t* triples, const int32_t
   });
 }
 
+int kp_dp_relevance(kp_ctx* c, int32_t n, const int32_t* items, float epsilon, float lambd, int32_t step_sign,
+                    int32_t rel_sign, float* out) {
+  if (!c || n < 0 || (n > 0 && (!items || !out)) || (step_sign != 1 && step_sign != -1) ||
+      (rel_sign != 1 && rel_sign != -1))
+    return KP_EINVAL;
+  return guarded(c, [&] {
+    if (n == 0) return;
+    KP_HIP(hipSetDevice(c->device));
+    dp_relevance(c, n, items, epsilon, lambd, step_sign, rel_sign, out);
+  });
+}
+
+int kp_criage_relevance(kp_ctx* c, int32_t n, const int32_t* items, int32_t n_ents, const int32_t* ent_ids,
+                        const int32_t* tails_off, const int32_t* tails, double* out, int32_t* status) {
+  if (!c || n < 0 || n_ents < 0 || (n > 0 && (!items || !out || !status || n_ents == 0)) ||
+      (n_ents > 0 && (!ent_ids || !tails_off)))
+    return KP_EINVAL;
+  return guarded(c, [&] {
+    if (n == 0) return;
+    KP_HIP(hipSetDevice(c->device));
+    criage_relevance(c, n, items, n_ents, ent_ids, tails_off, tails, out, status);
+  });
+}
+
 // The host RNG protocol entry points (kp_rng_*, kp_mt19937_discard) are in kp_rng.cpp.
 
 int kp_last_timing(const kp_ctx* c, double* dev_s, double* hot_s, int64_t* hot_n, double* hot_w) {

@@ -153,6 +153,13 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* b);
 void transe_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rels, float* out);
 void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* b);
 void conve_all_scores(kp_ctx* c, int n, const int32_t* heads, const int32_t* rels, float* out);
+// ConvE encoder output (eval mode) of n (lhs, rel) pairs -> [n][dp] (criage_first_step, conve.py:102-124)
+void conve_encode_dev(kp_ctx* c, int n, const int2* d_src, float* d_out);
+// baseline engines (kp_baselines.hip)
+void dp_relevance(kp_ctx* c, int n, const int32_t* items, float eps, float lambd, int step_sign, int rel_sign,
+                  float* out);
+void criage_relevance(kp_ctx* c, int n, const int32_t* items, int n_ents, const int32_t* ent_ids,
+                      const int32_t* tails_off, const int32_t* tails, double* out, int32_t* status);
 
 // shared rank kernel launcher (kp_rank.hip): scores [n][ld] already on device,
 // column `kcol` = kelpie score (or -1 when absent)

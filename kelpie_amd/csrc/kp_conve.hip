@@ -351,6 +351,8 @@ void encode_eval(kp_ctx* c, int n, const int2* dsrc, const float* dX, float* dQ)
 
 float* conve_fc_wt(kp_ctx* c);
 
+void conve_encode_dev(kp_ctx* c, int n, const int2* d_src, float* d_out) { encode_eval(c, n, d_src, nullptr, d_out); }
+
 void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   const int ns = bt->n_slots;
   const int K = c->n_ent;

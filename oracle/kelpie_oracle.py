@@ -797,3 +797,155 @@ def topology_prefilter(ds: OracleDataset, pred, k):
     res = {t: dist(t[2] if t[0] == s else t[0]) for t in triples}
     res = sorted(res.items(), key=lambda x: x[1])
     return [t for t, _ in res][:k]
+
+
+# ---------------------------------------------------------------------------- baseline engines (§8(f) f4)
+def complex_score_rows(om: OracleModel, lhs, rel, rhs):
+    """``ComplEx.score_embeddings`` (complex.py:48-57): sum over d of
+    (l0 r0 - l1 r1) rh0 + (l0 r1 + l1 r0) rh1, float32."""
+    d = om.dim
+    l0, l1 = lhs[..., :d], lhs[..., d:]
+    r0, r1 = rel[..., :d], rel[..., d:]
+    h0, h1 = rhs[..., :d], rhs[..., d:]
+    real = ((l0 * r0 - l1 * r1) * h0).astype(F32)
+    im = ((l0 * r1 + l1 * r0) * h1).astype(F32)
+    return (real + im).astype(F32).sum(-1, dtype=F32)
+
+
+def complex_score_grad(om: OracleModel, triple, entity):
+    """``DPEngine.get_gradient`` (data_poisoning_engine.py:21-49): d score / d (lhs if
+    entity == s else rhs), as torch's autograd forms it element by element."""
+    s, p, o = triple
+    d = om.dim
+    lhs, rel, rhs = om.E[s], om.R[p], om.E[o]
+    l0, l1, r0, r1, h0, h1 = lhs[:d], lhs[d:], rel[:d], rel[d:], rhs[:d], rhs[d:]
+    if entity == s:
+        return np.concatenate([h0 * r0 + h1 * r1, -(h0 * r1) + h1 * r0]).astype(F32)
+    return np.concatenate([l0 * r0 - l1 * r1, l0 * r1 + l1 * r0]).astype(F32)
+
+
+def dp_individual(om: OracleModel, pred, perspective, triple, epsilon, lambd, mode):
+    """``NecessaryDPEngine.compute_relevance`` / ``SufficientDPEngine.compute_individual_relevance``
+    (data_poisoning_engine.py:52-94, 97-137).  ComplEx only: the other models have no
+    ``score_embeddings`` (AttributeError in the reference)."""
+    if om.name != "ComplEx":
+        raise AttributeError(f"'{om.name}' object has no attribute 'score_embeddings'")
+    pred_s, _, pred_o = pred
+    s = triple[0]
+    entity = pred_s if perspective == "head" else pred_o
+    g = complex_score_grad(om, pred, entity)
+    e = om.E[entity]
+    step = (F32(epsilon) * g).astype(F32)
+    toward = (mode == "necessary") == om.is_minimizer()  # minimizer/necessary: + eps g
+    pert = (e + step if toward else e - step).astype(F32)
+    t = np.asarray([triple, triple])
+    lhs, rel, rhs = om.E[t[:, 0]].copy(), om.R[t[:, 1]], om.E[t[:, 2]].copy()
+    if s == entity:
+        lhs[1] = pert
+    else:
+        rhs[1] = pert
+    orig, per = complex_score_rows(om, lhs, rel, rhs)
+    diff = F32(orig - F32(lambd * per))
+    if mode == "necessary":
+        return F32(-diff) if om.is_minimizer() else diff
+    return diff if om.is_minimizer() else F32(-diff)
+
+
+def dp_relevance(om: OracleModel, pred, perspective, triple, epsilon, mode, entities=None, lambd=1):
+    if mode == "necessary":
+        return dp_individual(om, pred, perspective, triple, epsilon, lambd, mode)
+    pred_s = pred[0]
+    rels = []
+    for ent in entities:
+        # the reference rebinds triple and pred inside its loop (data_poisoning_engine.py:144-146),
+        # so every conversion after the first reuses the first conversion's triple and pred
+        triple = replace_entity(tuple(triple), pred_s, ent)
+        pred = replace_entity(tuple(pred), pred_s, ent)
+        rels.append(dp_individual(om, pred, perspective, triple, epsilon, lambd, mode))
+    acc = 0
+    for r in rels:
+        acc = acc + r
+    return acc / len(rels)
+
+
+def criage_z(om: OracleModel, triple):
+    """``criage_first_step`` of (s, p): ComplEx query (complex.py:131-132), ConvE encoder output
+    (conve.py:102-124, eval mode)."""
+    s, p = triple[0], triple[1]
+    lhs, rel = om.E[s][None], om.R[p][None]
+    if om.name == "ComplEx":
+        return om.complex_query(lhs, rel)
+    if om.name == "ConvE":
+        return om.conve_encode(lhs, rel)[0]
+    raise Exception("Criage does not support this model.")
+
+
+def _np_sigmoid(x):
+    return 1 / (1 + np.exp(-x))
+
+
+def criage_hessian(om: OracleModel, entity, tail_triples):
+    """``CriageEngine.compute_hessian`` (criage_engine.py:74-104): float32 terms
+    sig' * x^T x (x = lhs * rel elementwise) accumulated in float64, in triple order."""
+    e = om.E[entity]
+    D = om.E.shape[1]
+    H = np.zeros((D, D))
+    for s, p, _ in tail_triples:
+        x = (om.E[s] * om.R[p]).astype(F32).reshape(1, -1)
+        x2 = np.dot(e, x.T)
+        sig = _np_sigmoid(x2)
+        sig = sig * (1 - sig)
+        H += sig * np.dot(x.T, x)
+    return H
+
+
+def criage_variation(om: OracleModel, z_pred, z_triple, entity, H, mode):
+    """``estimate_score_variation`` (criage_engine.py:107-134, 158-177), float64 solve."""
+    e = om.E[entity]
+    x2 = np.dot(e, z_triple.T)
+    sig = _np_sigmoid(x2)
+    A = H + sig * (1 - sig) * np.dot(z_triple.T, z_triple)
+    m = np.linalg.inv(A)
+    rel = np.dot(z_pred, ((1 - sig) * np.dot(z_triple, m)).T)
+    return -rel[0][0] if mode == "necessary" else rel[0][0]
+
+
+def criage_relevance(om: OracleModel, ds: OracleDataset, pred, triple, perspective, mode, entities=None,
+                     tails=None):
+    """``Necessary/SufficientCriageEngine.compute_relevance`` (criage_engine.py:30-52, 140-155)."""
+    if tails is None:
+        tails = defaultdict(list)
+        for h, r, t in ds.training_triples.tolist():
+            tails[t].append((h, r, t))
+
+    def one(pred, triple):
+        ps, pp, po = pred
+        ent = po if perspective == "tail" else ps
+        if perspective == "head":
+            pred = (po, pp, ps)
+        H = criage_hessian(om, ent, tails.get(ent, []))
+        return criage_variation(om, criage_z(om, pred), criage_z(om, triple), ent, H, mode)
+
+    if mode == "necessary":
+        return one(tuple(pred), tuple(triple))
+    ps, pp, po = pred
+    s, p, _ = triple
+    rels = []
+    for ent in entities:
+        t2 = (s, p, ent)
+        p2 = (ent, pp, po) if perspective == "head" else (ps, pp, ent)
+        rels.append(one(p2, t2))
+    return sum(rels) / len(rels)
+
+
+def criage_prefilter(ds: OracleDataset, pred, k=50):
+    """``CriagePreFilter.select_triples`` (criage_prefilter.py:14-27)."""
+    tails = defaultdict(list)
+    for h, r, t in ds.training_triples.tolist():
+        tails[t].append((h, r, t))
+    s, _, o = pred
+    oo = sorted(tails.get(o, []))
+    so = sorted(tails.get(s, []))
+    if k == -1:
+        return oo + so
+    return oo[:k] + so[:k]

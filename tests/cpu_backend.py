@@ -161,3 +161,46 @@ class OracleBackedContext:
 
     def last_timing(self):
         return {"device_s": 0.0, "hot_s": 0.0, "hot_launches": 0}
+
+
+def _dp_relevance(self, items, epsilon, lambd, step_sign, rel_sign):
+    """Stand-in for kp_dp_relevance (oracle arithmetic on the shipped items)."""
+    om = self.om
+    out = []
+    for s, p, o, e, h, r, t in np.asarray(items).reshape(-1, 7).tolist():
+        g = ko.complex_score_grad(om, (s, p, o), e)
+        step = (np.float32(epsilon) * g).astype(np.float32)
+        pert = (om.E[e] + step if step_sign > 0 else om.E[e] - step).astype(np.float32)
+        lhs, rel, rhs = om.E[[h, h]].copy(), om.R[[r, r]], om.E[[t, t]].copy()
+        if h == e:
+            lhs[1] = pert
+        else:
+            rhs[1] = pert
+        a, b = ko.complex_score_rows(om, lhs, rel, rhs)
+        out.append(np.float32(rel_sign) * np.float32(a - np.float32(lambd * b)))
+    return np.asarray(out, np.float32)
+
+
+def _criage_relevance(self, items, ent_ids, tails_off, tails):
+    """Stand-in for kp_criage_relevance."""
+    om = self.om
+    H = {}
+    out, status = [], []
+    for zs, zp, ts, tp, slot in np.asarray(items).reshape(-1, 5).tolist():
+        ent = int(ent_ids[slot])
+        if ent not in H:
+            tl = [(h, r, ent) for h, r in np.asarray(tails).reshape(-1, 2)[tails_off[slot]:tails_off[slot + 1]].tolist()]
+            H[ent] = ko.criage_hessian(om, ent, tl)
+        try:
+            v = ko.criage_variation(om, ko.criage_z(om, (zs, zp, 0)), ko.criage_z(om, (ts, tp, 0)), ent, H[ent],
+                                    "sufficient")
+            out.append(float(v))
+            status.append(0)
+        except np.linalg.LinAlgError:
+            out.append(float("nan"))
+            status.append(1)
+    return np.asarray(out), np.asarray(status, np.int32)
+
+
+OracleBackedContext.dp_relevance = _dp_relevance
+OracleBackedContext.criage_relevance = _criage_relevance
