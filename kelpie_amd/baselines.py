@@ -73,6 +73,16 @@ class NecessaryDPEngine(DPEngine):
     def compute_relevance_batch(self, pred, perspective: str, triples):
         return [np.float32(v) for v in self._run(self._items(pred, perspective, triples), "necessary")]
 
+    def compute_relevance_multi(self, jobs, perspective: str):
+        """[(pred, triples), ...] in one launch -> [[relevance per triple], ...]."""
+        items = [it for pred, triples in jobs for it in self._items(pred, perspective, triples)]
+        vals = self._run(items, "necessary")
+        out, k = [], 0
+        for _, triples in jobs:
+            out.append([np.float32(v) for v in vals[k:k + len(triples)]])
+            k += len(triples)
+        return out
+
 
 class SufficientDPEngine(DPEngine):
     """data_poisoning_engine.py:97-152."""
@@ -152,6 +162,15 @@ class NecessaryCriageEngine(CriageEngine):
     def compute_relevance_batch(self, pred, triples, perspective: str):
         vals, status = self._items([(pred, t) for t in triples], perspective)
         return [None if st else -float(v) for v, st in zip(vals, status)]
+
+    def compute_relevance_multi(self, jobs, perspective: str):
+        """[(pred, triples), ...] in one launch (one Hessian per distinct entity)."""
+        vals, status = self._items([(pred, t) for pred, triples in jobs for t in triples], perspective)
+        out, k = [], 0
+        for _, triples in jobs:
+            out.append([None if st else -float(v) for v, st in zip(vals[k:k + len(triples)], status[k:k + len(triples)])])
+            k += len(triples)
+        return out
 
 
 class SufficientCriageEngine(CriageEngine):

@@ -163,9 +163,9 @@ __global__ __launch_bounds__(256) void kp_criage_solve(int D, int dp, const int3
   __syncthreads();
   const float sig = sig_s;
   const float c = sig * (1.0f - sig);
-  for (int idx = tid; idx < D * D; idx += 256) {
-    const int i = idx / D, j = idx - (idx / D) * D;
-    A[idx] = He[idx] + (double)(c * (zt[i] * zt[j]));
+  for (int i = tid >> 5; i < D; i += 8) {
+    const float zi = zt[i];
+    for (int j = tid & 31; j < D; j += 32) A[(size_t)i * D + j] = He[(size_t)i * D + j] + (double)(c * (zi * zt[j]));
   }
   for (int i = tid; i < D; i += 256) bsh[i] = (double)zt[i];
   __syncthreads();
@@ -218,10 +218,11 @@ __global__ __launch_bounds__(256) void kp_criage_solve(int D, int dp, const int3
       prow[i] = A[(size_t)k * D + i];
     }
     __syncthreads();
-    const int m = D - k - 1;
-    for (int idx = tid; idx < m * m; idx += 256) {
-      const int i = k + 1 + idx / m, j = k + 1 + (idx - (idx / m) * m);
-      A[(size_t)i * D + j] -= lcol[i] * prow[j];
+    // trailing update: 8 row groups x 32 consecutive columns (coalesced rows, no index division)
+    for (int i = k + 1 + (tid >> 5); i < D; i += 8) {
+      const double li = lcol[i];
+      double* Ai = A + (size_t)i * D;
+      for (int j = k + 1 + (tid & 31); j < D; j += 32) Ai[j] -= li * prow[j];
     }
     for (int i = k + 1 + tid; i < D; i += 256) bsh[i] -= lcol[i] * bsh[k];
     __syncthreads();

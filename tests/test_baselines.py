@@ -143,3 +143,21 @@ def test_dp_engine_gpu_vs_reference_goldens():
 @pytest.mark.gpu
 def test_criage_engine_gpu_vs_reference_goldens():
     _check_criage("gpu")
+
+
+def test_multi_equals_batch_cpu():
+    g = _golden()
+    case = g["criage"][0]
+    rec, ds, model = build_product(case["case"], "cpu")
+    nec = kb.NecessaryCriageEngine(model, ds)
+    jobs = [(tuple(b["pred"]), [tuple(t) for t in b["triples"]]) for b in case["necessary"] if b["perspective"] == "tail"]
+    multi = nec.compute_relevance_multi(jobs, "tail")
+    for (p, ts), m in zip(jobs, multi):
+        assert m == nec.compute_relevance_batch(p, ts, "tail")
+    dcase = g["dp"][0]
+    rec, ds, model = build_product(dcase["case"], "cpu")
+    dp = kb.NecessaryDPEngine(model, ds, dcase["epsilon"])
+    jobs = [(tuple(b["pred"]), [tuple(t) for t in b["triples"]]) for b in dcase["necessary"] if b["perspective"] == "head"]
+    multi = dp.compute_relevance_multi(jobs, "head")
+    for (p, ts), m in zip(jobs, multi):
+        assert m == dp.compute_relevance_batch(p, "head", ts)
