@@ -60,95 +60,108 @@ __device__ __forceinline__ float wave_fold_u(float v) {  // v: 16-lane sums (row
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
-// one work item of kp_te_posttrain: a positive row and up to TE_NB of its negatives
-template <int VPL>
-struct TeItem {
-  int h, t, fz, nb;
-  int ent[TE_NB];
-  bool ch[TE_NB];
-  float4 av[VPL], bb[VPL], bn[TE_NB][VPL];
-};
+constexpr int TE_RCH = 512;  // work-item records built in LDS per chunk
 
-template <int VPL>
-__device__ __forceinline__ void te_fetch(TeItem<VPL>& I, int it, int cpb, int mb, int ratio, int st, int B,
-                                         const int32_t* order, const int32_t* ents, const int32_t* hot,
-                                         const int32_t* rw, const float* __restrict__ E,
-                                         const float* __restrict__ Rt, int dp, int K, int lane, int NF4) {
+// Work-item record (three int4 in LDS), built by all threads once per step so that the
+// per-item loop is loads + arithmetic only (wave-uniform fields read with broadcast LDS
+// reads and readfirstlane; no index arithmetic, divisions or 64-bit multiplies):
+//   r0 = {element offset of the positive's frozen side (0 if it is the kelpie id K),
+//         element offset of the relation row, flags, #K occurrences over the item's pairs}
+//   r1 = {element offsets of negatives 0..3}, r2 = {offset of negative 4, sign bits, -, -}
+// flags: bit 0 h == K, bit 1 t == K, bits 4-7 #negatives, bits 8+q corrupted head,
+// bits 16+q negative entity == K; sign bits: 2 bits per negative, sgn + 1 with
+// sgn = (hn == K) - (tn == K) (TransE)
+__device__ __forceinline__ void te_record(int4* rec, int it, int cpb, int mb, int ratio, int st, int B,
+                                          const int32_t* order, const int32_t* ents, const int32_t* hot,
+                                          const int32_t* rw, int dp, int K) {
   const int m = mb + it / cpb, c = it - (it / cpb) * cpb;
-  const int ri = __builtin_amdgcn_readfirstlane(order[m]);
-  I.h = __builtin_amdgcn_readfirstlane(rw[3 * ri]);
-  const int r = __builtin_amdgcn_readfirstlane(rw[3 * ri + 1]);
-  I.t = __builtin_amdgcn_readfirstlane(rw[3 * ri + 2]);
-  I.fz = (I.h == K) ? I.t : I.h;  // the positive's frozen side (K too for a self loop)
+  const int ri = order[m];
+  const int h = rw[3 * ri], r = rw[3 * ri + 1], t = rw[3 * ri + 2];
+  const int fz = (h == K) ? t : h;
   const int j0 = max(m * ratio, st) + c * TE_NB;
   const int jhi = min(m * ratio + ratio, st + B);
-  I.nb = max(0, min(TE_NB, jhi - j0));
+  const int nb = max(0, min(TE_NB, jhi - j0));
+  int flags = (h == K ? 1 : 0) | (t == K ? 2 : 0) | (nb << 4);
+  int sgn = 0, cnt = 0;
+  int off[TE_NB];
 #pragma unroll
   for (int q = 0; q < TE_NB; ++q) {
     const int jj = min(j0 + q, jhi - 1);
-    I.ent[q] = __builtin_amdgcn_readfirstlane(ents[jj]);
-    I.ch[q] = __builtin_amdgcn_readfirstlane(hot[jj]) == 1;
+    const int ent = ents[jj];
+    const bool ch = hot[jj] == 1;
+    off[q] = (ent == K ? 0 : ent) * dp;
+    const int hn = ch ? ent : h, tn = ch ? t : ent;
+    if (q < nb) {
+      flags |= (ch ? 1 << (8 + q) : 0) | (ent == K ? 1 << (16 + q) : 0);
+      sgn |= ((hn == K) - (tn == K) + 1) << (2 * q);
+      cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
+    } else {
+      sgn |= 1 << (2 * q);
+    }
   }
-  const float* A = E + (size_t)(I.fz == K ? 0 : I.fz) * dp;
-  const float* rel = Rt + (size_t)r * dp;
-#pragma unroll
-  for (int u = 0; u < VPL; ++u) {
-    const int f0 = lane + 64 * u;
-    const int f = f0 < NF4 ? f0 : NF4 - 1;
-    I.av[u] = ld4(A + 4 * f);
-    I.bb[u] = ld4(rel + 4 * f);
-#pragma unroll
-    for (int q = 0; q < TE_NB; ++q) I.bn[q][u] = ld4(E + (size_t)(I.ent[q] == K ? 0 : I.ent[q]) * dp + 4 * f);
-  }
+  rec[0] = make_int4((fz == K ? 0 : fz) * dp, r * dp, flags, cnt);
+  rec[1] = make_int4(off[0], off[1], off[2], off[3]);
+  rec[2] = make_int4(off[4], sgn, 0, 0);
 }
 
-// VALU-lean pair math (the kernel is VALU-bound per CU, tools/te_times.py): lhs + rel
-// of the positive is shared by every tail-corrupted negative, squared norms are FMA
-// chains, the item's TE_NB norm reductions run interleaved, negatives without the
-// kelpie entity (zero gradient, the hinge only) skip the gradient FMAs, and the
-// positive's gradient is applied once with the summed coefficient.
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// One item: the positive and its negatives.  x4[u] is this lane's float4 of the kelpie
+// row (constant within a step), fo[u] its element offset clamped into the row, on[u]
+// whether that float4 is inside the row (out-of-row lanes load duplicates and are
+// dropped from the norms; their gradient lanes are never stored).  The kernel is
+// bound by VALU issue (tools/te_times.py): the selects below are per-lane with
+// wave-uniform masks; forcing them into scalar branches was measured 1.9x slower.
 template <int VPL>
-__device__ __forceinline__ void te_compute(const TeItem<VPL>& I, const float* xs, int K, int lane, int NF4,
-                                           float margin, float4* g, int& cnt) {
-  const int h = I.h, t = I.t;
+__device__ __forceinline__ void te_item(const int4* rec, const float* __restrict__ E, const float* __restrict__ Rt,
+                                        const float4* x4, const int* fo, const bool* on, float margin, float4* g,
+                                        int& cnt) {
+  const int4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+  const int a_off = rfl(r0.x), rel_off = rfl(r0.y), flags = rfl(r0.z);
+  const int noff[TE_NB] = {rfl(r1.x), rfl(r1.y), rfl(r1.z), rfl(r1.w), rfl(r2.x)};
+  const int sgnb = rfl(r2.y);
+  const int nb = (flags >> 4) & 15;
+  const bool hk = flags & 1, tk = flags & 2;
+  float4 av[VPL], bb[VPL], bn[TE_NB][VPL];
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    av[u] = ld4(E + a_off + fo[u]);
+    bb[u] = ld4(Rt + rel_off + fo[u]);
+#pragma unroll
+    for (int q = 0; q < TE_NB; ++q) bn[q][u] = ld4(E + noff[q] + fo[u]);
+  }
   float4 rp[VPL], lb[VPL], vp[VPL];
   float sp = 0.f;
 #pragma unroll
   for (int u = 0; u < VPL; ++u) {
-    const int f0 = lane + 64 * u;
-    const bool on = f0 < NF4;
-    const float4 xk = ld4(xs + 4 * (on ? f0 : NF4 - 1));
-    const float4 av = sel4(I.fz == K, xk, I.av[u]);
-    const float4 lp = sel4(h == K, xk, av);
-    rp[u] = sel4(t == K, xk, av);
-    const float4 b = I.bb[u];
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    // every kelpie row holds K on one side (both for a self loop)
+    const float4 lp = hk ? x4[u] : av[u];
+    rp[u] = tk ? x4[u] : av[u];
+    const float4 b = bb[u];
     lb[u] = make_float4(lp.x + b.x, lp.y + b.y, lp.z + b.z, lp.w + b.w);
-    // positive: v+ = (lhs + rel) - rhs, zero past the row end
-    vp[u] = sel4(on, make_float4(lb[u].x - rp[u].x, lb[u].y - rp[u].y, lb[u].z - rp[u].z, lb[u].w - rp[u].w), z);
-    sp = fmaf(vp[u].x, vp[u].x, fmaf(vp[u].y, vp[u].y, fmaf(vp[u].z, vp[u].z, fmaf(vp[u].w, vp[u].w, sp))));
+    vp[u] = make_float4(lb[u].x - rp[u].x, lb[u].y - rp[u].y, lb[u].z - rp[u].z, lb[u].w - rp[u].w);
+    const float s = fmaf(vp[u].x, vp[u].x, fmaf(vp[u].y, vp[u].y, fmaf(vp[u].z, vp[u].z, vp[u].w * vp[u].w)));
+    sp += on[u] ? s : 0.f;
   }
   float4 vn[TE_NB][VPL];
   float sn[TE_NB];
 #pragma unroll
   for (int q = 0; q < TE_NB; ++q) {
-    const bool ch = I.ch[q];
     sn[q] = 0.f;
+    const bool ch = flags & (1 << (8 + q));
+    const bool ek = flags & (1 << (16 + q));
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
-      const int f0 = lane + 64 * u;
-      const bool on = f0 < NF4;
-      const float4 bq = sel4(I.ent[q] == K, ld4(xs + 4 * (on ? f0 : NF4 - 1)), I.bn[q][u]);
-      const float4 b = I.bb[u];
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      // corrupted head: (e_n + rel) - rhs; corrupted tail: (lhs + rel) - e_n
-      const float4 vh = make_float4((bq.x + b.x) - rp[u].x, (bq.y + b.y) - rp[u].y, (bq.z + b.z) - rp[u].z,
-                                    (bq.w + b.w) - rp[u].w);
-      const float4 vt = make_float4(lb[u].x - bq.x, lb[u].y - bq.y, lb[u].z - bq.z, lb[u].w - bq.w);
-      const float4 v = sel4(ch, vh, vt);
-      vn[q][u] = sel4(on, v, z);
-      sn[q] = fmaf(vn[q][u].x, vn[q][u].x,
-                   fmaf(vn[q][u].y, vn[q][u].y, fmaf(vn[q][u].z, vn[q][u].z, fmaf(vn[q][u].w, vn[q][u].w, sn[q]))));
+      const float4 bq = ek ? x4[u] : bn[q][u];
+      const float4 b = bb[u];
+      float4 v;
+      if (ch)  // corrupted head: (e_n + rel) - rhs
+        v = make_float4((bq.x + b.x) - rp[u].x, (bq.y + b.y) - rp[u].y, (bq.z + b.z) - rp[u].z, (bq.w + b.w) - rp[u].w);
+      else  // corrupted tail: (lhs + rel) - e_n
+        v = make_float4(lb[u].x - bq.x, lb[u].y - bq.y, lb[u].z - bq.z, lb[u].w - bq.w);
+      vn[q][u] = v;
+      const float s = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+      sn[q] += on[u] ? s : 0.f;
     }
   }
   // TE_NB + 1 independent wave reductions, interleaved
@@ -156,20 +169,16 @@ __device__ __forceinline__ void te_compute(const TeItem<VPL>& I, const float* xs
 #pragma unroll
   for (int q = 0; q < TE_NB; ++q) sn[q] = row16_sum(sn[q]);
   const float fp = sqrtf(wave_fold_u(sp));
-  const float sgn_p = (float)((h == K) - (t == K));
-  float cps = 0.f;
+  int n_act = 0;
 #pragma unroll
   for (int q = 0; q < TE_NB; ++q) {
     const float fn = sqrtf(wave_fold_u(sn[q]));
-    if (q >= I.nb) continue;
-    const bool ch = I.ch[q];
-    const int ent = I.ent[q];
-    const int hn = ch ? ent : h, tn = ch ? t : ent;
+    if (q >= nb) continue;
     const bool act = (fp - fn) + margin >= 0.f;  // clamp_min backward passes grad where self >= min
-    const float sgn_n = (float)((hn == K) - (tn == K));
-    cps += (act && fp > 0.f) ? sgn_p / fp : 0.f;
-    const float cn = (act && fn > 0.f) ? -sgn_n / fn : 0.f;
-    if (cn != 0.f) {
+    n_act += act ? 1 : 0;
+    const int sgn_n = ((sgnb >> (2 * q)) & 3) - 1;
+    if (act && sgn_n != 0 && fn > 0.f) {  // negatives without the kelpie entity: hinge only
+      const float cn = -(float)sgn_n / fn;
 #pragma unroll
       for (int u = 0; u < VPL; ++u) {
         g[u].x = fmaf(cn, vn[q][u].x, g[u].x);
@@ -178,9 +187,10 @@ __device__ __forceinline__ void te_compute(const TeItem<VPL>& I, const float* xs
         g[u].w = fmaf(cn, vn[q][u].w, g[u].w);
       }
     }
-    cnt += (h == K) + (t == K) + (hn == K) + (tn == K);
   }
-  if (cps != 0.f) {
+  const int sgn_p = (hk ? 1 : 0) - (tk ? 1 : 0);
+  if (n_act > 0 && sgn_p != 0 && fp > 0.f) {
+    const float cps = (float)n_act * ((float)sgn_p / fp);
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
       g[u].x = fmaf(cps, vp[u].x, g[u].x);
@@ -189,6 +199,7 @@ __device__ __forceinline__ void te_compute(const TeItem<VPL>& I, const float* xs
       g[u].w = fmaf(cps, vp[u].w, g[u].w);
     }
   }
+  cnt += rfl(r0.w);
 }
 
 // One workgroup per slot (slots issued longest first) runs every epoch on chip: x in
@@ -227,6 +238,7 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
   float* red = sm + dp;  // [TE_NW][dp] per-wave gradient partials
   int* rws = reinterpret_cast<int*>(red + TE_NW * dp);  // STAGED: [3 R] the slot's rows
   int* drw = rws + 3 * (STAGED ? slots[slot_of_block[blockIdx.x]].R : 0);  // STAGED: [2][3 R] draws
+  __shared__ int4 recs[3 * TE_RCH];  // work-item records of the current chunk
   __shared__ int cnt_s[TE_NW];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -256,6 +268,14 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
   const int32_t* rw = STAGED ? rws : rwg;
   const int NF4 = dp / 4;
   const int ratio = hp.ratio;
+  int fo[VPL];
+  bool on[VPL];
+#pragma unroll
+  for (int u = 0; u < VPL; ++u) {
+    const int f = lane + 64 * u;
+    on[u] = f < NF4;
+    fo[u] = 4 * (f < NF4 ? f : NF4 - 1);
+  }
   double b1t = 1.0, b2t = 1.0;
   for (int e = 0; e < hp.epochs; ++e) {
     const int32_t* order = STAGED ? drw + (e & 1) * R3 : rngs + (long long)e * R3;
@@ -276,30 +296,32 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
       for (int u = 0; u < VPL; ++u) g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       int cnt = 0;
       // work items: (bundle m, chunk of <= TE_NB of its negatives) over the bundles that
-      // overlap the step's positions [st, st + B), strided over the waves
+      // overlap the step's positions [st, st + B); records built per chunk of TE_RCH items
       const int cpb = (ratio + TE_NB - 1) / TE_NB;
       const int mb = st / ratio;
       const int n_items = ((st + B - 1) / ratio - mb + 1) * cpb;
 #ifdef KP_TE_STAMPS
       const long long c_step = __builtin_amdgcn_s_memtime();
 #endif
-      for (int it = wave; it < n_items; it += TE_NW) {
-        TeItem<VPL> I;
+      float4 x4[VPL];
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) x4[u] = ld4(xs + fo[u]);
+      for (int c0 = 0; c0 < n_items; c0 += TE_RCH) {
+        const int nc = min(TE_RCH, n_items - c0);
+        if (c0 > 0) __syncthreads();  // the previous chunk's records are consumed
+        for (int k = tid; k < nc; k += NT)
+          te_record(recs + 3 * k, c0 + k, cpb, mb, ratio, st, B, order, ents, hot, rw, dp, K);
+        __syncthreads();
+        for (int k = wave; k < nc; k += TE_NW) {
 #ifdef KP_TE_STAMPS
-        const long long c0 = __builtin_amdgcn_s_memtime();
+          const long long c1 = __builtin_amdgcn_s_memtime();
 #endif
-        te_fetch<VPL>(I, it, cpb, mb, ratio, st, B, order, ents, hot, rw, E, Rt, dp, K, lane, NF4);
+          te_item<VPL>(recs + 3 * k, E, Rt, x4, fo, on, hp.margin, g, cnt);
 #ifdef KP_TE_STAMPS
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        const long long c1 = __builtin_amdgcn_s_memtime();
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          st_comp += __builtin_amdgcn_s_memtime() - c1;
 #endif
-        te_compute<VPL>(I, xs, K, lane, NF4, hp.margin, g, cnt);
-#ifdef KP_TE_STAMPS
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        const long long c2 = __builtin_amdgcn_s_memtime();
-        st_fetch += c1 - c0;
-        st_comp += c2 - c1;
-#endif
+        }
       }
 #ifdef KP_TE_STAMPS
       const long long c3 = __builtin_amdgcn_s_memtime();
