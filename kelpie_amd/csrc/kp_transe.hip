@@ -54,6 +54,16 @@ constexpr int TE_NB = 5;  // negatives per bundle held in registers (the referen
 
 // sum over the 64 lanes of 16-lane sums (row16_sum), returned wave-uniform: row_bcast15 /
 // row_bcast31 fold the four rows into lane 63
+// 16-lane row sums as DPP adds: bound_ctrl set (every source lane of these patterns is
+// inside its row, so it changes nothing) lets the compiler fuse each move into the add
+__device__ __forceinline__ float row16_sum_f(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
+  return v;
+}
+
 __device__ __forceinline__ float wave_fold_u(float v) {  // v: 16-lane sums (row16_sum)
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false));
@@ -165,9 +175,9 @@ __device__ __forceinline__ void te_item(const int4* rec, const float* __restrict
     }
   }
   // TE_NB + 1 independent wave reductions, interleaved
-  sp = row16_sum(sp);
+  sp = row16_sum_f(sp);
 #pragma unroll
-  for (int q = 0; q < TE_NB; ++q) sn[q] = row16_sum(sn[q]);
+  for (int q = 0; q < TE_NB; ++q) sn[q] = row16_sum_f(sn[q]);
   const float fp = sqrtf(wave_fold_u(sp));
   int n_act = 0;
 #pragma unroll
