@@ -242,10 +242,10 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
                                                     const float* __restrict__ bnb, float* __restrict__ X,
                                                     float* __restrict__ S1, float* __restrict__ S2, CvOpt opt) {
   __shared__ float xs[640];
-  __shared__ float xf[640];
-  __shared__ float red[4];
+  __shared__ float gw_s[4][640];  // per-wave partial gradients of the frozen-head pairs
   const CvAct A = act[blockIdx.x];
   const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
   float* x = X + (size_t)A.slot * k.dp;
   for (int d = tid; d < k.dp; d += 256) xs[d] = x[d];
   __syncthreads();
@@ -258,30 +258,44 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
       if (d < k.dim) g[u] += G * Q[(size_t)ii * k.dp + d] + dl[(size_t)ii * k.dp + d];
     }
   }
+  // frozen-head pairs (o, r_inv, kelpie): the kelpie column's BCE gradient G * x_fc,
+  // one pair per wave at a time (wave reductions, no workgroup barrier per pair)
   const float* a3 = bna + 33;
   const float* b3 = bnb + 33;
-  for (int j = 0; j < A.f_count; ++j) {
+  float gw[10];
+#pragma unroll
+  for (int u = 0; u < 10; ++u) gw[u] = 0.f;
+  for (int j = wave; j < A.f_count; j += 4) {
     const CvFInst F = fi[A.f_begin + j];
+    float v[10];
     float part = 0.f;
-    for (int u = 0; u < 3; ++u) {
-      const int d = tid + 256 * u;
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int d = lane + 64 * u;
+      v[u] = 0.f;
       if (d < k.dim) {
         const float fc = fcf[(size_t)F.fp * k.dim + d];
         const float nz = k.has_mask ? noise_at(bits, F.mask_off, F.pos * k.dim + d, k.scale) : 1.0f;
         const float dr = k.has_mask ? fc * nz : fc;
-        const float v = fmaxf(dr * a3[d] + b3[d], 0.f);
-        xf[d] = v;
-        part += v * xs[d];
+        v[u] = fmaxf(dr * a3[d] + b3[d], 0.f);
+        part += v[u] * xs[d];
       }
     }
-    const float s = block_sum(part, red);
+    const float s = wave_sum(part);
     const float gs = 1.0f / (float)((long long)F.b * (long long)(k.n_ent + 1));
     const float G = bce_g(s, k.yhi, gs);
-    for (int u = 0; u < 3; ++u) {
-      const int d = tid + 256 * u;
-      if (d < k.dim) g[u] += G * xf[d];
-    }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 10; ++u) gw[u] += G * v[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 10; ++u) {
+    const int d = lane + 64 * u;
+    if (d < k.dim) gw_s[wave][d] = gw[u];
+  }
+  __syncthreads();
+  for (int u = 0; u < 3; ++u) {
+    const int d = tid + 256 * u;
+    if (d < k.dim) g[u] += (gw_s[0][d] + gw_s[1][d]) + (gw_s[2][d] + gw_s[3][d]);
   }
   for (int u = 0; u < 3; ++u) {
     const int d = tid + 256 * u;

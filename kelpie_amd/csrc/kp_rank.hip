@@ -50,13 +50,17 @@ __global__ __launch_bounds__(256) void kp_gemm_abt(const float* __restrict__ A, 
       *reinterpret_cast<float4*>(&Es[row * SG_LD + c4]) = ve;
     }
     __syncthreads();
+    // k permuted within each 16-deep chunk: MFMA i of a chunk pairs lane group g with
+    // k = kk + 4g + i on both operands, so a lane's A and B values for four MFMAs are
+    // one 16-byte LDS read each (the sum over k is unchanged, only its order)
 #pragma unroll
-    for (int kk = 0; kk < SG_BK; kk += 4) {
-      float a = Qs[(16 * w + c) * SG_LD + kk + g];
+    for (int kk = 0; kk < SG_BK; kk += 16) {
+      const f32x4 a4 = *reinterpret_cast<const f32x4*>(&Qs[(16 * w + c) * SG_LD + kk + 4 * g]);
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        float b = Es[(16 * n + c) * SG_LD + kk + g];
-        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[n], 0, 0, 0);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(&Es[(16 * n + c) * SG_LD + kk + 4 * g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i], b4[i], acc[n], 0, 0, 0);
       }
     }
     __syncthreads();
