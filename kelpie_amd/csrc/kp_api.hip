@@ -1,6 +1,7 @@
 // kp_api.hip -- C ABI entry points of libkelpie_hip.so (include/kelpie_hip.h).
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 
 #include "kp_common.hpp"
 
@@ -70,6 +71,7 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     } else {
       c->dp = round_up(m->dim, 16);
     }
+    if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "bf16x3") == 0 ? 1 : 0;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     KP_HIP(hipEventCreate(&c->ev0));
     KP_HIP(hipEventCreate(&c->ev1));
@@ -103,6 +105,7 @@ int kp_ctx_destroy(kp_ctx* c) {
   for (float* p : {c->dE, c->dR, c->dEt, c->d_conv_w, c->d_conv_b, c->d_fc_w, c->d_fc_b, c->d_bn_a, c->d_bn_b})
     if (p) (void)hipFree(p);
   for (auto& b : c->ws) b.release();
+  c->e3.release();
   for (auto e : c->evpool) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

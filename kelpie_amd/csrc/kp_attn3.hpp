@@ -1,0 +1,441 @@
+// kp_attn3.hpp -- kp_attn on bf16 MFMA with three-piece operands ("bf16x3").
+//
+// Same contract as kpattn::kp_attn (kp_attn.hpp): per query q over the frozen keys
+// [key_begin, key_end) of its stream-K segment, the softmax statistics (m, l) and
+// O = sum_e w(s_e) E_e with s_e = q . E_e, w = exp(s - m_ref) (ComplEx) or the
+// BCE-through-sigmoid gradient (ConvE).  The contractions run on
+// v_mfma_f32_16x16x32_bf16 (16x the per-clock rate of the f32-input MFMA on gfx950)
+// with every fp32 operand x split exactly into three bf16 pieces
+//   x = x0 + x1 + x2,  x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)
+// (8 significant bits each: together the 24 of fp32).  A product a.b is taken as
+//   a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0      (six MFMAs)
+// whose bf16 x bf16 products are exact in the fp32 accumulator; the dropped terms
+// (a1 b2, a2 b1, a2 b2) are below 2^-25 of |a||b|, under fp32's own rounding of the
+// sum, so the scores and O agree with the fp32 path to fp32 rounding (not bitwise:
+// the accumulation order differs).  6 MFMAs of 16 cycles per 16x16x32 block against
+// 8 f32 MFMAs of 32 cycles: 2.67x fewer MFMA cycles.
+//
+// Table image (built once per context, kp_split3_table): entity e is one ROW_B-byte
+// row [piece 0: DP bf16 | piece 1 | piece 2 | 16 B pad], rows padded with zero rows to
+// a multiple of 32, so a 32-entity key tile is TILE_B contiguous bytes and the LDS
+// tile is the same bytes (one linear LDS-DMA copy).  ROW_B / 16 is odd, so the
+// 16-lane groups of the S-phase ds_read_b128 (16 entity rows, same columns) are
+// conflict-free.
+//
+// S phase (swapped, as kp_attn): S^T = E . Q^T, A = the entity rows (ds_read_b128 of
+// 8 dims per lane), B = the query pieces held in VGPRs.  C row = entity 4g + r of a
+// 16-entity sub-tile, C column = query c.
+// O phase: O^T += E^T . P with the 32 entities of the tile as K.  k-slot j of lane
+// group g is entity 4g + j (j < 4, sub-tile 0) or 16 + 4g + j - 4 (sub-tile 1): that
+// is where the S^T accumulators already put P, so P's pieces are the B operand as
+// they sit; A = E^T by two ds_read_b64_tr_b16 per piece (rows 4g.. and 16 + 4g..).
+#pragma once
+#include "kp_attn.hpp"
+
+namespace kpattn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// bytes of one entity row of the split image and of a 32-entity tile
+__host__ __device__ constexpr int split3_row_bytes(int DP) { return 3 * 2 * DP + 16; }
+__host__ __device__ constexpr int split3_tile_bytes(int DP) { return 32 * split3_row_bytes(DP); }
+// LDS-DMA pieces (1 KiB) per tile and the LDS bytes of kp_attn3 (two tile buffers)
+__host__ __device__ constexpr int split3_pieces(int DP) { return (split3_tile_bytes(DP) + 1023) / 1024; }
+constexpr size_t attn3_lds_bytes(int DB) { return 2u * 1024u * (size_t)split3_pieces(16 * DB); }
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = __fsub_rn(x, (float)h);
+  m = (__bf16)r1;
+  const float r2 = __fsub_rn(r1, (float)m);
+  l = (__bf16)r2;
+}
+
+__device__ __forceinline__ bf16x8 lds_rd_bf8(uint32_t addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ bf16x4 lds_rd_bf4(uint32_t addr) {
+  bf16x4 v;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ bf16x4 lds_rd_tr(uint32_t addr) {
+  bf16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ bf16x8 tied(bf16x8 v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ bf16x4 tied(bf16x4 v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// six-product a.b on one accumulator (smallest terms first)
+__device__ __forceinline__ f32x4 mfma3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+  return c;
+}
+__device__ __forceinline__ f32x4 mfma3_k16(const bf16x4 (&a)[3], const bf16x4 (&b)[3], f32x4 c) {
+#define KP_M16(x, y) \
+  c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, x), __builtin_bit_cast(s16x4, y), c, 0, 0, 0)
+  KP_M16(a[2], b[0]);
+  KP_M16(a[1], b[1]);
+  KP_M16(a[0], b[2]);
+  KP_M16(a[1], b[0]);
+  KP_M16(a[0], b[1]);
+  KP_M16(a[0], b[0]);
+#undef KP_M16
+  return c;
+}
+
+// Split image of the fp32 table E [n_ent][DP]: one thread per (entity, 2 dims).
+// The destination is zeroed by the caller (padding rows and bytes).
+template <int DP>
+__global__ void kp_split3_table(const float* __restrict__ E, int n_ent, uint8_t* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)n_ent * (DP / 2)) return;
+  const int e = (int)(i / (DP / 2)), d = 2 * (int)(i % (DP / 2));
+  __bf16 h[2], m[2], l[2];
+  split3(E[(size_t)e * DP + d], h[0], m[0], l[0]);
+  split3(E[(size_t)e * DP + d + 1], h[1], m[1], l[1]);
+  __bf16* row = reinterpret_cast<__bf16*>(out + (size_t)e * split3_row_bytes(DP));
+  row[d] = h[0];
+  row[d + 1] = h[1];
+  row[DP + d] = m[0];
+  row[DP + d + 1] = m[1];
+  row[2 * DP + d] = l[0];
+  row[2 * DP + d + 1] = l[1];
+}
+
+template <int DB, int MODE>
+__global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E3, int n_ent,
+                                                   const float* __restrict__ Qpre, int nq, AttnWork wk,
+                                                   float* __restrict__ out_m, float* __restrict__ out_l,
+                                                   float* __restrict__ out_O, const float* __restrict__ qscale,
+                                                   float ylo) {
+  constexpr bool WITH_O = MODE != ATT_SOFTMAX;
+  constexpr int DP = 16 * DB;
+  constexpr int NK = DP / 32;         // full 32-deep k-steps of the S phase
+  constexpr int TAIL = (DP % 32) / 16;  // one 16-deep k-step (16x16x16 MFMA) when DP % 32 == 16
+  constexpr int KT = 32;
+  constexpr int PART_B = 2 * DP;
+  constexpr int ROW_B = split3_row_bytes(DP);
+  constexpr int PIECES = split3_pieces(DP);
+  constexpr int BUF_B = 1024 * PIECES;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds3[];  // [2][BUF_B]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  int key_begin = 0, key_end = 0;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds3;
+
+  // linear LDS-DMA of a tile: piece p = bytes [1024 p, 1024 p + 1024) of the tile,
+  // wave w issues p = w, w + 4, ... (the image has >= 1 KiB of slack past its end)
+  auto issue = [&](int tile, int buf) {
+    const uint8_t* src = E3 + (size_t)(key_begin + tile * KT) * ROW_B + 16 * lane;
+#pragma unroll
+    for (int p0 = 0; p0 < PIECES; p0 += 4) {
+      const int p = p0 + w;
+      if (p < PIECES)
+        glds16(reinterpret_cast<const float*>(src + 1024 * p),
+               __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)));
+    }
+  };
+  const int QT = (nq + 63) / 64;
+  const long long total = (long long)QT * wk.ktq;
+  long long it = (long long)blockIdx.x * wk.per_wg;
+  const long long it_end = min(total, it + (long long)wk.per_wg);
+  while (it < it_end) {
+    const int qt = (int)(it / wk.ktq);
+    const int kt0 = (int)(it - (long long)qt * wk.ktq);
+    const int kt1 = (int)min((long long)wk.ktq, (long long)kt0 + (it_end - it));
+    const int part = (int)blockIdx.x - (int)(((long long)qt * wk.ktq) / wk.per_wg);
+    key_begin = kt0 * KT;
+    key_end = min(n_ent, kt1 * KT);
+    const int ntiles = kt1 - kt0;
+    const int q = qt * 64 + 16 * w + c;
+    const bool valid = q < nq;
+    // ---- query pieces -> VGPRs: B operand of k-step s is q[32 s + 8 g + j]
+    bf16x8 qb[NK > 0 ? NK : 1][3];
+    bf16x4 qt4[3];
+    float gsc = 0.f;
+    if (MODE == ATT_BCE_O) gsc = valid ? qscale[q] : 0.f;
+    {
+      const float* qp = Qpre + (size_t)(valid ? q : 0) * DP;
+#pragma unroll
+      for (int s = 0; s < NK; ++s) {
+        const float4 v0 = *reinterpret_cast<const float4*>(qp + 32 * s + 8 * g);
+        const float4 v1 = *reinterpret_cast<const float4*>(qp + 32 * s + 8 * g + 4);
+        const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 h, m, l;
+          split3(valid ? f[j] : 0.f, h, m, l);
+          qb[s][0][j] = h;
+          qb[s][1][j] = m;
+          qb[s][2][j] = l;
+        }
+      }
+      if (TAIL) {
+        const float4 v0 = *reinterpret_cast<const float4*>(qp + 32 * NK + 4 * g);
+        const float f[4] = {v0.x, v0.y, v0.z, v0.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 h, m, l;
+          split3(valid ? f[j] : 0.f, h, m, l);
+          qt4[0][j] = h;
+          qt4[1][j] = m;
+          qt4[2][j] = l;
+        }
+      }
+    }
+    f32x4 O[WITH_O ? DB : 1];
+    float m_ref = kNegInf, l_run = 0.f;
+
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < (WITH_O ? DB : 1); ++j) O[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      l_run = 0.f;
+      float m_seen = kNegInf;
+      if (ntiles > 0) issue(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+
+      for (int t = 0; t < ntiles; ++t) {
+        const int k0 = key_begin + t * KT;
+        const uint32_t tb = lds0 + (uint32_t)((t & 1) * BUF_B);
+        // ---- S^T per 16-entity sub-tile u (entity row 16u + c of the tile)
+        // Both sub-tiles per k-step; each step's six operand reads are issued one step
+        // ahead of its MFMAs (LDS returns in order: a counted lgkmcnt wait).
+        f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+        const uint32_t rb = tb + (uint32_t)(c * ROW_B + 16 * g);
+        constexpr uint32_t SUB_B = 16u * ROW_B;  // the second sub-tile's rows
+        bf16x8 ra[2][2][3];
+        bf16x4 rt[2][3];
+        auto load_full = [&](int s, int b) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) ra[b][u][p] = lds_rd_bf8(rb + u * SUB_B + (uint32_t)(p * PART_B + 64 * s));
+        };
+        auto load_tail = [&]() {
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+              rt[u][p] = lds_rd_bf4(rb - 8u * g + u * SUB_B + (uint32_t)(p * PART_B + 64 * NK));  // dims 32 NK + 4g ..
+        };
+        if (NK > 0)
+          load_full(0, 0);
+        else
+          load_tail();
+#pragma unroll
+        for (int s = 0; s < NK; ++s) {
+          if (s + 1 < NK) {
+            load_full(s + 1, (s + 1) & 1);
+            lgkm_wait<6>();
+          } else if (TAIL) {
+            load_tail();
+            lgkm_wait<6>();
+          } else {
+            lgkm_wait<0>();
+          }
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            bf16x8 a[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) a[p] = tied(ra[s & 1][u][p]);
+            sc[u] = mfma3(a, qb[s], sc[u]);
+          }
+        }
+        if (TAIL) {
+          lgkm_wait<0>();
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            bf16x4 a[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) a[p] = tied(rt[u][p]);
+            sc[u] = mfma3_k16(a, qt4, sc[u]);
+          }
+        }
+#ifndef KP_ATTN_NODMA
+        if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
+#endif
+        // O-phase operands: block m's six transposed reads (rows 4g.. and 16 + 4g.. of
+        // each piece); lane c = 4 qq + pp reads row qq of the 4-row block, columns
+        // 4 pp .. 4 pp + 3.  Block 0's are issued before the softmax, block m + 1's
+        // before block m's MFMAs.
+        const uint32_t ob = tb + (uint32_t)((4 * g + (c >> 2)) * ROW_B + 8 * (c & 3));
+        bf16x4 ol[2][3], oh[2][3];
+        auto load_o = [&](int m, int b) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            ol[b][p] = lds_rd_tr(ob + (uint32_t)(p * PART_B + 32 * m));
+            oh[b][p] = lds_rd_tr(ob + (uint32_t)(16 * ROW_B + p * PART_B + 32 * m));
+          }
+        };
+        if (WITH_O) load_o(0, 0);
+        float pw[2][4];
+        if (MODE == ATT_BCE_O) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float x0 = __builtin_amdgcn_rcpf(1.0f + __expf(-sc[u][r]));
+              const float w0 = (1.0f - x0) * x0;
+              pw[u][r] = (k0 + 16 * u + 4 * g + r < key_end)
+                             ? (((x0 - ylo) * __builtin_amdgcn_rcpf(fmaxf(w0, 1e-12f))) * gsc) * w0
+                             : 0.f;
+            }
+        } else {
+          float v[2][4];
+          float tmax = kNegInf;
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[u][r] = (k0 + 16 * u + 4 * g + r < key_end) ? sc[u][r] : kNegInf;
+              tmax = fmaxf(tmax, v[u][r]);
+            }
+          m_seen = fmaxf(m_seen, tmax);
+          if (pass == 0 && t == 0) {
+            float mq = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+            m_ref = fmaxf(mq, __shfl_xor(mq, 32, 64));
+          }
+          float lt = 0.f;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pw[u][r] = __expf(v[u][r] - m_ref);
+            lt += (pw[u][0] + pw[u][1]) + (pw[u][2] + pw[u][3]);
+          }
+          l_run += lt;
+        }
+        if (WITH_O) {
+          // P pieces in the B layout: element j of lane group g = entity 4g + j (j < 4)
+          // or 16 + 4g + j - 4
+          bf16x8 pb[3];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            __bf16 h, m, l;
+            split3(pw[j >> 2][j & 3], h, m, l);
+            pb[0][j] = h;
+            pb[1][j] = m;
+            pb[2][j] = l;
+          }
+#pragma unroll
+          for (int m = 0; m < DB; ++m) {
+            if (m + 1 < DB) {
+              load_o(m + 1, (m + 1) & 1);
+              lgkm_wait<6>();
+            } else {
+              lgkm_wait<0>();
+            }
+            bf16x8 a[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              const bf16x4 x = tied(ol[m & 1][p]), y = tied(oh[m & 1][p]);
+              a[p] = (bf16x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+            }
+            O[m] = mfma3(a, pb, O[m]);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      if (MODE == ATT_BCE_O) break;
+      float mq = fmaxf(m_seen, __shfl_xor(m_seen, 16, 64));
+      mq = fmaxf(mq, __shfl_xor(mq, 32, 64));
+      if (pass == 1 || !__syncthreads_or(mq > m_ref + kMargin)) break;
+      m_ref = mq;
+    }
+
+    float l_tot = l_run + __shfl_xor(l_run, 16, 64);
+    l_tot += __shfl_xor(l_tot, 32, 64);
+    if (valid) {
+      const size_t o = (size_t)part * nq + q;
+      if (g == 0 && MODE != ATT_BCE_O) {
+        out_m[o] = m_ref;
+        out_l[o] = l_tot;
+      }
+      if (WITH_O) {
+        // O^T block m: lane (g, c) holds dims 16 m + 4 g + r of query c
+        float* dst = out_O + o * DP;
+#pragma unroll
+        for (int m = 0; m < DB; ++m)
+          *reinterpret_cast<float4*>(dst + 16 * m + 4 * g) = make_float4(O[m][0], O[m][1], O[m][2], O[m][3]);
+      }
+    }
+    if (kt1 == wk.ktq && valid) {
+      for (int pp = part + 1; pp < wk.n_parts; ++pp) {
+        const size_t o = (size_t)pp * nq + q;
+        if (g == 0 && MODE != ATT_BCE_O) {
+          out_m[o] = kNegInf;
+          out_l[o] = 0.f;
+        }
+        if (WITH_O) {
+          float* dst = out_O + o * DP;
+          for (int d = 4 * g; d < DP; d += 16) *reinterpret_cast<float4*>(dst + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+    it += kt1 - kt0;
+  }
+}
+
+// Host: the split image of c->dE (row stride DP = c->dp), built once per context.
+template <int DB>
+const uint8_t* split3_image(kp_ctx* c) {
+  constexpr int DP = 16 * DB;
+  KP_REQUIRE(c->dp == DP, "attn3: table stride mismatch");
+  if (!c->e3_ready) {
+    const size_t n_pad = (size_t)(c->n_ent + 31) / 32 * 32;
+    const size_t bytes = n_pad * split3_row_bytes(DP) + 1024;  // slack for the last tile's whole DMA pieces
+    uint8_t* d = reinterpret_cast<uint8_t*>(c->e3.ensure(bytes));
+    KP_HIP(hipMemsetAsync(d, 0, bytes, c->stream));
+    const long long n = (long long)c->n_ent * (DP / 2);
+    hipLaunchKernelGGL((kp_split3_table<DP>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->dE,
+                       c->n_ent, d);
+    KP_HIP(hipGetLastError());
+    c->e3_ready = true;
+  }
+  return c->e3.as<uint8_t>();
+}
+
+// Host: co-resident kp_attn3 workgroups per CU (registers and LDS), cached per context.
+template <int DB>
+int attn3_wpc(kp_ctx* c) {
+  if (c->attn3_wpc <= 0) {
+    int n = 0;
+    KP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kp_attn3<DB, ATT_SOFTMAX_O>, 256, attn3_lds_bytes(DB)));
+    int n2 = 0;
+    KP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n2, kp_attn3<DB, ATT_BCE_O>, 256, attn3_lds_bytes(DB)));
+    c->attn3_wpc = std::max(1, std::min(n, n2));
+  }
+  return c->attn3_wpc;
+}
+
+template <int DB, int MODE>
+void launch_attn3(kp_ctx* c, int n_ent, const float* Q, int nq, const AttnPlan& plan, float* m, float* l, float* O,
+                  const float* qscale, float ylo) {
+  const uint8_t* E3 = split3_image<DB>(c);
+  hipLaunchKernelGGL((kp_attn3<DB, MODE>), dim3(plan.n_wg), dim3(256), attn3_lds_bytes(DB), c->stream, E3, n_ent, Q,
+                     nq, plan.wk, m, l, O, qscale, ylo);
+  KP_HIP(hipGetLastError());
+}
+
+}  // namespace kpattn

@@ -90,6 +90,11 @@ struct kp_ctx {
   std::string err;
   Timing timing;
   bool time_hot = true;
+  // attention contraction: 0 = fp32 MFMA (kp_attn.hpp), 1 = bf16x3 MFMA (kp_attn3.hpp)
+  int attn_mode = 0;
+  DevBuf e3;               // kp_attn3's split image of dE, built on first use
+  bool e3_ready = false;
+  int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<double, double>> hot_pairs;  // (work units, seconds) per hot launch
   hipEvent_t event(size_t i) {

@@ -28,6 +28,7 @@
 #include <unordered_map>
 
 #include "kp_attn.hpp"
+#include "kp_attn3.hpp"
 
 namespace {
 using namespace kpattn;
@@ -282,12 +283,24 @@ void launch_stepq(kp_ctx* c, const int4* stepq, const float* X, int nq, float* Q
 
 // co-resident attention workgroups: LDS and registers allow two per CU for rows up
 // to 208 floats, one for wider rows
-inline int attn_slots(const kp_ctx* c, int DB) { return c->n_cu * (DB <= 13 ? 2 : 1); }
+// (kp_attn3: as many as the occupancy API reports)
+template <int DB>
+int attn_slots_db(kp_ctx* c) {
+  if (c->attn_mode == 1) return c->n_cu * attn3_wpc<DB>(c);
+  return c->n_cu * (DB <= 13 ? 2 : 1);
+}
 
 template <int DB>
 void launch_attn(kp_ctx* c, bool with_o, const float* Q, int nq, const AttnPlan& plan, float* m, float* l,
                  float* O) {
   if (nq <= 0) return;
+  if (c->attn_mode == 1) {
+    if (with_o)
+      launch_attn3<DB, ATT_SOFTMAX_O>(c, c->n_ent, Q, nq, plan, m, l, O, nullptr, 0.f);
+    else
+      launch_attn3<DB, ATT_SOFTMAX>(c, c->n_ent, Q, nq, plan, m, l, O, nullptr, 0.f);
+    return;
+  }
   const size_t shm = attn_lds_bytes(DB);
   if (with_o)
     hipLaunchKernelGGL((kp_attn<DB, ATT_SOFTMAX_O>), dim3(plan.n_wg), dim3(256), shm, c->stream, c->dE, c->n_ent, Q,
@@ -528,13 +541,15 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     KP_HIP(hipGetLastError());
   }
   // frozen-head pairs: q and frozen log-sum-exp
-  const AttnPlan plan_pairs = attn_plan(std::max(npairs, 1), c->n_ent, attn_slots(c, DBV));
+  int slots_attn = 0;
+  CX_DISPATCH(DBV, slots_attn = attn_slots_db<DB>(c));
+  const AttnPlan plan_pairs = attn_plan(std::max(npairs, 1), c->n_ent, slots_attn);
   const int split_pairs = plan_pairs.wk.n_parts;
   size_t att_rows = (size_t)std::max(npairs, 1) * split_pairs;
   std::vector<AttnPlan> step_plan(T);
   for (int t = 0; t < T; ++t) {
     const int nq = q_off[t + 1] - q_off[t];
-    step_plan[t] = attn_plan(std::max(nq, 1), c->n_ent, attn_slots(c, DBV));
+    step_plan[t] = attn_plan(std::max(nq, 1), c->n_ent, slots_attn);
     att_rows = std::max(att_rows, (size_t)nq * step_plan[t].wk.n_parts);
   }
   float* dAm = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * att_rows));

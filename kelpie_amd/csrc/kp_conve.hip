@@ -22,6 +22,7 @@
 #include <unordered_map>
 
 #include "kp_attn.hpp"
+#include "kp_attn3.hpp"
 
 int cx_pick_db(int dim);
 
@@ -540,7 +541,17 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       KP_HIP(hipMemcpyAsync(dgs, gsv.data(), sizeof(float) * gsv.size(), hipMemcpyHostToDevice, c->stream));
     }
   }
-  const int attn_slots = c->n_cu * (DBV <= 13 ? 2 : 1);  // co-resident attention workgroups
+  int attn_slots = c->n_cu * (DBV <= 13 ? 2 : 1);  // co-resident attention workgroups
+  if (c->attn_mode == 1) {
+    switch (DBV) {
+      case 4: attn_slots = c->n_cu * attn3_wpc<4>(c); break;
+      case 8: attn_slots = c->n_cu * attn3_wpc<8>(c); break;
+      case 13: attn_slots = c->n_cu * attn3_wpc<13>(c); break;
+      case 16: attn_slots = c->n_cu * attn3_wpc<16>(c); break;
+      case 25: attn_slots = c->n_cu * attn3_wpc<25>(c); break;
+      default: throw KpError{KP_ENOTSUP, "ConvE: unsupported padded dimension"};
+    }
+  }
   std::vector<AttnPlan> step_plan(T);
   size_t o_rows = 1;
   for (int t = 0; t < T; ++t) {
@@ -589,9 +600,12 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       }
       dim3 grid(step_plan[t].n_wg);
 #define CV_ATT(DBX)                                                                                                  \
-  hipLaunchKernelGGL((kp_attn<DBX, ATT_BCE_O>), grid, dim3(256), shm_attn, c->stream, c->dE, K, dQ, nk,            \
-                     step_plan[t].wk,                                                                                 \
-                     nullptr, nullptr, dO, dgs + kin_off[t], kc.ylo)
+  if (c->attn_mode == 1)                                                                                             \
+    launch_attn3<DBX, ATT_BCE_O>(c, K, dQ, nk, step_plan[t], nullptr, nullptr, dO, dgs + kin_off[t], kc.ylo);       \
+  else                                                                                                               \
+    hipLaunchKernelGGL((kp_attn<DBX, ATT_BCE_O>), grid, dim3(256), shm_attn, c->stream, c->dE, K, dQ, nk,          \
+                       step_plan[t].wk,                                                                               \
+                       nullptr, nullptr, dO, dgs + kin_off[t], kc.ylo)
       switch (DBV) {
         case 4: CV_ATT(4); break;
         case 8: CV_ATT(8); break;
