@@ -81,8 +81,8 @@ def committed_traffic(workload, kernel):
         return None, None
     with open(files[-1]) as f:
         d = json.load(f).get("fetch_bytes_per_launch", {})
-    m = re.match(r"kp_attn<(\d+),(\w+)>", kernel)
-    want = f"kp_attn<{m.group(1)}, {ATT_MODES[m.group(2)]}>" if m else kernel
+    m = re.match(r"(kp_attn3?)<(\d+),(\w+)>", kernel)
+    want = f"{m.group(1)}<{m.group(2)}, {ATT_MODES[m.group(3)]}>" if m else kernel
     for name, v in d.items():
         if want in name:
             return v["hbm_bytes"], os.path.relpath(files[-1], here)
@@ -90,6 +90,9 @@ def committed_traffic(workload, kernel):
 
 
 ATT_MODES = {"ATT_SOFTMAX_O": 0, "ATT_SOFTMAX": 1, "ATT_BCE_O": 2}
+# dense bf16 MFMA peak of MI355X: 256 CUs x 4 SIMDs x 1024 FLOP/clk (16x16x32 bf16 in 16
+# cycles) x 2.4 GHz (MI355X_MICROARCH.md: ~2.5 PF dense)
+BF16_DENSE_TFLOPS = 2516.6
 
 
 def log(*a):
@@ -272,11 +275,18 @@ def main():
         D = wl["dim"] * (2 if wl["model"] == "ComplEx" else 1)
         flops = 4.0 * D * hot[1]
         achieved = flops / hot[0] / 1e12 if hot[0] > 0 else None
-        peak = 157.3
+        kname = "kp_attn<%d,%s>" % (-(-D // 16), "ATT_SOFTMAX_O" if wl["model"] == "ComplEx" else "ATT_BCE_O")
+        from kelpie_amd._lib import attention_contraction
+        if attention_contraction() == "bf16x3":
+            # kp_attn3: each fp32 product as six bf16 MFMA products (exact three-piece
+            # operand splits), so the fp32-equivalent ceiling is the dense bf16 MFMA peak / 6
+            peak = BF16_DENSE_TFLOPS / 6.0
+            kname = kname.replace("kp_attn<", "kp_attn3<")
+        else:
+            peak = 157.3
         roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": (achieved / peak) if achieved else None, "traffic": None,
-                "kernel": "kp_attn<%d,%s>" % (-(-D // 16), "ATT_SOFTMAX_O" if wl["model"] == "ComplEx"
-                                              else "ATT_BCE_O")}
+                "frac": (achieved / peak) if achieved else None, "traffic": None, "kernel": kname,
+                "fp32_mfma_peak_frac": (achieved / 157.3) if achieved else None}
     roof["traffic"], roof["traffic_source"] = committed_traffic(args.workload, roof["kernel"])
     roof["launches"] = hot[2]
     roof["avg_launch_ms"] = (hot[0] / hot[2] * 1e3) if hot[2] else None

@@ -91,6 +91,12 @@ def lib():
     return _LIB
 
 
+def attention_contraction():
+    """The ComplEx / ConvE attention kernel a new Context uses (kp_api.hip reads the same
+    variable): "bf16x3" (kp_attn3, default) or "f32" (kp_attn, KP_ATTN=f32)."""
+    return "f32" if os.environ.get("KP_ATTN") == "f32" else "bf16x3"
+
+
 def _ptr(a):
     """Raw data address of a C-contiguous numpy array.  ``a.ctypes.data_as`` costs
     15-40 us per call once torch is imported (most of the per-slot host time of

@@ -71,7 +71,10 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     } else {
       c->dp = round_up(m->dim, 16);
     }
-    if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "bf16x3") == 0 ? 1 : 0;
+    // attention contraction (kp_attn3.hpp): bf16x3 MFMA by default, KP_ATTN=f32 selects
+    // the fp32-MFMA kernel of kp_attn.hpp
+    c->attn_mode = 1;
+    if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "f32") == 0 ? 0 : 1;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     KP_HIP(hipEventCreate(&c->ev0));
     KP_HIP(hipEventCreate(&c->ev1));

@@ -10,17 +10,18 @@
 // (8 significant bits each: together the 24 of fp32).  A product a.b is taken as
 //   a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0      (six MFMAs)
 // whose bf16 x bf16 products are exact in the fp32 accumulator; the dropped terms
-// (a1 b2, a2 b1, a2 b2) are below 2^-25 of |a||b|, under fp32's own rounding of the
-// sum, so the scores and O agree with the fp32 path to fp32 rounding (not bitwise:
-// the accumulation order differs).  6 MFMAs of 16 cycles per 16x16x32 block against
+// (a1 b2, a2 b1, a2 b2) are below 2^-24 of |a||b| (one fp32 rounding of the product;
+// tests/test_bf16x3_split.py), so the scores and O agree with the fp32 path to fp32
+// rounding (not bitwise: the accumulation order differs).  6 MFMAs of 16 cycles per 16x16x32 block against
 // 8 f32 MFMAs of 32 cycles: 2.67x fewer MFMA cycles.
 //
 // Table image (built once per context, kp_split3_table): entity e is one ROW_B-byte
-// row [piece 0: DP bf16 | piece 1 | piece 2 | 16 B pad], rows padded with zero rows to
-// a multiple of 32, so a 32-entity key tile is TILE_B contiguous bytes and the LDS
-// tile is the same bytes (one linear LDS-DMA copy).  ROW_B / 16 is odd, so the
-// 16-lane groups of the S-phase ds_read_b128 (16 entity rows, same columns) are
-// conflict-free.
+// row [piece 0: DP bf16 | piece 1 | piece 2 | pad], rows padded with zero rows to a
+// multiple of 32, so a 32-entity key tile is TILE_B contiguous bytes and the LDS tile
+// is the same bytes (one linear LDS-DMA copy).  The pad (split3_row_bytes) makes both
+// the S-phase row reads and the O-phase transposed reads conflict-free (checked
+// against the ds_read_b128 / ds_read_b64_tr_b16 lane groups of MI355X_MICROARCH §LDS:
+// tools/attn3_banks.py); only the 16-deep tail reads stay 2-way.
 //
 // S phase (swapped, as kp_attn): S^T = E . Q^T, A = the entity rows (ds_read_b128 of
 // 8 dims per lane), B = the query pieces held in VGPRs.  C row = entity 4g + r of a
@@ -39,7 +40,10 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 // bytes of one entity row of the split image and of a 32-entity tile
-__host__ __device__ constexpr int split3_row_bytes(int DP) { return 3 * 2 * DP + 16; }
+// (pad: 0 B for an odd number of 16-dim blocks, 32 B for an even one -- the padding
+// that makes the S-phase ds_read_b128 and the O-phase ds_read_b64_tr_b16 conflict-free
+// under gfx950's lane groups; a tile is then a whole number of KiB)
+__host__ __device__ constexpr int split3_row_bytes(int DP) { return 3 * 2 * DP + ((DP / 16) % 2 ? 0 : 32); }
 __host__ __device__ constexpr int split3_tile_bytes(int DP) { return 32 * split3_row_bytes(DP); }
 // LDS-DMA pieces (1 KiB) per tile and the LDS bytes of kp_attn3 (two tile buffers)
 __host__ __device__ constexpr int split3_pieces(int DP) { return (split3_tile_bytes(DP) + 1023) / 1024; }
@@ -53,28 +57,59 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
   l = (__bf16)r2;
 }
 
+// LDS operand reads, two forms (template flag ASM):
+//  - compiler-visible loads: the compiler folds each read's constant offset into the
+//    instruction and places counted lgkmcnt waits itself (best at two waves per SIMD:
+//    ConvE d = 200, 2.80 -> 2.22 ms per launch);
+//  - inline asm (ASM): the reads issue exactly one k-step / O block ahead with the
+//    kernel's own counted waits, at the price of a v_add per read (best for the
+//    register-bound one-wave-per-SIMD ComplEx d = 200 kernel: 0.383 vs 0.408 ms).
+typedef __bf16 bf16v4 __attribute__((__vector_size__(8)));
+template <bool ASM>
 __device__ __forceinline__ bf16x8 lds_rd_bf8(uint32_t addr) {
-  bf16x8 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
+  if constexpr (ASM) {
+    bf16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+  } else {
+    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>((uintptr_t)addr);
+  }
 }
+template <bool ASM>
 __device__ __forceinline__ bf16x4 lds_rd_bf4(uint32_t addr) {
-  bf16x4 v;
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
+  if constexpr (ASM) {
+    bf16x4 v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+  } else {
+    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x4*>((uintptr_t)addr);
+  }
 }
+template <bool ASM>
 __device__ __forceinline__ bf16x4 lds_rd_tr(uint32_t addr) {
-  bf16x4 v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  if constexpr (ASM) {
+    bf16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+  } else {
+    const bf16v4 v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        reinterpret_cast<__attribute__((address_space(3))) bf16v4*>((uintptr_t)addr));
+    return __builtin_bit_cast(bf16x4, v);
+  }
+}
+template <bool ASM>
+__device__ __forceinline__ bf16x8 tied3(bf16x8 v) {
+  if constexpr (ASM) asm volatile("" : "+v"(v));
   return v;
 }
-__device__ __forceinline__ bf16x8 tied(bf16x8 v) {
-  asm volatile("" : "+v"(v));
+template <bool ASM>
+__device__ __forceinline__ bf16x4 tied3(bf16x4 v) {
+  if constexpr (ASM) asm volatile("" : "+v"(v));
   return v;
 }
-__device__ __forceinline__ bf16x4 tied(bf16x4 v) {
-  asm volatile("" : "+v"(v));
-  return v;
+template <bool ASM, int N>
+__device__ __forceinline__ void lgkm_wait3() {
+  if constexpr (ASM) lgkm_wait<N>();
 }
 
 // six-product a.b on one accumulator (smallest terms first)
@@ -127,6 +162,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                                                    float ylo) {
   constexpr bool WITH_O = MODE != ATT_SOFTMAX;
   constexpr int DP = 16 * DB;
+  constexpr bool ASM = DB > 13;  // read form (see lds_rd_bf8)
   constexpr int NK = DP / 32;         // full 32-deep k-steps of the S phase
   constexpr int TAIL = (DP % 32) / 16;  // one 16-deep k-step (16x16x16 MFMA) when DP % 32 == 16
   constexpr int KT = 32;
@@ -230,14 +266,14 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #pragma unroll
           for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) ra[b][u][p] = lds_rd_bf8(rb + u * SUB_B + (uint32_t)(p * PART_B + 64 * s));
+            for (int p = 0; p < 3; ++p) ra[b][u][p] = lds_rd_bf8<ASM>(rb + u * SUB_B + (uint32_t)(p * PART_B + 64 * s));
         };
         auto load_tail = [&]() {
 #pragma unroll
           for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-              rt[u][p] = lds_rd_bf4(rb - 8u * g + u * SUB_B + (uint32_t)(p * PART_B + 64 * NK));  // dims 32 NK + 4g ..
+              rt[u][p] = lds_rd_bf4<ASM>(rb - 8u * g + u * SUB_B + (uint32_t)(p * PART_B + 64 * NK));  // dims 32 NK + 4g ..
         };
         if (NK > 0)
           load_full(0, 0);
@@ -247,28 +283,28 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         for (int s = 0; s < NK; ++s) {
           if (s + 1 < NK) {
             load_full(s + 1, (s + 1) & 1);
-            lgkm_wait<6>();
+            lgkm_wait3<ASM, 6>();
           } else if (TAIL) {
             load_tail();
-            lgkm_wait<6>();
+            lgkm_wait3<ASM, 6>();
           } else {
-            lgkm_wait<0>();
+            lgkm_wait3<ASM, 0>();
           }
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             bf16x8 a[3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) a[p] = tied(ra[s & 1][u][p]);
+            for (int p = 0; p < 3; ++p) a[p] = tied3<ASM>(ra[s & 1][u][p]);
             sc[u] = mfma3(a, qb[s], sc[u]);
           }
         }
         if (TAIL) {
-          lgkm_wait<0>();
+          lgkm_wait3<ASM, 0>();
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             bf16x4 a[3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) a[p] = tied(rt[u][p]);
+            for (int p = 0; p < 3; ++p) a[p] = tied3<ASM>(rt[u][p]);
             sc[u] = mfma3_k16(a, qt4, sc[u]);
           }
         }
@@ -284,8 +320,8 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         auto load_o = [&](int m, int b) {
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
-            ol[b][p] = lds_rd_tr(ob + (uint32_t)(p * PART_B + 32 * m));
-            oh[b][p] = lds_rd_tr(ob + (uint32_t)(16 * ROW_B + p * PART_B + 32 * m));
+            ol[b][p] = lds_rd_tr<ASM>(ob + (uint32_t)(p * PART_B + 32 * m));
+            oh[b][p] = lds_rd_tr<ASM>(ob + (uint32_t)(16 * ROW_B + p * PART_B + 32 * m));
           }
         };
         if (WITH_O) load_o(0, 0);
@@ -341,14 +377,14 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           for (int m = 0; m < DB; ++m) {
             if (m + 1 < DB) {
               load_o(m + 1, (m + 1) & 1);
-              lgkm_wait<6>();
+              lgkm_wait3<ASM, 6>();
             } else {
-              lgkm_wait<0>();
+              lgkm_wait3<ASM, 0>();
             }
             bf16x8 a[3];
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-              const bf16x4 x = tied(ol[m & 1][p]), y = tied(oh[m & 1][p]);
+              const bf16x4 x = tied3<ASM>(ol[m & 1][p]), y = tied3<ASM>(oh[m & 1][p]);
               a[p] = (bf16x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
             }
             O[m] = mfma3(a, pb, O[m]);

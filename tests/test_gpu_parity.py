@@ -293,3 +293,49 @@ def test_complex_db100k_sufficient_batch_equals_sequential(db100k):
             runs.append([eng.compute_relevance(pred, [c]) for c in cands])
     assert runs[0] == runs[1]
     assert np.allclose(runs[0], runs[2], rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("model_name", ["ComplEx", "ConvE"])
+def test_attention_contractions_agree(model_name, monkeypatch):
+    """kp_attn3 (bf16 MFMA, exact three-piece operand splits, the default) against
+    kp_attn (fp32 MFMA, KP_ATTN=f32) on the same post-trainings at the production
+    widths (ComplEx D = 400, ConvE d = 200): target scores within 1e-5 relative, ranks
+    equal.  Both differ from the fp32 FMA chain only in accumulation order."""
+    from kelpie_amd import synth
+    g = synth.make_graph("small", seed=5)
+    ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    deg = ds.entity_to_degree
+    test = [tuple(int(v) for v in t) for t in g.test]
+    preds = [t for t in test if 8 <= deg.get(t[0], 0) <= 40][:2]
+    if model_name == "ComplEx":
+        w = synth.make_weights("ComplEx", g.num_entities, g.num_relations, 200, seed=5, trained_scale=0.3)
+        make = lambda: ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"], init_scale=1e-3)
+        hp = HP
+    else:
+        w = synth.make_weights("ConvE", g.num_entities, g.num_relations, 200, seed=5, conve_random_bn=True,
+                               trained_scale=0.5)
+        bn = {i: {"weight": w[f"bn{i}_weight"], "bias": w[f"bn{i}_bias"], "running_mean": w[f"bn{i}_mean"],
+                  "running_var": w[f"bn{i}_var"]} for i in (1, 2, 3)}
+        make = lambda: ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"],
+                                w["conv_weight"].reshape(32, 3, 3), w["conv_bias"], w["fc_weight"], w["fc_bias"],
+                                bn=bn, hidden_dropout_rate=0.2)
+        hp = CV_HP
+    out = {}
+    for mode in ("f32", "bf16x3"):
+        monkeypatch.setenv("KP_ATTN", mode)
+        model = make()
+        seed_all(42)
+        eng = ka.NecessaryPostTrainingEngine(model, ds, hp)
+        res = []
+        for pred in preds:
+            eng.set_cache()
+            cands = sorted(ds.entity_to_training_triples[pred[0]])[:4]
+            eng.compute_relevance_batch(pred, [[c] for c in cands])
+            res += [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+                    for pt, b in eng.last_results]
+        model.close() if hasattr(model, "close") else None
+        out[mode] = res
+    for a, b in zip(out["bf16x3"], out["f32"]):
+        assert abs(a[1] - b[1]) <= 1e-5 * max(1e-3, abs(b[1])), (a, b)
+        assert abs(a[3] - b[3]) <= 1e-5 * max(1e-3, abs(b[3])), (a, b)
+        assert a[0] == b[0] and a[2] == b[2], (a, b)
