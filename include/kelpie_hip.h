@@ -209,6 +209,19 @@ int kp_rng_bernoulli_bits(uint8_t* state, size_t state_len, uint64_t n, double p
 int kp_rng_transe_epochs(uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos, int32_t R,
                          int32_t epochs, int32_t ratio, int64_t n_entities, int32_t* out);
 
+/* Deferred form of kp_rng_transe_epochs for a batch of slots scheduled in order:
+ * snapshots the torch state, advances it past the slot's randints at once, and
+ * queues the draws.  One worker thread runs the queued numpy shuffles in queue
+ * order on the live numpy state at np_key / np_pos (which nobody else may touch
+ * until kp_rng_wait returns); a small pool (KP_RNG_THREADS, default 2) fills the
+ * randints from each snapshot.  `out` must stay valid until kp_rng_wait.
+ * Same draws, same final states as calling kp_rng_transe_epochs per slot. */
+int kp_rng_transe_enqueue(uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos, int32_t R,
+                          int32_t epochs, int32_t ratio, int64_t n_entities, int32_t* out);
+
+/* Block until every slot queued by kp_rng_transe_enqueue is written. */
+int kp_rng_wait(void);
+
 /* ConvE hidden-dropout keep bits for n_steps steps of rows_per_step[i] x dim
  * (torch.empty(b, dim).bernoulli_(keep) each), each step starting on a fresh
  * 32-bit word; advances the torch state. */

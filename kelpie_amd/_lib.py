@@ -19,7 +19,7 @@ KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
 # symbols declared by include/kelpie_hip.h
 EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_rank", "kp_all_scores",
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
-           "kp_rng_transe_epochs", "kp_rng_conve_masks", "kp_graph_create", "kp_graph_destroy",
+           "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
            "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance"]
 
@@ -82,6 +82,8 @@ def lib():
         L.kp_rng_bernoulli_bits.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_double, C.c_void_p]
         L.kp_rng_transe_epochs.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                            C.c_int32, C.c_int64, C.c_void_p]
+        L.kp_rng_transe_enqueue.argtypes = L.kp_rng_transe_epochs.argtypes
+        L.kp_rng_wait.argtypes = []
         L.kp_rng_conve_masks.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_int32, C.c_double,
                                          C.c_void_p]
         L.kp_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -134,6 +136,24 @@ def transe_epochs(torch_state: np.ndarray, np_key, np_pos, R: int, epochs: int,
     check(lib().kp_rng_transe_epochs(_ptr(torch_state), torch_state.size, key, pos, int(R),
                                      int(epochs), int(ratio), int(n_entities), _ptr(out)))
     return out[:epochs * 3 * R]
+
+
+def transe_enqueue(torch_state: np.ndarray, np_key: int, np_pos: int, R: int, epochs: int,
+                   ratio: int, n_entities: int, out: np.ndarray | None = None) -> np.ndarray:
+    """Deferred :func:`transe_epochs` on the live numpy state at the raw addresses
+    ``np_key`` / ``np_pos``: advances ``torch_state`` now and returns the output
+    array (``out``, int32 C-contiguous of ``epochs*3*R`` elements, if given), which
+    is complete only after :func:`rng_wait`."""
+    if out is None:
+        out = np.empty(max(1, epochs * 3 * R), np.int32)
+    assert out.dtype == np.int32 and out.flags.c_contiguous and out.size >= epochs * 3 * R
+    check(lib().kp_rng_transe_enqueue(_ptr(torch_state), torch_state.size, C.c_void_p(np_key), C.c_void_p(np_pos),
+                                      int(R), int(epochs), int(ratio), int(n_entities), _ptr(out)))
+    return out[:epochs * 3 * R]
+
+
+def rng_wait():
+    check(lib().kp_rng_wait())
 
 
 def conve_masks(torch_state: np.ndarray, rows_per_step, dim: int, keep: float) -> np.ndarray:

@@ -27,6 +27,8 @@
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
+#include <cstdlib>
+#include <deque>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -294,6 +296,139 @@ void bernoulli_words(TorchMt& mt, uint64_t n, double p, uint32_t* out, std::vect
   }
 }
 
+// Deferred TransE draws (kp_rng_transe_enqueue / kp_rng_wait).  The engine schedules
+// a batch's slots one after another on the Python thread; with the synchronous entry
+// point each slot waited for its own shuffles and randints.  Here the caller only
+// snapshots the torch generator and advances it past the slot's randints (twisting,
+// nothing tempered), and the draws are produced behind its back:
+//   * one sequential worker runs the numpy shuffles of every queued slot in queue
+//     order (numpy's consumption is data-dependent: rejection sampling), reading and
+//     writing the live numpy state only between the caller's enqueue and its wait;
+//   * a small pool fills each slot's randints from its own snapshot, in any order.
+// Both write disjoint parts of the slot's output ([row order | entity | head_or_tail]
+// per epoch).  kp_rng_wait() returns once every queued slot is complete.
+struct TeJob {
+  TorchMt mt;  // torch state at the slot's first randint
+  uint32_t* np_key;
+  int32_t* np_pos;
+  int32_t R, epochs, ratio;
+  uint32_t nent;
+  int32_t* out;
+};
+
+void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np,
+                 std::vector<int32_t>& idx) {
+  np.load(np_key, np_pos);
+  idx.resize(std::max(R, 1));
+  for (int i = 0; i < R; ++i) idx[i] = i;
+  for (int e = 0; e < epochs; ++e) {
+    for (int i = R - 1; i >= 1; --i) {  // for i in reversed(range(1, n)): j = interval(i)
+      const uint32_t j = np.interval((uint32_t)i);
+      std::swap(idx[i], idx[j]);
+    }
+    std::memcpy(out + (size_t)e * 3 * R, idx.data(), sizeof(int32_t) * R);
+  }
+  np.store(np_key, np_pos);
+}
+
+// torch.randint(high=N) = random() % N and randint(high=2), ratio*R each per epoch;
+// only the first R of each are stepped
+void te_randints(TorchMt& mt, int32_t R, int32_t epochs, int32_t ratio, uint32_t nent, int32_t* out,
+                 std::vector<uint32_t>& draw) {
+  const uint64_t n = (uint64_t)ratio * (uint64_t)R;
+  const uint64_t fm = UINT64_C(0xFFFFFFFFFFFFFFFF) / nent + 1;
+  draw.resize(std::max(R, 1));
+  for (int e = 0; e < epochs; ++e) {
+    int32_t* o = out + (size_t)e * 3 * R;
+    mt.fill(draw.data(), R);
+    for (int k = 0; k < R; ++k) o[R + k] = (int32_t)fastmod_u32(draw[k], fm, nent);
+    mt.skip(n - (uint64_t)R);
+    mt.fill(draw.data(), R);
+    for (int k = 0; k < R; ++k) o[2 * R + k] = (int32_t)(draw[k] & 1u);
+    mt.skip(n - (uint64_t)R);
+  }
+}
+
+class DrawQueue {
+ public:
+  static DrawQueue& get() {
+    static DrawQueue* q = new DrawQueue();  // never destroyed: workers are detached
+    return *q;
+  }
+  // false: the workers could not be started (the caller then runs the job inline)
+  bool enqueue(const TeJob& j) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!ensure_locked()) return false;
+    shuffles_.push_back(j);
+    fills_.push_back(j);
+    pending_ += 2;
+    cv_work_.notify_all();
+    return true;
+  }
+  int wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_done_.wait(lk, [this] { return pending_ == 0; });
+    const bool f = failed_;
+    failed_ = false;
+    return f ? KP_ENOMEM : KP_OK;
+  }
+
+ private:
+  bool ensure_locked() {
+    const pid_t me = getpid();
+    if (pid_ == me) return true;
+    // first use, or a forked child (the parent's workers do not exist here)
+    shuffles_.clear();
+    fills_.clear();
+    pending_ = 0;
+    int nfill = 2;
+    if (const char* e = std::getenv("KP_RNG_THREADS")) nfill = std::max(1, std::min(16, std::atoi(e)));
+    try {
+      std::thread([this] { loop(true); }).detach();
+      for (int i = 0; i < nfill; ++i) std::thread([this] { loop(false); }).detach();
+    } catch (...) {
+      return false;
+    }
+    pid_ = me;
+    return true;
+  }
+  void loop(bool numpy_worker) {
+    NumpyMt np;
+    std::vector<int32_t> idx;
+    std::vector<uint32_t> draw;
+    const pid_t me = getpid();
+    for (;;) {
+      TeJob j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        auto& q = numpy_worker ? shuffles_ : fills_;
+        cv_work_.wait(lk, [&] { return !q.empty(); });
+        if (pid_ != me) return;
+        j = q.front();
+        q.pop_front();
+      }
+      bool ok = true;
+      try {
+        if (numpy_worker)
+          te_shuffles(j.np_key, j.np_pos, j.R, j.epochs, j.out, np, idx);
+        else
+          te_randints(j.mt, j.R, j.epochs, j.ratio, j.nent, j.out, draw);
+      } catch (...) {
+        ok = false;
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!ok) failed_ = true;
+      if (--pending_ == 0) cv_done_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_work_, cv_done_;
+  std::deque<TeJob> shuffles_, fills_;
+  int64_t pending_ = 0;
+  bool failed_ = false;
+  pid_t pid_ = 0;
+};
+
 }  // namespace
 
 extern "C" {
@@ -305,39 +440,16 @@ int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np
     return KP_EINVAL;
   if (*np_pos < 0 || *np_pos > kN) return KP_EINVAL;
   try {
-    // numpy stream: per epoch np.random.shuffle(rows) in place; the row order composes
     auto shuffles = [&] {
       NumpyMt np;
-      np.load(np_key, np_pos);
-      std::vector<int32_t> idx(R);
-      for (int i = 0; i < R; ++i) idx[i] = i;
-      for (int e = 0; e < epochs; ++e) {
-        for (int i = R - 1; i >= 1; --i) {  // for i in reversed(range(1, n)): j = interval(i)
-          const uint32_t j = np.interval((uint32_t)i);
-          std::swap(idx[i], idx[j]);
-        }
-        std::memcpy(out + (size_t)e * 3 * R, idx.data(), sizeof(int32_t) * R);
-      }
-      np.store(np_key, np_pos);
+      std::vector<int32_t> idx;
+      te_shuffles(np_key, np_pos, R, epochs, out, np, idx);
     };
-    // torch stream: randint(high=N) = random() % N and randint(high=2), ratio*R each;
-    // only the first R of each are stepped
     auto randints = [&] {
       TorchMt mt;
       mt.load(ts);
-      const uint64_t n = (uint64_t)ratio * (uint64_t)R;
-      const uint32_t nent = (uint32_t)n_entities;
-      const uint64_t fm = UINT64_C(0xFFFFFFFFFFFFFFFF) / nent + 1;
-      std::vector<uint32_t> draw(std::max(R, 1));
-      for (int e = 0; e < epochs; ++e) {
-        int32_t* o = out + (size_t)e * 3 * R;
-        mt.fill(draw.data(), R);
-        for (int k = 0; k < R; ++k) o[R + k] = (int32_t)fastmod_u32(draw[k], fm, nent);
-        mt.skip(n - (uint64_t)R);
-        mt.fill(draw.data(), R);
-        for (int k = 0; k < R; ++k) o[2 * R + k] = (int32_t)(draw[k] & 1u);
-        mt.skip(n - (uint64_t)R);
-      }
+      std::vector<uint32_t> draw;
+      te_randints(mt, R, epochs, ratio, (uint32_t)n_entities, out, draw);
       mt.store(ts);
     };
     if (R >= 16 && epochs >= 4) {
@@ -352,6 +464,44 @@ int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np
   }
   return KP_OK;
 }
+
+int kp_rng_transe_enqueue(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs,
+                          int32_t ratio, int64_t n_entities, int32_t* out) {
+  if (!ts || tlen < 24 + kN * 8 || !np_key || !np_pos || R < 0 || epochs < 0 || ratio < 1 || n_entities < 1 ||
+      n_entities >= (1LL << 32) || (R > 0 && epochs > 0 && !out))
+    return KP_EINVAL;
+  if (*np_pos < 0 || *np_pos > kN) return KP_EINVAL;
+  if (R == 0 || epochs == 0) return KP_OK;  // np.random.shuffle of an empty array draws nothing
+  try {
+    TeJob j;
+    j.mt.load(ts);
+    j.np_key = np_key;
+    j.np_pos = np_pos;
+    j.R = R;
+    j.epochs = epochs;
+    j.ratio = ratio;
+    j.nent = (uint32_t)n_entities;
+    j.out = out;
+    TorchMt adv = j.mt;
+    adv.skip((uint64_t)epochs * 2u * (uint64_t)ratio * (uint64_t)R);
+    if (!DrawQueue::get().enqueue(j)) {
+      // no worker threads: finish every queued job first (numpy order), then this one
+      const int rc = DrawQueue::get().wait();
+      if (rc != KP_OK) return rc;
+      NumpyMt np;
+      std::vector<int32_t> idx;
+      std::vector<uint32_t> draw;
+      te_shuffles(np_key, np_pos, R, epochs, out, np, idx);
+      te_randints(j.mt, R, epochs, ratio, j.nent, out, draw);
+    }
+    adv.store(ts);
+  } catch (...) {
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+int kp_rng_wait(void) { return DrawQueue::get().wait(); }
 
 int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim, double keep,
                        uint32_t* out) {

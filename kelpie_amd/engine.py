@@ -40,6 +40,27 @@ class _Slot:
     result: dict = field(default=None)
 
 
+def _contiguous_draws(slots, total):
+    """The slots' draws as one int32 array: a view when they already lie back to back
+    in one buffer (the deferred arena of ReferenceRNG), else a concatenation."""
+    if total == 0:
+        return np.zeros(1, np.int32)
+    arrs = [s.rng for s in slots if s.rng.size]
+    first = arrs[0]
+    base = first.base
+    if base is not None and all(a.dtype == np.int32 and a.base is base and a.flags.c_contiguous for a in arrs):
+        addr = first.__array_interface__["data"][0]
+        end = addr
+        for a in arrs:
+            if a.__array_interface__["data"][0] != end:
+                break
+            end += 4 * a.size
+        else:
+            off = (addr - base.__array_interface__["data"][0]) // 4
+            return base.reshape(-1)[off:off + total]
+    return np.concatenate([s.rng.reshape(-1) for s in slots]).astype(np.int32, copy=False)
+
+
 class RelevanceEngine:
     """engine.py:13-20 + select_entities_to_convert (engine.py:22-126)."""
 
@@ -154,8 +175,7 @@ class PostTrainingEngine(RelevanceEngine):
             else np.zeros((0, 3), np.int32)
         rng_off = np.zeros(n + 1, np.int64)
         rng_off[1:] = np.cumsum([s.rng.size for s in slots])
-        rng = np.concatenate([s.rng.reshape(-1) for s in slots]).astype(np.int32) if rng_off[-1] \
-            else np.zeros(1, np.int32)
+        rng = _contiguous_draws(slots, int(rng_off[-1]))
         pred = np.array([s.pred for s in slots], np.int32)
         filt_off = np.zeros(n + 1, np.int32)
         filt_off[1:] = np.cumsum([len(s.filt) for s in slots])
@@ -193,7 +213,8 @@ class PostTrainingEngine(RelevanceEngine):
     def _multi(self, items, checkpoints=None):
         t0 = time.perf_counter()
         self._deferred_error = None
-        slots, pending, jobs = self._schedule_multi(items, checkpoints)
+        with self.rng.deferred():
+            slots, pending, jobs = self._schedule_multi(items, checkpoints)
         t_sched = time.perf_counter() - t0
         self._run(slots)
         self.last_batch_stats["schedule_s"] = t_sched
@@ -247,7 +268,8 @@ class PostTrainingEngine(RelevanceEngine):
             self.set_cache()
             t0 = time.perf_counter()
             self._deferred_error = None
-            slots, pending, jobs = self._schedule_multi(items, None)
+            with self.rng.deferred():
+                slots, pending, jobs = self._schedule_multi(items, None)
             err, self._deferred_error = self._deferred_error, None
             t_sched = time.perf_counter() - t0
             if inflight is not None:

@@ -28,6 +28,7 @@ bernoulli_: two per element) are pinned by ``tests/test_rng_protocol.py``.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import numpy as np
@@ -49,8 +50,53 @@ def _np_mt_state_address() -> int:
     return int(np.random.mtrand._rand._bit_generator.ctypes.state_address)
 
 
+# TransE draws queued by ReferenceRNG.deferred() and not yet waited for: the live numpy
+# state belongs to the library's worker until sync()
+_outstanding = False
+
+
+def sync():
+    """Wait for every queued TransE draw (the numpy global state is then current)."""
+    global _outstanding
+    if _outstanding:
+        _outstanding = False
+        _lib.rng_wait()
+
+
 class ReferenceRNG:
     """Draws from the process-global torch / numpy generators (reference order)."""
+
+    _defer_depth = 0
+
+    @contextlib.contextmanager
+    def deferred(self):
+        """Inside this block :meth:`transe_epochs` returns arrays that the library's
+        workers fill in the background (kp_rng_transe_enqueue): the caller keeps
+        scheduling while the shuffles and randints of earlier slots are generated.
+        The arrays are complete, and numpy's global state current, on exit (or
+        after :func:`sync`)."""
+        self._defer_depth += 1
+        if self._defer_depth == 1:
+            self._arena, self._arena_pos = None, 0
+        try:
+            yield self
+        finally:
+            self._defer_depth -= 1
+            if self._defer_depth == 0:
+                self._arena = None
+                sync()
+
+    # The deferred draws of one block are laid out back to back in an arena, so the
+    # engine ships a batch's draws without concatenating them (engine._run).  A fresh
+    # arena per block: the arrays of an earlier batch may still be in flight.
+    _ARENA = 1 << 24  # int32 words (64 MiB of address space; untouched pages cost nothing)
+
+    def _take(self, n: int) -> np.ndarray:
+        if self._arena is None or self._arena_pos + n > self._arena.size:
+            self._arena, self._arena_pos = np.empty(max(self._ARENA, n), np.int32), 0
+        out = self._arena[self._arena_pos:self._arena_pos + n]
+        self._arena_pos += n
+        return out
 
     # ---------------------------------------------------------------- model construction
     def rand_init(self, D: int) -> np.ndarray:
@@ -88,12 +134,19 @@ class ReferenceRNG:
         Generated in C++ from the two generators' states (kp_rng_transe_epochs)."""
         if epochs <= 0:
             return np.zeros(0, np.int32)
+        global _outstanding
         st = _get_state()
         # numpy's global MT19937 is advanced in place through its C state struct
         # (BitGenerator.ctypes.state_address -> {uint32 key[624]; int pos}):
         # get_state/set_state would cost ~0.1 ms per slot
         addr = _np_mt_state_address()
-        out = _lib.transe_epochs(st, addr, addr + 4 * 624, R, epochs, ratio, n_entities)
+        if self._defer_depth:
+            out = _lib.transe_enqueue(st, addr, addr + 4 * 624, R, epochs, ratio, n_entities,
+                                      self._take(epochs * 3 * R))
+            _outstanding = True
+        else:
+            sync()
+            out = _lib.transe_epochs(st, addr, addr + 4 * 624, R, epochs, ratio, n_entities)
         _set_state(st)
         return out
 
@@ -111,9 +164,11 @@ class StateCheckpoint:
     """Snapshot of the torch / numpy generators (to rewind speculative draws)."""
 
     def __init__(self):
+        sync()
         self.torch_state = torch.get_rng_state()
         self.np_state = np.random.get_state()
 
     def restore(self):
+        sync()
         torch.set_rng_state(self.torch_state)
         np.random.set_state(self.np_state)

@@ -110,3 +110,43 @@ def test_numpy_state_address_layout():
     k = np.ctypeslib.as_array((ctypes.c_uint32 * 624).from_address(addr))
     p = ctypes.c_int.from_address(addr + 4 * 624).value
     assert np.array_equal(k, np.asarray(key, np.uint32)) and p == pos
+
+
+def test_deferred_transe_draws_match_reference_calls():
+    """ReferenceRNG.deferred(): the slots' shuffles and randints are queued to the
+    library's workers (kp_rng_transe_enqueue) while other torch draws interleave on
+    the calling thread; after the block every array and both generator states equal
+    the reference's sequential calls.  Includes empty slots (R = 0, epochs = 0), a
+    single-row slot and rows that cross numpy regenerations."""
+    ratio, N, E = 5, 301, 6
+    Rs = [9, 0, 150, 1, 700, 33, 16]
+    torch.manual_seed(5)
+    np.random.seed(5)
+    rng = ReferenceRNG()
+    blobs, inits = [], []
+    with rng.deferred():
+        for i, R in enumerate(Rs):
+            inits.append(rng.rand_init(8))
+            blobs.append(rng.transe_epochs(R, 0 if i == 3 else E, ratio, N))
+    # the arrays of one block lie back to back in one arena
+    live = [b for b in blobs if b.size]
+    assert all(b.base is live[0].base for b in live)
+    after = torch.rand(2)
+    np_after = np.random.randint(0, 1 << 30, 8)
+    torch.manual_seed(5)
+    np.random.seed(5)
+    for i, R in enumerate(Rs):
+        assert np.array_equal(torch.rand(1, 8).numpy()[0], inits[i])
+        epochs = 0 if i == 3 else E
+        assert blobs[i].size == epochs * 3 * R
+        blob = blobs[i].reshape(epochs, 3, R)
+        rows = np.arange(R * 3).reshape(R, 3)
+        for e in range(epochs):
+            np.random.shuffle(rows)
+            ents = torch.randint(high=N, size=(ratio * R,))
+            hot = torch.randint(high=2, size=(ratio * R,))
+            assert np.array_equal(rows[:, 0] // 3, blob[e, 0])
+            assert np.array_equal(ents[:R].numpy(), blob[e, 1])
+            assert np.array_equal(hot[:R].numpy(), blob[e, 2])
+    assert torch.equal(torch.rand(2), after)
+    assert np.array_equal(np.random.randint(0, 1 << 30, 8), np_after)

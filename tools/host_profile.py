@@ -1,0 +1,75 @@
+"""Host-side cost of one engine batch's scheduling (no GPU needed): the reference-order
+RNG protocol, kelpie views and slot assembly of a bench workload, with the deferred
+TransE draws' final wait timed separately and a cProfile of the scheduling thread.
+
+    python tools/host_profile.py [--workload transe-fb15k237-necessary] [--preds 16]
+"""
+import argparse
+import cProfile
+import os
+import pstats
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine, rng as krng  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="transe-fb15k237-necessary", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--preds", type=int, default=16)
+    ap.add_argument("--repeats", type=int, default=3)
+    args = ap.parse_args()
+    wl = bench.WORKLOADS[args.workload]
+    ds, model, _ = bench.build(wl, 0, 0)
+    cls = SufficientPostTrainingEngine if wl["mode"] == "sufficient" else NecessaryPostTrainingEngine
+    eng = cls(model, ds, wl["hp"])
+    preds = bench.pick_preds(ds, args.preds * (args.repeats + 1), seed=1234)
+    random.seed(42)
+    np.random.seed(42)
+    torch.manual_seed(42)
+    waits = []
+    orig_wait = krng._lib.rng_wait
+
+    def timed_wait():
+        t = time.perf_counter()
+        orig_wait()
+        waits.append(time.perf_counter() - t)
+    krng._lib.rng_wait = timed_wait
+
+    def items(ps):
+        out = []
+        for p in ps:
+            rules = [[c] for c in bench.candidates_of(ds, p, wl["candidates"])]
+            if wl["mode"] == "sufficient":
+                out.append((p, rules, eng.select_entities_to_convert(p, wl["convert"], 200)))
+            else:
+                out.append((p, rules))
+        return out
+    batches = [items(preds[k * args.preds:(k + 1) * args.preds]) for k in range(args.repeats + 1)]
+    for k in range(args.repeats + 1):
+        eng.set_cache()
+        waits.clear()
+        prof = cProfile.Profile() if k == args.repeats else None
+        t0 = time.perf_counter()
+        if prof:
+            prof.enable()
+        with eng.rng.deferred():
+            slots, _, _ = eng._schedule_multi(batches[k], None)
+        if prof:
+            prof.disable()
+        dt = time.perf_counter() - t0
+        rows = sum(len(s.rows) for s in slots)
+        print(f"batch {k}: schedule {dt * 1e3:.2f} ms  final draw wait {sum(waits) * 1e3:.2f} ms  "
+              f"slots {len(slots)}  rows {rows}", flush=True)
+    pstats.Stats(prof).sort_stats("tottime").print_stats(16)
+
+
+if __name__ == "__main__":
+    main()
