@@ -228,6 +228,11 @@ int kp_rng_wait(void);
 int kp_rng_conve_masks(uint8_t* torch_state, size_t torch_len, int32_t n_steps, const int32_t* rows_per_step,
                        int32_t dim, double keep, uint32_t* out_words);
 
+/* Deferred form of kp_rng_conve_masks (see kp_rng_transe_enqueue): advances the
+ * torch state now, fills `out_words` on the worker pool; complete after kp_rng_wait. */
+int kp_rng_conve_masks_enqueue(uint8_t* torch_state, size_t torch_len, int32_t n_steps, const int32_t* rows_per_step,
+                               int32_t dim, double keep, uint32_t* out_words);
+
 /* Device time of the last kp_posttrain_rank (HIP events on the context's
  * stream): the whole call, the summed durations of its dominant kernel's
  * launches, their count, and the work units those launches processed

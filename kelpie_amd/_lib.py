@@ -19,7 +19,7 @@ KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
 # symbols declared by include/kelpie_hip.h
 EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_rank", "kp_all_scores",
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
-           "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_graph_create", "kp_graph_destroy",
+           "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_rng_conve_masks_enqueue", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
            "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance"]
 
@@ -86,6 +86,7 @@ def lib():
         L.kp_rng_wait.argtypes = []
         L.kp_rng_conve_masks.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_int32, C.c_double,
                                          C.c_void_p]
+        L.kp_rng_conve_masks_enqueue.argtypes = L.kp_rng_conve_masks.argtypes
         L.kp_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                      C.POINTER(C.c_int64), C.POINTER(C.c_double)]
         L.kp_version.restype = C.c_char_p
@@ -156,9 +157,25 @@ def rng_wait():
     check(lib().kp_rng_wait())
 
 
+def mask_words(rows_per_step, dim: int) -> int:
+    """uint32 words of the per-step packed dropout masks (each step starts on a word)."""
+    rows = np.asarray(rows_per_step, dtype=np.int64)
+    return int(((rows * int(dim) + 31) // 32).sum())
+
+
+def conve_masks_enqueue(torch_state: np.ndarray, rows_per_step, dim: int, keep: float, out: np.ndarray):
+    """Deferred :func:`conve_masks` into ``out`` (int32 / uint32, :func:`mask_words`
+    elements): advances ``torch_state`` now; ``out`` is complete after :func:`rng_wait`."""
+    rows = np.ascontiguousarray(rows_per_step, dtype=np.int32)
+    assert out.dtype.itemsize == 4 and out.flags.c_contiguous and out.size >= mask_words(rows, dim)
+    check(lib().kp_rng_conve_masks_enqueue(_ptr(torch_state), torch_state.size, len(rows), _ptr(rows), int(dim),
+                                           float(keep), _ptr(out)))
+    return out
+
+
 def conve_masks(torch_state: np.ndarray, rows_per_step, dim: int, keep: float) -> np.ndarray:
     rows = np.ascontiguousarray(rows_per_step, dtype=np.int32)
-    words = int(sum((int(b) * dim + 31) // 32 for b in rows))
+    words = mask_words(rows, dim)
     out = np.zeros(max(1, words), np.uint32)
     check(lib().kp_rng_conve_masks(_ptr(torch_state), torch_state.size, len(rows), _ptr(rows), int(dim),
                                    float(keep), _ptr(out)))

@@ -307,14 +307,6 @@ void bernoulli_words(TorchMt& mt, uint64_t n, double p, uint32_t* out, std::vect
 //   * a small pool fills each slot's randints from its own snapshot, in any order.
 // Both write disjoint parts of the slot's output ([row order | entity | head_or_tail]
 // per epoch).  kp_rng_wait() returns once every queued slot is complete.
-struct TeJob {
-  TorchMt mt;  // torch state at the slot's first randint
-  uint32_t* np_key;
-  int32_t* np_pos;
-  int32_t R, epochs, ratio;
-  uint32_t nent;
-  int32_t* out;
-};
 
 void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np,
                  std::vector<int32_t>& idx) {
@@ -349,19 +341,32 @@ void te_randints(TorchMt& mt, int32_t R, int32_t epochs, int32_t ratio, uint32_t
   }
 }
 
+// A queued task runs with the worker's scratch (numpy copy, index and draw buffers).
+struct Scratch {
+  NumpyMt np;
+  std::vector<int32_t> idx;
+  std::vector<uint32_t> draw;
+};
+using Task = std::function<void(Scratch&)>;
+
 class DrawQueue {
  public:
   static DrawQueue& get() {
     static DrawQueue* q = new DrawQueue();  // never destroyed: workers are detached
     return *q;
   }
-  // false: the workers could not be started (the caller then runs the job inline)
-  bool enqueue(const TeJob& j) {
+  // seq: runs on the one sequential worker in queue order (may be empty); fill: on the
+  // pool.  false: the workers could not be started (the caller then runs both inline
+  // after a wait()).
+  bool enqueue(Task seq, Task fill) {
     std::lock_guard<std::mutex> lk(mu_);
     if (!ensure_locked()) return false;
-    shuffles_.push_back(j);
-    fills_.push_back(j);
-    pending_ += 2;
+    if (seq) {
+      seq_.push_back(std::move(seq));
+      ++pending_;
+    }
+    fills_.push_back(std::move(fill));
+    ++pending_;
     cv_work_.notify_all();
     return true;
   }
@@ -378,7 +383,7 @@ class DrawQueue {
     const pid_t me = getpid();
     if (pid_ == me) return true;
     // first use, or a forked child (the parent's workers do not exist here)
-    shuffles_.clear();
+    seq_.clear();
     fills_.clear();
     pending_ = 0;
     int nfill = 2;
@@ -392,27 +397,22 @@ class DrawQueue {
     pid_ = me;
     return true;
   }
-  void loop(bool numpy_worker) {
-    NumpyMt np;
-    std::vector<int32_t> idx;
-    std::vector<uint32_t> draw;
+  void loop(bool sequential) {
+    Scratch sc;
     const pid_t me = getpid();
     for (;;) {
-      TeJob j;
+      Task t;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        auto& q = numpy_worker ? shuffles_ : fills_;
+        auto& q = sequential ? seq_ : fills_;
         cv_work_.wait(lk, [&] { return !q.empty(); });
         if (pid_ != me) return;
-        j = q.front();
+        t = std::move(q.front());
         q.pop_front();
       }
       bool ok = true;
       try {
-        if (numpy_worker)
-          te_shuffles(j.np_key, j.np_pos, j.R, j.epochs, j.out, np, idx);
-        else
-          te_randints(j.mt, j.R, j.epochs, j.ratio, j.nent, j.out, draw);
+        t(sc);
       } catch (...) {
         ok = false;
       }
@@ -423,7 +423,7 @@ class DrawQueue {
   }
   std::mutex mu_;
   std::condition_variable cv_work_, cv_done_;
-  std::deque<TeJob> shuffles_, fills_;
+  std::deque<Task> seq_, fills_;
   int64_t pending_ = 0;
   bool failed_ = false;
   pid_t pid_ = 0;
@@ -473,26 +473,60 @@ int kp_rng_transe_enqueue(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* n
   if (*np_pos < 0 || *np_pos > kN) return KP_EINVAL;
   if (R == 0 || epochs == 0) return KP_OK;  // np.random.shuffle of an empty array draws nothing
   try {
-    TeJob j;
-    j.mt.load(ts);
-    j.np_key = np_key;
-    j.np_pos = np_pos;
-    j.R = R;
-    j.epochs = epochs;
-    j.ratio = ratio;
-    j.nent = (uint32_t)n_entities;
-    j.out = out;
-    TorchMt adv = j.mt;
+    TorchMt mt;
+    mt.load(ts);
+    TorchMt adv = mt;
     adv.skip((uint64_t)epochs * 2u * (uint64_t)ratio * (uint64_t)R);
-    if (!DrawQueue::get().enqueue(j)) {
-      // no worker threads: finish every queued job first (numpy order), then this one
+    const uint32_t nent = (uint32_t)n_entities;
+    Task seq = [=](Scratch& sc) { te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx); };
+    Task fill = [=](Scratch& sc) {
+      TorchMt m = mt;
+      te_randints(m, R, epochs, ratio, nent, out, sc.draw);
+    };
+    if (!DrawQueue::get().enqueue(seq, fill)) {
+      // no worker threads: finish every queued task first (numpy order), then this one
       const int rc = DrawQueue::get().wait();
       if (rc != KP_OK) return rc;
-      NumpyMt np;
-      std::vector<int32_t> idx;
-      std::vector<uint32_t> draw;
-      te_shuffles(np_key, np_pos, R, epochs, out, np, idx);
-      te_randints(j.mt, R, epochs, ratio, j.nent, out, draw);
+      Scratch sc;
+      seq(sc);
+      fill(sc);
+    }
+    adv.store(ts);
+  } catch (...) {
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+int kp_rng_conve_masks_enqueue(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim,
+                               double keep, uint32_t* out) {
+  if (!ts || tlen < 24 + kN * 8 || n_steps < 0 || dim <= 0 || (n_steps > 0 && (!rows || !out))) return KP_EINVAL;
+  try {
+    TorchMt mt;
+    mt.load(ts);
+    std::vector<int32_t> rv(rows, rows + n_steps);
+    uint64_t total = 0;
+    for (int st = 0; st < n_steps; ++st) {
+      if (rv[st] < 0) return KP_EINVAL;
+      total += (uint64_t)rv[st] * (uint64_t)dim;
+    }
+    if (total == 0) return KP_OK;
+    TorchMt adv = mt;
+    adv.skip(2 * total);  // bernoulli_: one random64 (two outputs) per element
+    Task fill = [=](Scratch& sc) {
+      TorchMt m = mt;
+      size_t w0 = 0;
+      for (int st = 0; st < n_steps; ++st) {
+        const uint64_t n = (uint64_t)rv[st] * (uint64_t)dim;
+        bernoulli_words(m, n, keep, out + w0, sc.draw);
+        w0 += (size_t)((n + 31) / 32);
+      }
+    };
+    if (!DrawQueue::get().enqueue(Task(), fill)) {
+      const int rc = DrawQueue::get().wait();
+      if (rc != KP_OK) return rc;
+      Scratch sc;
+      fill(sc);
     }
     adv.store(ts);
   } catch (...) {

@@ -154,8 +154,14 @@ class ReferenceRNG:
         """Hidden-dropout keep bits for every step, packed per step in uint32 words."""
         if p_drop <= 0.0 or len(n_rows_per_step) == 0:
             return np.zeros(0, np.int32)
+        global _outstanding
         st = _get_state()
-        words = _lib.conve_masks(st, n_rows_per_step, dim, 1.0 - p_drop)
+        if self._defer_depth:
+            words = _lib.conve_masks_enqueue(st, n_rows_per_step, dim, 1.0 - p_drop,
+                                             self._take(_lib.mask_words(n_rows_per_step, dim)))
+            _outstanding = True
+        else:
+            words = _lib.conve_masks(st, n_rows_per_step, dim, 1.0 - p_drop)
         _set_state(st)
         return words.view(np.int32)
 

@@ -150,3 +150,31 @@ def test_deferred_transe_draws_match_reference_calls():
             assert np.array_equal(hot[:R].numpy(), blob[e, 2])
     assert torch.equal(torch.rand(2), after)
     assert np.array_equal(np.random.randint(0, 1 << 30, 8), np_after)
+
+
+def test_deferred_conve_masks_match_torch_dropout_sequence():
+    """Deferred masks (kp_rng_conve_masks_enqueue) interleaved with other torch draws
+    and a discard, as in a ConvE batch schedule: same bits, same final state."""
+    rng = ReferenceRNG()
+    plans = [[3, 7, 1], [0, 2], [], [40, 40, 13]]
+    torch.manual_seed(23)
+    got, inits = [], []
+    with rng.deferred():
+        for steps in plans:
+            inits.append(rng.rand_init(6))
+            rng.conve_construction(4, 20)
+            got.append(rng.conve_masks(steps, 20, 0.2))
+    after = torch.rand(2)
+    torch.manual_seed(23)
+    for steps, words, init in zip(plans, got, inits):
+        assert np.array_equal(torch.rand(1, 6).numpy()[0], init)
+        torch.empty(32 * 9 + 32 + 4 * 20 + 20).uniform_()  # the construction's draws, one output each
+        off = 0
+        for b in steps:
+            m = torch.empty(b, 20).bernoulli_(0.8).numpy().reshape(-1).astype(np.uint8)
+            nw = (b * 20 + 31) // 32
+            bits = np.unpackbits(words[off:off + nw].view(np.uint32).view(np.uint8), bitorder="little")[:b * 20]
+            assert np.array_equal(bits, m)
+            off += nw
+        assert off == words.size
+    assert torch.equal(torch.rand(2), after)
