@@ -113,8 +113,9 @@ constexpr float kMargin = 40.0f;  // max exponent s - m_ref of a pass-1 weight (
 // partials per query exactly as they merged N-split partials.
 struct AttnWork {
   int ktq;      // key tiles per query tile, ceil(n_ent / 32)
-  int per_wg;   // iterations per workgroup
+  int per_wg;   // iterations per workgroup (stream-K)
   int n_parts;  // partial slots per query
+  int ranges;   // > 0: XCD-grouped aligned key ranges (kp_attn3 only; attn_plan_ranges)
 };
 
 template <int DB, int MODE>
@@ -417,6 +418,38 @@ inline AttnPlan attn_plan(int nq, int n_ent, int slots) {
     parts = std::max(parts, (int)(w1 - w0 + 1));
   }
   p.wk.n_parts = parts;
+  return p;
+}
+
+// Host: the XCD-grouped partition of kp_attn3.  The key tiles are cut into S aligned
+// ranges; a unit is (query tile, range), numbered range-major, so consecutive units
+// read the same keys.  Workgroup b (placed on XCD b % 8 by the dispatcher; used for
+// speed only) takes logical id L = (b % 8) * (n_wg / 8) + b / 8 and units L, L + n_wg,
+// ...: the workgroups of one XCD run consecutive units at the same time, so one key
+// range streams into that XCD's L2 once and serves up to 32 query tiles, where the
+// stream-K ranges of different workgroups are unrelated and every query tile re-reads
+// the table from the Infinity Cache.  S minimises rounds x (range length + a per-unit
+// overhead), at most 16 (the consumers' merge limit); every (query, range) partial is
+// written.
+inline AttnPlan attn_plan_ranges(int nq, int n_ent, int slots) {
+  const int QT = (nq + 63) / 64, ktq = (n_ent + 31) / 32;
+  const int n_wg = std::max(8, slots / 8 * 8);
+  int best_s = 1;
+  long long best = -1;
+  for (int S = 1; S <= std::min(16, ktq); ++S) {
+    const long long rounds = ((long long)QT * S + n_wg - 1) / n_wg;
+    const long long cost = rounds * ((ktq + S - 1) / S + 2);
+    if (best < 0 || cost < best) {
+      best = cost;
+      best_s = S;
+    }
+  }
+  AttnPlan p{};
+  p.wk.ktq = ktq;
+  p.wk.per_wg = 0;
+  p.wk.n_parts = best_s;
+  p.wk.ranges = best_s;
+  p.n_wg = (int)std::min<long long>(n_wg, ((long long)QT * best_s + 7) / 8 * 8);
   return p;
 }
 

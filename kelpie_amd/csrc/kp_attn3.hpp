@@ -33,6 +33,15 @@
 #pragma once
 #include "kp_attn.hpp"
 
+#ifndef KP_O_AHEAD
+#define KP_O_AHEAD 1
+#endif
+#ifndef KP_S_AHEAD
+#define KP_S_AHEAD 1
+#endif
+static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt holds at most 15)");
+static_assert(KP_O_AHEAD >= 1 && KP_O_AHEAD <= 2, "KP_O_AHEAD: 1..2 (lgkmcnt holds at most 15)");
+
 namespace kpattn {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -192,14 +201,33 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
     }
   };
   const int QT = (nq + 63) / 64;
+  // work segments: stream-K ranges (wk.ranges == 0) or XCD-grouped units (attn_plan_ranges)
   const long long total = (long long)QT * wk.ktq;
-  long long it = (long long)blockIdx.x * wk.per_wg;
-  const long long it_end = min(total, it + (long long)wk.per_wg);
-  while (it < it_end) {
-    const int qt = (int)(it / wk.ktq);
-    const int kt0 = (int)(it - (long long)qt * wk.ktq);
-    const int kt1 = (int)min((long long)wk.ktq, (long long)kt0 + (it_end - it));
-    const int part = (int)blockIdx.x - (int)(((long long)qt * wk.ktq) / wk.per_wg);
+  long long it = wk.ranges ? 0 : (long long)blockIdx.x * wk.per_wg;
+  const long long it_end = wk.ranges ? 0 : min(total, it + (long long)wk.per_wg);
+  const int n_units = QT * wk.ranges;
+  int unit = ((int)gridDim.x % 8 == 0) ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8)
+                                       : (int)blockIdx.x;
+  for (;;) {
+    int qt, kt0, kt1, part;
+    bool fill_rest;
+    if (wk.ranges) {
+      if (unit >= n_units) break;
+      qt = unit % QT;
+      part = unit / QT;
+      kt0 = (int)((long long)part * wk.ktq / wk.ranges);
+      kt1 = (int)((long long)(part + 1) * wk.ktq / wk.ranges);
+      fill_rest = false;
+      unit += (int)gridDim.x;
+    } else {
+      if (it >= it_end) break;
+      qt = (int)(it / wk.ktq);
+      kt0 = (int)(it - (long long)qt * wk.ktq);
+      kt1 = (int)min((long long)wk.ktq, (long long)kt0 + (it_end - it));
+      part = (int)blockIdx.x - (int)(((long long)qt * wk.ktq) / wk.per_wg);
+      fill_rest = kt1 == wk.ktq;
+      it += kt1 - kt0;
+    }
     key_begin = kt0 * KT;
     key_end = min(n_ent, kt1 * KT);
     const int ntiles = kt1 - kt0;
@@ -254,13 +282,21 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
       for (int t = 0; t < ntiles; ++t) {
         const int k0 = key_begin + t * KT;
         const uint32_t tb = lds0 + (uint32_t)((t & 1) * BUF_B);
+#if !defined(KP_ATTN_NODMA) && defined(KP_DMA_EARLY)
+        // the other buffer was released by the previous tile's closing barrier
+        if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
+#endif
         // ---- S^T per 16-entity sub-tile u (entity row 16u + c of the tile)
         // Both sub-tiles per k-step; each step's six operand reads are issued one step
         // ahead of its MFMAs (LDS returns in order: a counted lgkmcnt wait).
         f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
         const uint32_t rb = tb + (uint32_t)(c * ROW_B + 16 * g);
         constexpr uint32_t SUB_B = 16u * ROW_B;  // the second sub-tile's rows
-        bf16x8 ra[2][2][3];
+        // k-step j < NK: six ds_read_b128 into buffer j % (SA + 1); step NK (TAIL): six
+        // ds_read_b64.  Reads run KP_S_AHEAD steps ahead of their MFMAs.
+        constexpr int SA = KP_S_AHEAD;
+        constexpr int LAST = NK + TAIL - 1;  // index of the last k-step
+        bf16x8 ra[SA + 1][2][3];
         bf16x4 rt[2][3];
         auto load_full = [&](int s, int b) {
 #pragma unroll
@@ -275,17 +311,23 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             for (int p = 0; p < 3; ++p)
               rt[u][p] = lds_rd_bf4<ASM>(rb - 8u * g + u * SUB_B + (uint32_t)(p * PART_B + 64 * NK));  // dims 32 NK + 4g ..
         };
-        if (NK > 0)
-          load_full(0, 0);
-        else
-          load_tail();
+        auto load_step = [&](int j) {
+          if (j < NK)
+            load_full(j, j % (SA + 1));
+          else
+            load_tail();
+        };
+#pragma unroll
+        for (int j = 0; j < SA && j <= LAST; ++j) load_step(j);
 #pragma unroll
         for (int s = 0; s < NK; ++s) {
-          if (s + 1 < NK) {
-            load_full(s + 1, (s + 1) & 1);
-            lgkm_wait3<ASM, 6>();
-          } else if (TAIL) {
-            load_tail();
+          // pending after step s's reads: steps s + 1 .. min(s + SA, LAST)
+          if (s + SA <= LAST) {
+            load_step(s + SA);
+            lgkm_wait3<ASM, 6 * SA>();
+          } else if (LAST - s >= 2) {
+            lgkm_wait3<ASM, 12>();
+          } else if (LAST - s == 1) {
             lgkm_wait3<ASM, 6>();
           } else {
             lgkm_wait3<ASM, 0>();
@@ -294,7 +336,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           for (int u = 0; u < 2; ++u) {
             bf16x8 a[3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) a[p] = tied3<ASM>(ra[s & 1][u][p]);
+            for (int p = 0; p < 3; ++p) a[p] = tied3<ASM>(ra[s % (SA + 1)][u][p]);
             sc[u] = mfma3(a, qb[s], sc[u]);
           }
         }
@@ -308,7 +350,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             sc[u] = mfma3_k16(a, qt4, sc[u]);
           }
         }
-#ifndef KP_ATTN_NODMA
+#if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
         if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
 #endif
         // O-phase operands: block m's six transposed reads (rows 4g.. and 16 + 4g.. of
@@ -316,7 +358,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         // 4 pp .. 4 pp + 3.  Block 0's are issued before the softmax, block m + 1's
         // before block m's MFMAs.
         const uint32_t ob = tb + (uint32_t)((4 * g + (c >> 2)) * ROW_B + 8 * (c & 3));
-        bf16x4 ol[2][3], oh[2][3];
+        // O-phase read-ahead depth: KP_O_AHEAD blocks (one block is 6 MFMAs = 96 cycles,
+        // less than an LDS read's latency with four waves reading)
+        constexpr int OA = KP_O_AHEAD;
+        bf16x4 ol[OA + 1][3], oh[OA + 1][3];
         auto load_o = [&](int m, int b) {
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
@@ -324,7 +369,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             oh[b][p] = lds_rd_tr<ASM>(ob + (uint32_t)(16 * ROW_B + p * PART_B + 32 * m));
           }
         };
-        if (WITH_O) load_o(0, 0);
+        if (WITH_O) {
+#pragma unroll
+          for (int m = 0; m < OA && m < DB; ++m) load_o(m, m);
+        }
         float pw[2][4];
         if (MODE == ATT_BCE_O) {
 #pragma unroll
@@ -375,8 +423,13 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           }
 #pragma unroll
           for (int m = 0; m < DB; ++m) {
-            if (m + 1 < DB) {
-              load_o(m + 1, (m + 1) & 1);
+            // block m's reads are complete once at most (issued after them) reads are pending
+            if (m + OA < DB) {
+              load_o(m + OA, (m + OA) % (OA + 1));
+              lgkm_wait3<ASM, 6 * OA>();
+            } else if (DB - 1 - m >= 2) {
+              lgkm_wait3<ASM, 12>();
+            } else if (DB - 1 - m == 1) {
               lgkm_wait3<ASM, 6>();
             } else {
               lgkm_wait3<ASM, 0>();
@@ -384,7 +437,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             bf16x8 a[3];
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-              const bf16x4 x = tied3<ASM>(ol[m & 1][p]), y = tied3<ASM>(oh[m & 1][p]);
+              const bf16x4 x = tied3<ASM>(ol[m % (OA + 1)][p]), y = tied3<ASM>(oh[m % (OA + 1)][p]);
               a[p] = (bf16x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
             }
             O[m] = mfma3(a, pb, O[m]);
@@ -416,7 +469,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           *reinterpret_cast<float4*>(dst + 16 * m + 4 * g) = make_float4(O[m][0], O[m][1], O[m][2], O[m][3]);
       }
     }
-    if (kt1 == wk.ktq && valid) {
+    if (fill_rest && valid) {
       for (int pp = part + 1; pp < wk.n_parts; ++pp) {
         const size_t o = (size_t)pp * nq + q;
         if (g == 0 && MODE != ATT_BCE_O) {
@@ -429,7 +482,6 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         }
       }
     }
-    it += kt1 - kt0;
   }
 }
 
@@ -463,6 +515,26 @@ int attn3_wpc(kp_ctx* c) {
     c->attn3_wpc = std::max(1, std::min(n, n2));
   }
   return c->attn3_wpc;
+}
+
+// Host: the partition of the context's attention kernel.  kp_attn3 takes the XCD-grouped
+// aligned ranges unless their quantisation costs more than a slack over stream-K's
+// balanced split.  The L2 reuse they buy (FETCH_SIZE 14x lower) was worth 2-7 % per
+// launch with the 35 MB FB15k-237 ComplEx image and 6 % with the 158 MB YAGO3-10 ConvE
+// image, which stream-K re-reads through the Infinity Cache at worse hit rates: slack
+// 5 % up to 64 MB of image, 15 % above.  KP_ATTN_PART=streamk
+// forces stream-K.  The fp32 kp_attn always uses stream-K.
+inline AttnPlan attn_plan_ctx(const kp_ctx* c, int nq, int n_ent, int slots) {
+  const AttnPlan sk = attn_plan(nq, n_ent, slots);
+  if (c->attn_mode != 1 || !c->attn_ranges) return sk;
+  const AttnPlan r = attn_plan_ranges(nq, n_ent, slots);
+  const long long QT = (nq + 63) / 64, S = r.wk.ranges, ktq = r.wk.ktq;
+  const long long n_wg = std::max(8, slots / 8 * 8);
+  const long long cost_r = (QT * S + n_wg - 1) / n_wg * ((ktq + S - 1) / S + 2);
+  const long long cost_sk = (long long)sk.wk.per_wg + 2;
+  const long long image = (long long)n_ent * split3_row_bytes(c->dp);
+  const long long slack = image > (64ll << 20) ? 115 : 105;
+  return 100 * cost_r <= slack * cost_sk ? r : sk;
 }
 
 template <int DB, int MODE>

@@ -92,6 +92,7 @@ struct kp_ctx {
   bool time_hot = true;
   // attention contraction: 0 = fp32 MFMA (kp_attn.hpp), 1 = bf16x3 MFMA (kp_attn3.hpp)
   int attn_mode = 0;
+  bool attn_ranges = true;  // kp_attn3 partition: XCD-grouped ranges (false: stream-K)
   DevBuf e3;               // kp_attn3's split image of dE, built on first use
   bool e3_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)

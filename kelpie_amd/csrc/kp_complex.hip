@@ -543,13 +543,13 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   // frozen-head pairs: q and frozen log-sum-exp
   int slots_attn = 0;
   CX_DISPATCH(DBV, slots_attn = attn_slots_db<DB>(c));
-  const AttnPlan plan_pairs = attn_plan(std::max(npairs, 1), c->n_ent, slots_attn);
+  const AttnPlan plan_pairs = attn_plan_ctx(c, std::max(npairs, 1), c->n_ent, slots_attn);
   const int split_pairs = plan_pairs.wk.n_parts;
   size_t att_rows = (size_t)std::max(npairs, 1) * split_pairs;
   std::vector<AttnPlan> step_plan(T);
   for (int t = 0; t < T; ++t) {
     const int nq = q_off[t + 1] - q_off[t];
-    step_plan[t] = attn_plan(std::max(nq, 1), c->n_ent, slots_attn);
+    step_plan[t] = attn_plan_ctx(c, std::max(nq, 1), c->n_ent, slots_attn);
     att_rows = std::max(att_rows, (size_t)nq * step_plan[t].wk.n_parts);
   }
   float* dAm = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * att_rows));

@@ -556,7 +556,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   size_t o_rows = 1;
   for (int t = 0; t < T; ++t) {
     const int nk = kin_off[t + 1] - kin_off[t];
-    step_plan[t] = attn_plan(std::max(nk, 1), K, attn_slots);
+    step_plan[t] = attn_plan_ctx(c, std::max(nk, 1), K, attn_slots);
     o_rows = std::max(o_rows, (size_t)nk * step_plan[t].wk.n_parts);
   }
   float* dO = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * o_rows * DP));
