@@ -122,27 +122,35 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
     const float hi = fmaxf(lse_f, z), lo = fminf(lse_f, z);
     const float lse = hi + log1pf(__expf(lo - hi));
     const float pk = __expf(z - lse);
-    float wsp[UPD_MAXSPLIT];
+    // merge the partials split by split: each split's loads for all of this lane's
+    // dimensions are in flight together, with few live registers (occupancy)
+    constexpr int NI = (DP / 2 + 63) / 64;
+    float ore_k[NI], oim_k[NI];
 #pragma unroll
-    for (int sp = 0; sp < UPD_MAXSPLIT; ++sp) {
-      float ms = (sp < n_split) ? att_m[(size_t)sp * nq + item] : kNegInf;
-      wsp[sp] = (ms == kNegInf) ? 0.f : __expf(ms - lse);
+    for (int k = 0; k < NI; ++k) ore_k[k] = oim_k[k] = 0.f;
+    for (int sp = 0; sp < n_split; ++sp) {
+      const float ms = att_m[(size_t)sp * nq + item];
+      const float wv = (ms == kNegInf) ? 0.f : __expf(ms - lse);
+      const float* Op = att_O + ((size_t)sp * nq + item) * DP;
+#pragma unroll
+      for (int k = 0; k < NI; ++k) {
+        const int i = lane + 64 * k;
+        if (i < half) {
+          ore_k[k] += wv * Op[i];
+          oim_k[k] += wv * Op[i + half];
+        }
+      }
     }
     const float fc = (float)Q.c, fck = (float)Q.ck;
     const float cf = fc * pk - fck;
     const float* ts = Tsum + (size_t)sq.z * DP;
-    for (int i = lane; i < half; i += 64) {
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = lane + 64 * k;
+      if (i >= half) continue;
       const float a = x[i], b = x[i + half];
       const float cc = rel[i], ee = rel[i + half];
-      float ore = 0.f, oim = 0.f;
-#pragma unroll
-      for (int sp = 0; sp < UPD_MAXSPLIT; ++sp) {
-        if (sp < n_split) {
-          const float* Op = att_O + ((size_t)sp * nq + item) * DP;
-          ore += wsp[sp] * Op[i];
-          oim += wsp[sp] * Op[i + half];
-        }
-      }
+      const float ore = ore_k[k], oim = oim_k[k];
       const float ere = ore + pk * a, eim = oim + pk * b;
       const float dre = fc * ere - ts[i] - fck * a;
       const float dim_ = fc * eim - ts[i + half] - fck * b;
@@ -177,20 +185,47 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
   const CxPlan P = plans[a4.y];
   float* x = X + (size_t)slot * DP;
   const float inv_b = 1.0f / (float)P.b;
+  // contribution rows: the slot's queries, then its frozen-head rows
+  const int nc = P.q_count + P.t_count;
+  auto crow = [&](int j) -> const float* {
+    return j < P.q_count ? contrib + (size_t)(a4.z + j) * DP : contrib + (size_t)(nq + a4.w + j - P.q_count) * DP;
+  };
+  // The rows sum in four wave-strided partials with four chains each, so 16 rows'
+  // loads are in flight at once (one sequential chain per dimension was bound by the
+  // load latency: ~90 us per step at FB15k-237 sizes); a slot with at most UPD_WIDE
+  // rows keeps the sequential chain (the choice is block-uniform).
+  constexpr int UPD_WIDE = 4;
+  __shared__ float red[4][DP];
+  if (nc > UPD_WIDE) {
+    const int w = tid >> 6, lane = tid & 63;
+    for (int d = lane; d < 2 * half; d += 64) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      int j = w;
+      for (; j + 12 < nc; j += 16) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += crow(j + 4 * k)[d];
+      }
+      if (j < nc) acc[0] += crow(j)[d];  // at most three rows are left
+      if (j + 4 < nc) acc[1] += crow(j + 4)[d];
+      if (j + 8 < nc) acc[2] += crow(j + 8)[d];
+      red[w][d] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int u = 0; u < (DP / 2 + 255) / 256; ++u) {
     const int i = tid + 256 * u;
     if (i >= half) continue;
     float gv[2] = {0.f, 0.f};
-    for (int j = 0; j < P.q_count; ++j) {
-      const float* cq = contrib + (size_t)(a4.z + j) * DP;
-      gv[0] += cq[i];
-      gv[1] += cq[i + half];
-    }
-    for (int j = 0; j < P.t_count; ++j) {
-      const float* ct = contrib + (size_t)(nq + a4.w + j) * DP;
-      gv[0] += ct[i];
-      gv[1] += ct[i + half];
+    if (nc > UPD_WIDE) {
+      gv[0] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+      gv[1] = (red[0][i + half] + red[1][i + half]) + (red[2][i + half] + red[3][i + half]);
+    } else {
+      for (int j = 0; j < nc; ++j) {
+        const float* c = crow(j);
+        gv[0] += c[i];
+        gv[1] += c[i + half];
+      }
     }
     gv[0] *= inv_b;
     gv[1] *= inv_b;
