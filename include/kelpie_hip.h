@@ -241,6 +241,13 @@ int kp_rng_conve_masks_enqueue(uint8_t* torch_state, size_t torch_len, int32_t n
 int kp_last_timing(const kp_ctx* ctx, double* device_seconds, double* hot_kernel_seconds,
                    int64_t* hot_kernel_launches, double* hot_work_units);
 
+/* [start, end] (seconds, on a time base shared by every context of the device) of
+ * each dominant-kernel launch of the last kp_posttrain_rank: *n = the launch count,
+ * the first min(cap, *n) pairs are written to out[2 i], out[2 i + 1].  With batches
+ * in flight on several contexts the launches can overlap; bench.py merges the
+ * intervals to the time the device spent in the kernel. */
+int kp_hot_intervals(const kp_ctx* ctx, int64_t cap, double* out, int64_t* n);
+
 /* ---- candidate prefilters, host C++ ----------------
  * The undirected multigraph of TopologyPreFilter / WeightedTopologyPreFilter
  * (topology_prefilter.py:12-14, weighted_topology_prefilter.py:16-18): one

@@ -21,7 +21,7 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
            "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_rng_conve_masks_enqueue", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
-           "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance"]
+           "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals"]
 
 
 class ModelDesc(C.Structure):
@@ -89,6 +89,7 @@ def lib():
         L.kp_rng_conve_masks_enqueue.argtypes = L.kp_rng_conve_masks.argtypes
         L.kp_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                      C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+        L.kp_hot_intervals.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(C.c_int64)]
         L.kp_version.restype = C.c_char_p
         _LIB = L
     return _LIB
@@ -281,6 +282,14 @@ class Context:
         check(lib().kp_criage_relevance(self.h, len(it), _ptr(it), len(ents), _ptr(ents), _ptr(off), _ptr(tl),
                                         _ptr(out), _ptr(status)), self.h)
         return out, status
+
+    def hot_intervals(self) -> np.ndarray:
+        """[start, end] seconds of each dominant-kernel launch of the last batch (kp_hot_intervals)."""
+        n = C.c_int64()
+        check(lib().kp_hot_intervals(self.h, 0, None, C.byref(n)), self.h)
+        out = np.zeros((max(1, n.value), 2), np.float64)
+        check(lib().kp_hot_intervals(self.h, n.value, _ptr(out), C.byref(n)), self.h)
+        return out[:n.value]
 
     def last_timing(self):
         a, b, n, w = C.c_double(), C.c_double(), C.c_int64(), C.c_double()

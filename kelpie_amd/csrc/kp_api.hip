@@ -63,6 +63,7 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     c->dim = m->dim;
     KP_HIP(hipSetDevice(device));
     KP_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    (void)kp_time_base(device, nullptr);
     if (m->model == KP_MODEL_COMPLEX || m->model == KP_MODEL_CONVE) {
       KP_REQUIRE(m->model != KP_MODEL_COMPLEX || m->dim % 2 == 0, "ComplEx: row width must be even ([Re | Im])");
       int db = cx_pick_db(m->dim);
@@ -264,6 +265,17 @@ int kp_criage_relevance(kp_ctx* c, int32_t n, const int32_t* items, int32_t n_en
 }
 
 // The host RNG protocol entry points (kp_rng_*, kp_mt19937_discard) are in kp_rng.cpp.
+
+int kp_hot_intervals(const kp_ctx* c, int64_t cap, double* out, int64_t* n) {
+  if (!c || cap < 0 || (cap > 0 && !out)) return KP_EINVAL;
+  const int64_t have = (int64_t)(c->hot_iv.size() / 2);
+  if (n) *n = have;
+  for (int64_t i = 0; i < std::min(cap, have); ++i) {
+    out[2 * i] = c->hot_iv[2 * i];
+    out[2 * i + 1] = c->hot_iv[2 * i + 1];
+  }
+  return KP_OK;
+}
 
 int kp_last_timing(const kp_ctx* c, double* dev_s, double* hot_s, int64_t* hot_n, double* hot_w) {
   if (!c) return KP_EINVAL;

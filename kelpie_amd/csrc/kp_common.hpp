@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -98,6 +99,7 @@ struct kp_ctx {
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<double, double>> hot_pairs;  // (work units, seconds) per hot launch
+  std::vector<double> hot_iv;  // [start, end] per hot launch, seconds since the device's time base
   hipEvent_t event(size_t i) {
     while (evpool.size() <= i) {
       hipEvent_t e;
@@ -178,3 +180,34 @@ void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, in
                        const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
                        int minimizer, float* d_target, int64_t* d_rank,
                        int mode = 0);
+
+// Per-device time base: one event recorded (and completed) when the device's first
+// context is created.  Hot-launch intervals of every context on the device are taken
+// against it, so launches of contexts that run at once can be merged on one axis
+// (kp_hot_intervals).
+inline hipEvent_t kp_time_base(int device, hipStream_t stream) {
+  static std::mutex mu;
+  static hipEvent_t base[64] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (device < 0 || device >= 64) return nullptr;
+  if (!base[device]) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventRecord(e, stream) != hipSuccess || hipEventSynchronize(e) != hipSuccess) {
+      (void)hipEventDestroy(e);
+      return nullptr;
+    }
+    base[device] = e;
+  }
+  return base[device];
+}
+
+// append the [start, end] of one timed launch (events a -> b) to c->hot_iv
+inline void kp_push_interval(kp_ctx* c, hipEvent_t a, hipEvent_t b) {
+  const hipEvent_t t0 = kp_time_base(c->device, c->stream);
+  float ms_a = 0.f, ms_b = 0.f;
+  if (!t0 || hipEventElapsedTime(&ms_a, t0, a) != hipSuccess || hipEventElapsedTime(&ms_b, t0, b) != hipSuccess)
+    return;
+  c->hot_iv.push_back(ms_a * 1e-3);
+  c->hot_iv.push_back(ms_b * 1e-3);
+}

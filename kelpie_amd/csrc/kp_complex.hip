@@ -631,6 +631,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   KP_HIP(hipEventRecord(h0, c->stream));
   int64_t hot_launches = 0;
   c->hot_pairs.clear();
+  c->hot_iv.clear();
   for (int t = 0; t < T; ++t) {
     const int nq = q_off[t + 1] - q_off[t];
     const int na = act_off[t + 1] - act_off[t];
@@ -697,6 +698,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     KP_HIP(hipEventElapsedTime(&ms, c->event(2 * i), c->event(2 * i + 1)));
     c->hot_pairs[i].second = ms * 1e-3;
     hot += ms * 1e-3;
+    kp_push_interval(c, c->event(2 * i), c->event(2 * i + 1));
   }
   c->timing.device_s = ms_all * 1e-3;
   c->timing.loop_s = ms_loop * 1e-3;

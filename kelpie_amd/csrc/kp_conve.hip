@@ -576,6 +576,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   double hot = 0.0, work = 0.0;
   int64_t launches = 0;
   c->hot_pairs.clear();
+  c->hot_iv.clear();
   const size_t shm_attn = attn_lds_bytes(DP / 16);
   const size_t shm_cbwd = sizeof(float) * 32 * 20 * (c->dim / 20 - 2);
   for (int t = 0; t < T; ++t) {
@@ -676,6 +677,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     float ms = 0.f;
     KP_HIP(hipEventElapsedTime(&ms, c->event(2 * i), c->event(2 * i + 1)));
     hot += ms * 1e-3;
+    kp_push_interval(c, c->event(2 * i), c->event(2 * i + 1));
     work += c->hot_pairs[i].first * (double)K;
   }
   for (DevBuf* b : {&bF, &bT, &bR}) b->release();

@@ -574,6 +574,8 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float ms_all = 0.f, ms_hot = 0.f;
   KP_HIP(hipEventElapsedTime(&ms_all, c->ev0, c->ev1));
   KP_HIP(hipEventElapsedTime(&ms_hot, ea, eb));
+  c->hot_iv.clear();
+  kp_push_interval(c, ea, eb);
   double work = 0;
   for (int s = 0; s < ns; ++s) work += (double)hp->epochs * slots[s].R;
   c->timing.device_s = ms_all * 1e-3;

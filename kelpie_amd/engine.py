@@ -162,9 +162,9 @@ class PostTrainingEngine(RelevanceEngine):
         slots.append(self._slot(x_pt, rows, kp, filt))
         return len(slots) - 1, pred
 
-    def _run(self, slots):
+    def _run(self, slots, ctx=None):
         if not slots:
-            return
+            return {}
         t_run = time.perf_counter()
         n = len(slots)
         D = self.model.dimension
@@ -182,13 +182,17 @@ class PostTrainingEngine(RelevanceEngine):
         filt = np.array([e for s in slots for e in s.filt], np.int32) if filt_off[-1] else np.zeros(1, np.int32)
         assert x0.shape == (n, D)
         t_lib = time.perf_counter()
-        score, rank, _ = self.model.ctx.posttrain_rank(self._kp_hp, x0, row_off, rows, rng_off, rng, pred,
-                                                       filt_off, filt)
+        ctx = ctx or self.model.ctx
+        score, rank, _ = ctx.posttrain_rank(self._kp_hp, x0, row_off, rows, rng_off, rng, pred, filt_off, filt)
         t_end = time.perf_counter()
         for i, s in enumerate(slots):
             s.result = {"target_score": float(score[i]), "target_rank": int(rank[i])}
-        self.last_batch_stats = {"slots": n, "rows": int(row_off[-1]), "pack_s": t_lib - t_run,
-                                 "lib_s": t_end - t_lib, **self.model.ctx.last_timing()}
+        stats = {"slots": n, "rows": int(row_off[-1]), "pack_s": t_lib - t_run, "lib_s": t_end - t_lib,
+                 **ctx.last_timing()}
+        if hasattr(ctx, "hot_intervals"):
+            stats["hot_iv"] = ctx.hot_intervals()
+        self.last_batch_stats = stats
+        return stats
 
     def _base_result(self, key, slots, pending_base):
         if key in self.base_pt_results:
@@ -232,24 +236,58 @@ class PostTrainingEngine(RelevanceEngine):
             self.base_pt_results.setdefault(key, slots[i].result)
         raise err
 
-    def compute_relevance_pipeline(self, batches):
+    def warm_contexts(self, items, depth=None):
+        """Run the batch ``items`` once on every extra pipeline context, so their
+        workspaces are allocated and the attention table image is built outside a
+        timed region.  Consumes no random draws: the generator states are restored."""
+        import os
+        if depth is None:
+            depth = int(os.environ.get("KELPIE_PIPELINE_DEPTH", "2"))
+        ctxs = self.model.contexts(max(1, depth))
+        if len(ctxs) < 2:
+            return
+        cp = StateCheckpoint()
+        try:
+            self.set_cache()
+            self._deferred_error = None
+            with self.rng.deferred():
+                slots, _, _ = self._schedule_multi(items, None)
+            self._deferred_error = None
+            for ctx in ctxs[1:]:
+                self._run(slots, ctx=ctx)
+        finally:
+            cp.restore()
+            self.set_cache()
+
+    def compute_relevance_pipeline(self, batches, depth=None):
         """Equivalent to ``[(self.set_cache(), self.compute_relevance_multi(b))[1] for b in batches]``
         but the host schedules batch k+1 (its reference-order random draws and
         slot assembly) while batch k runs on the device: the library call
         releases the GIL.  Draw order is unchanged because scheduling stays
         sequential on this thread; each batch starts from a cleared cache, so no
         batch's schedule depends on another's results.  ``last_batch_stats`` is
-        a list of the per-batch stats."""
+        a list of the per-batch stats.
+
+        With ``depth`` > 1 (default ``KELPIE_PIPELINE_DEPTH``, else 2) up to that many
+        batches are in flight, each on its own device context
+        (``FrozenModel.contexts``: own stream and workspaces over a replica of the
+        frozen tables), so one batch's library-side planning, uploads and result
+        download overlap the other's kernels instead of leaving the device idle."""
+        import collections
+        import os
         import threading
+
+        if depth is None:
+            depth = int(os.environ.get("KELPIE_PIPELINE_DEPTH", "2"))
+        ctxs = self.model.contexts(max(1, depth))
 
         def run(state):
             try:
-                self._run(state["slots"])
-                state["stats"] = dict(self.last_batch_stats)
+                state["stats"] = dict(self._run(state["slots"], ctx=state["ctx"]))
             except BaseException as e:  # re-raised on the scheduling thread
                 state["error"] = e
 
-        outs, stats, inflight = [], [], None
+        outs, stats, inflight = [], [], collections.deque()
 
         def finish(state):
             state["thread"].join()
@@ -264,24 +302,30 @@ class PostTrainingEngine(RelevanceEngine):
             self._deferred_error = state.get("deferred")
             self._raise_deferred(state["slots"], state["pending"])
 
-        for items in batches:
-            self.set_cache()
-            t0 = time.perf_counter()
-            self._deferred_error = None
-            with self.rng.deferred():
-                slots, pending, jobs = self._schedule_multi(items, None)
-            err, self._deferred_error = self._deferred_error, None
-            t_sched = time.perf_counter() - t0
-            if inflight is not None:
-                finish(inflight)
-            inflight = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched, "error": None}
-            inflight["deferred"] = err
-            inflight["thread"] = threading.Thread(target=run, args=(inflight,), daemon=True)
-            inflight["thread"].start()
-            if err is not None:
-                break  # the sequential reference stops at the failing call
-        if inflight is not None:
-            finish(inflight)
+        try:
+            for b, items in enumerate(batches):
+                self.set_cache()
+                t0 = time.perf_counter()
+                self._deferred_error = None
+                with self.rng.deferred():
+                    slots, pending, jobs = self._schedule_multi(items, None)
+                err, self._deferred_error = self._deferred_error, None
+                t_sched = time.perf_counter() - t0
+                # batch b uses context b % depth: the batch before it on that context is done
+                while len(inflight) >= len(ctxs):
+                    finish(inflight.popleft())
+                state = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched, "error": None,
+                         "deferred": err, "ctx": ctxs[b % len(ctxs)]}
+                state["thread"] = threading.Thread(target=run, args=(state,), daemon=True)
+                state["thread"].start()
+                inflight.append(state)
+                if err is not None:
+                    break  # the sequential reference stops at the failing call
+            while inflight:
+                finish(inflight.popleft())
+        finally:
+            for st in inflight:  # an earlier batch raised: let the others' device work end
+                st["thread"].join()
         self.last_batch_stats = stats
         return outs
 

@@ -51,6 +51,17 @@ class FrozenModel:
     def _make_ctx(self):
         return _lib.Context(self.name, self.entity_embeddings, self.relation_embeddings, device=self.device)
 
+    def contexts(self, n: int) -> list:
+        """``n`` device contexts over replicas of the frozen tables (the first is
+        :attr:`ctx`), for batches in flight at once; a stand-in context (tests) is
+        never replicated."""
+        if not isinstance(self.ctx, _lib.Context):
+            return [self.ctx]
+        extra = self.__dict__.setdefault("_ctx_extra", [])
+        while len(extra) < n - 1:
+            extra.append(self._make_ctx())
+        return [self.ctx] + extra[:n - 1]
+
     def all_scores(self, triples):
         """``Model.all_scores`` over the frozen entities (model.py:19): float32 [B, |E|]."""
         t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
