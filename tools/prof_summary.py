@@ -31,11 +31,28 @@ def main():
         for r in rows:
             w.writerow([r[0], r[1], f"{r[2]:.3f}", f"{r[3]:.3f}", f"{r[4]:.2f}"])
     per = defaultdict(list)
+    spans = defaultdict(list)
     for name, s, e in c.execute("select name, start, end from kernels order by start"):
         per[name].append((e - s) / 1e3)
+        spans[name].append((s, e))
     timed = {n: (sum(d[a.skip_first:]) / max(1, len(d) - a.skip_first), len(d) - a.skip_first)
              for n, d in per.items() if len(d) > a.skip_first}
-    summary = {"timed_avg_us": {n: {"avg_us": v[0], "launches": v[1]} for n, v in timed.items()}}
+
+    def union_us(iv):
+        # launches of one kernel on two streams can overlap: the time the device spent in it
+        iv = sorted(iv)
+        total, (s0, e0) = 0, iv[0]
+        for s1, e1 in iv[1:]:
+            if s1 > e0:
+                total += e0 - s0
+                s0, e0 = s1, e1
+            else:
+                e0 = max(e0, e1)
+        return (total + e0 - s0) / 1e3
+
+    summary = {"timed_avg_us": {n: {"avg_us": v[0], "launches": v[1],
+                                    "union_us_per_launch": union_us(spans[n][a.skip_first:]) / v[1]}
+                                for n, v in timed.items()}}
     if a.pmc:
         p = sqlite3.connect(a.pmc)
         acc = defaultdict(list)
