@@ -251,12 +251,34 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
   for (int d = tid; d < k.dp; d += 256) xs[d] = x[d];
   __syncthreads();
   float g[3] = {0.f, 0.f, 0.f};
-  for (int j = 0; j < A.k_count; ++j) {
-    const int ii = A.k_begin + j;
-    const float G = gk[ii];
-    for (int u = 0; u < 3; ++u) {
-      const int d = tid + 256 * u;
-      if (d < k.dim) g[u] += G * Q[(size_t)ii * k.dp + d] + dl[(size_t)ii * k.dp + d];
+  // kelpie-head pair rows: a slot with more than 4 sums them in four wave-strided
+  // partials with two chains each (one chain per dimension was bound by load latency);
+  // the choice is block-uniform
+  __shared__ float gk_s[4][640];
+  const bool wide = A.k_count > 4;
+  if (wide) {
+    for (int d = lane; d < k.dim; d += 64) {
+      float a0 = 0.f, a1 = 0.f;
+      int j = wave;
+      for (; j + 4 < A.k_count; j += 8) {
+        const int i0 = A.k_begin + j, i1 = i0 + 4;
+        a0 += gk[i0] * Q[(size_t)i0 * k.dp + d] + dl[(size_t)i0 * k.dp + d];
+        a1 += gk[i1] * Q[(size_t)i1 * k.dp + d] + dl[(size_t)i1 * k.dp + d];
+      }
+      if (j < A.k_count) {
+        const int i0 = A.k_begin + j;
+        a0 += gk[i0] * Q[(size_t)i0 * k.dp + d] + dl[(size_t)i0 * k.dp + d];
+      }
+      gk_s[wave][d] = a0 + a1;
+    }
+  } else {
+    for (int j = 0; j < A.k_count; ++j) {
+      const int ii = A.k_begin + j;
+      const float G = gk[ii];
+      for (int u = 0; u < 3; ++u) {
+        const int d = tid + 256 * u;
+        if (d < k.dim) g[u] += G * Q[(size_t)ii * k.dp + d] + dl[(size_t)ii * k.dp + d];
+      }
     }
   }
   // frozen-head pairs (o, r_inv, kelpie): the kelpie column's BCE gradient G * x_fc,
@@ -296,7 +318,9 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
   __syncthreads();
   for (int u = 0; u < 3; ++u) {
     const int d = tid + 256 * u;
-    if (d < k.dim) g[u] += (gw_s[0][d] + gw_s[1][d]) + (gw_s[2][d] + gw_s[3][d]);
+    if (d >= k.dim) continue;
+    if (wide) g[u] = (gk_s[0][d] + gk_s[1][d]) + (gk_s[2][d] + gk_s[3][d]);
+    g[u] += (gw_s[0][d] + gw_s[1][d]) + (gw_s[2][d] + gw_s[3][d]);
   }
   for (int u = 0; u < 3; ++u) {
     const int d = tid + 256 * u;
