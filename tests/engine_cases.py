@@ -107,10 +107,20 @@ def check_builder(name, backend, window=32):
             assert abs(rel - erel) <= TOL
 
 
-def check_pipeline(name, backend):
+def _two_stand_in_contexts(model):
+    """CPU tier: give the pipeline a second (stand-in) context, so two batches are in
+    flight on two contexts as on the GPU (FrozenModel.contexts)."""
+    from cpu_backend import OracleBackedContext
+    extra = OracleBackedContext(model)
+    model.contexts = lambda n: [model.ctx, extra][:max(1, min(n, 2))]
+
+
+def check_pipeline(name, backend, two_contexts=False):
     """compute_relevance_pipeline (host schedules batch k+1 while batch k runs)
     over every recorded prediction equals the reference's sequential calls."""
     rec, ds, model = build_product(name, backend)
+    if two_contexts and backend == "cpu":
+        _two_stand_in_contexts(model)
     seed_all(rec["seed"])
     eng = ka.NecessaryPostTrainingEngine(model, ds, rec["hp"])
     batches = [[(tuple(b["pred"]), [[tuple(t) for t in c["rule"]] for c in b["calls"]])] for b in rec["necessary"]]
@@ -122,6 +132,8 @@ def check_pipeline(name, backend):
     if not rec.get("sufficient"):
         return
     rec, ds, model = build_product(name, backend)
+    if two_contexts and backend == "cpu":
+        _two_stand_in_contexts(model)
     seed_all(rec["seed"])
     eng = ka.SufficientPostTrainingEngine(model, ds, rec["hp"])
     batches = []

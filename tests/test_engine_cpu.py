@@ -36,5 +36,12 @@ def test_pipeline_host_protocol(name):
 
 
 @pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
+def test_pipeline_two_contexts(name):
+    """Two batches in flight on two contexts (batch b on context b mod 2) return the
+    reference's sequential results, in order."""
+    check_pipeline(name, "cpu", two_contexts=True)
+
+
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
 def test_explain_pipeline_and_output_json(name, tmp_path):
     check_pipeline_explain(name, "cpu", str(tmp_path))
