@@ -40,6 +40,13 @@
 #define KP_S_AHEAD 1
 #endif
 static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt holds at most 15)");
+// Diagnostic builds (timing only, wrong results): KP_DIAG_NO_S drops the S phase,
+// KP_DIAG_NO_O the O phase, to see how the phases add up per tile.
+#ifdef KP_DIAG_NO_O
+#define KP_DIAG_O false
+#else
+#define KP_DIAG_O true
+#endif
 static_assert(KP_O_AHEAD >= 1 && KP_O_AHEAD <= 2, "KP_O_AHEAD: 1..2 (lgkmcnt holds at most 15)");
 
 namespace kpattn {
@@ -317,6 +324,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           else
             load_tail();
         };
+#ifndef KP_DIAG_NO_S
 #pragma unroll
         for (int j = 0; j < SA && j <= LAST; ++j) load_step(j);
 #pragma unroll
@@ -350,6 +358,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             sc[u] = mfma3_k16(a, qt4, sc[u]);
           }
         }
+#endif
 #if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
         if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
 #endif
@@ -369,7 +378,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             oh[b][p] = lds_rd_tr<ASM>(ob + (uint32_t)(16 * ROW_B + p * PART_B + 32 * m));
           }
         };
-        if (WITH_O) {
+        if (WITH_O && KP_DIAG_O) {
 #pragma unroll
           for (int m = 0; m < OA && m < DB; ++m) load_o(m, m);
         }
@@ -409,7 +418,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           }
           l_run += lt;
         }
-        if (WITH_O) {
+        if (WITH_O && KP_DIAG_O) {
           // P pieces in the B layout: element j of lane group g = entity 4g + j (j < 4)
           // or 16 + 4g + j - 4
           bf16x8 pb[3];
@@ -449,6 +458,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
       if (MODE == ATT_BCE_O) break;
       float mq = fmaxf(m_seen, __shfl_xor(m_seen, 16, 64));
       mq = fmaxf(mq, __shfl_xor(mq, 32, 64));
+#if defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O)
+      break;
+#endif
       if (pass == 1 || !__syncthreads_or(mq > m_ref + kMargin)) break;
       m_ref = mq;
     }
