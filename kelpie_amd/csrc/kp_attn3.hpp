@@ -42,6 +42,14 @@
 static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt holds at most 15)");
 // Diagnostic builds (timing only, wrong results): KP_DIAG_NO_S drops the S phase,
 // KP_DIAG_NO_O the O phase, to see how the phases add up per tile.
+// KP_DMA_SPREAD: the next tile's LDS-DMA goes out one piece per O block instead of one
+// burst after the S phase, in the inline-asm read form (ASM) only: ComplEx D = 400
+// 1.795 -> 1.713 ms (necessary) and 0.512 -> 0.492 ms (sufficient) per launch.  With
+// the compiler-visible reads (ConvE D = 208) the spread form failed the GPU parity
+// tests; that path keeps the burst until the cause is found.
+#ifndef KP_DMA_SPREAD
+#define KP_DMA_SPREAD 1
+#endif
 #ifdef KP_DIAG_NO_O
 #define KP_DIAG_O false
 #else
@@ -207,6 +215,16 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)));
     }
   };
+  // the wave's k-th piece of a tile's DMA (pieces w, w + 4, ...), for spreading the
+  // copy over the O-phase MFMA stream (KP_DMA_SPREAD)
+  constexpr int NPW = (PIECES + 3) / 4;
+  constexpr bool SPREAD = KP_DMA_SPREAD && ASM && WITH_O && KP_DIAG_O;
+  auto issue_piece = [&](int tile, int buf, int k) {
+    const int p = 4 * k + w;
+    if (p < PIECES)
+      glds16(reinterpret_cast<const float*>(E3 + (size_t)(key_begin + tile * KT) * ROW_B + 16 * lane + 1024 * p),
+             __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)));
+  };
   const int QT = (nq + 63) / 64;
   // work segments: stream-K ranges (wk.ranges == 0) or XCD-grouped units (attn_plan_ranges)
   const long long total = (long long)QT * wk.ktq;
@@ -360,7 +378,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         }
 #endif
 #if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
-        if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
+        // one burst here, or (KP_DMA_SPREAD, with an O phase) one piece per O block below:
+        // a burst of ~19 LDS-DMA instructions per wave stalls the wave's issue behind the
+        // texture-address queue before its O MFMAs start
+        if (!SPREAD && t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
 #endif
         // O-phase operands: block m's six transposed reads (rows 4g.. and 16 + 4g.. of
         // each piece); lane c = 4 qq + pp reads row qq of the 4-row block, columns
@@ -432,6 +453,13 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           }
 #pragma unroll
           for (int m = 0; m < DB; ++m) {
+#if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
+            if (SPREAD && t + 1 < ntiles) {
+              if (m < NPW) issue_piece(t + 1, (t + 1) & 1, m);
+              if (m == DB - 1)
+                for (int k = DB; k < NPW; ++k) issue_piece(t + 1, (t + 1) & 1, k);
+            }
+#endif
             // block m's reads are complete once at most (issued after them) reads are pending
             if (m + OA < DB) {
               load_o(m + OA, (m + OA) % (OA + 1));
