@@ -38,7 +38,8 @@ from . import _lib
 
 
 def _get_state():
-    return torch.get_rng_state().numpy().copy()
+    # get_rng_state() returns a fresh copy of the generator state: its numpy view is ours
+    return torch.get_rng_state().numpy()
 
 
 def _set_state(st):
@@ -100,11 +101,11 @@ class ReferenceRNG:
 
     # ---------------------------------------------------------------- model construction
     def rand_init(self, D: int) -> np.ndarray:
-        return torch.rand(1, D).numpy()[0].astype(np.float32)
+        return torch.rand(1, D).numpy()[0]  # float32 already
 
     def xavier_row(self, d: int) -> np.ndarray:
         # xavier_normal_ on a (1, d) parameter: normal_(0, sqrt(2 / (d + 1)))
-        return torch.empty(1, d).normal_(0.0, math.sqrt(2.0 / float(d + 1))).numpy()[0].astype(np.float32)
+        return torch.empty(1, d).normal_(0.0, math.sqrt(2.0 / float(d + 1))).numpy()[0]  # float32 already
 
     def discard(self, n: int):
         if n <= 0:
