@@ -46,7 +46,7 @@ __device__ __forceinline__ float cx_q(const float* __restrict__ lhs, const float
 // before the barrier that hands the buffer to the readers.
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
 }
 
 // LDS reads issued through inline asm, so their placement is the source order:

@@ -63,6 +63,9 @@ __device__ __forceinline__ float noise_at(const int32_t* __restrict__ bits, long
 
 // image (BN1) -> conv 3x3 + bias -> BN2 -> ReLU -> flat (conve.py:134-146).
 // src[i] = (lhs, rel): lhs >= 0 a frozen entity row, lhs < 0 the kelpie row X[-lhs-1].
+// W2C > 0: the feature-map width H - 2 as a compile-time constant (d = 200: 8), so the
+// per-output index divisions become multiplies; 0: read from k.H
+template <int W2C>
 __global__ __launch_bounds__(256) void kp_cv_conv_fwd(int M, const int2* __restrict__ src,
                                                       const float* __restrict__ E, const float* __restrict__ X,
                                                       const float* __restrict__ R, CvConst k,
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(256) void kp_cv_conv_fwd(int M, const int2* __restr
     b2[tid] = bnb[1 + tid];
   }
   __syncthreads();
-  const int W2 = k.H - 2;
+  const int W2 = W2C > 0 ? W2C : k.H - 2;
   const int per_c = 38 * W2;
   for (int o = tid; o < k.hid; o += 256) {
     const int c = o / per_c, rem = o - c * per_c;
@@ -229,6 +232,15 @@ __global__ __launch_bounds__(256) void kp_cv_conv_bwd(int M, CvConst k, const fl
     dl[(size_t)i * k.dp + j] = acc * a1;
   }
 }
+
+// kp_cv_conv_fwd with the width specialised for d = 200 (H = 10)
+#define KP_CONV_FWD(grid, block, shm, stream, M, src, E, X, R, kk, ...)                                      \
+  do {                                                                                                      \
+    if ((kk).H == 10)                                                                                       \
+      hipLaunchKernelGGL(kp_cv_conv_fwd<8>, grid, block, shm, stream, M, src, E, X, R, kk, __VA_ARGS__);    \
+    else                                                                                                    \
+      hipLaunchKernelGGL(kp_cv_conv_fwd<0>, grid, block, shm, stream, M, src, E, X, R, kk, __VA_ARGS__);    \
+  } while (0)
 
 struct CvOpt {
   float lr, b1, b2, eps, one_minus_b1, one_minus_b2, step_size, bc2_sqrt;
@@ -377,7 +389,7 @@ void encode_eval(kp_ctx* c, int n, const int2* dsrc, const float* dX, float* dQ)
   CvConst k = make_const(c, nullptr);
   float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)n * c->hidden));
   float* dfc = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * (size_t)n * c->dim));
-  hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(n), dim3(256), 0, c->stream, n, dsrc, c->dE, dX, c->dR, k, c->d_conv_w,
+  KP_CONV_FWD(dim3(n), dim3(256), 0, c->stream, n, dsrc, c->dE, dX, c->dR, k, c->d_conv_w,
                      c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
   KP_HIP(hipGetLastError());
   launch_gemm_abt(c, dflat, c->hidden, n, c->d_fc_w, c->hidden, c->dim, c->hidden, dfc, c->dim, c->d_fc_b, 0, 1);
@@ -540,7 +552,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   if (nfp > 0) {
     int2* dFp = upload(c, c->ws[9], fpairs.data(), fpairs.size());
     float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)nfp * c->hidden));
-    hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(nfp), dim3(256), 0, c->stream, nfp, dFp, c->dE, dX, c->dR, kc,
+    KP_CONV_FWD(dim3(nfp), dim3(256), 0, c->stream, nfp, dFp, c->dE, dX, c->dR, kc,
                        c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
     KP_HIP(hipGetLastError());
     launch_gemm_abt(c, dflat, c->hidden, nfp, c->d_fc_w, c->hidden, c->dim, c->hidden, dFcf, c->dim, c->d_fc_b, 0, 1);
@@ -609,7 +621,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     const CvInst* KI = dKI + kin_off[t];
     if (nk > 0) {
       const int n_split = step_plan[t].wk.n_parts;
-      hipLaunchKernelGGL(kp_cv_conv_fwd, dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
+      KP_CONV_FWD(dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
                          kc, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
       KP_HIP(hipGetLastError());
       launch_gemm_abt(c, dflat, c->hidden, nk, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b, 0,
