@@ -560,7 +560,7 @@ int attn3_wpc(kp_ctx* c) {
 // Host: the partition of the context's attention kernel.  kp_attn3 takes the XCD-grouped
 // aligned ranges unless their quantisation costs more than a slack over stream-K's
 // balanced split.  The L2 reuse they buy (FETCH_SIZE 14x lower) was worth 2-7 % per
-// launch with the 35 MB FB15k-237 ComplEx image and 6 % with the 158 MB YAGO3-10 ConvE
+// launch with the 35 MB FB15k-237 ComplEx image and 6 % with the 154 MB YAGO3-10 ConvE
 // image, which stream-K re-reads through the Infinity Cache at worse hit rates: slack
 // 5 % up to 64 MB of image, 15 % above.  KP_ATTN_PART=streamk
 // forces stream-K.  The fp32 kp_attn always uses stream-K.
