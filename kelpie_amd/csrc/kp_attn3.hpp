@@ -218,7 +218,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   // the wave's k-th piece of a tile's DMA (pieces w, w + 4, ...), for spreading the
   // copy over the O-phase MFMA stream (KP_DMA_SPREAD)
   constexpr int NPW = (PIECES + 3) / 4;
+#ifdef KP_DMA_SPREAD_ALL
+  constexpr bool SPREAD = KP_DMA_SPREAD && WITH_O && KP_DIAG_O;  // diagnostic: every read form
+#else
   constexpr bool SPREAD = KP_DMA_SPREAD && ASM && WITH_O && KP_DIAG_O;
+#endif
   auto issue_piece = [&](int tile, int buf, int k) {
     const int p = 4 * k + w;
     if (p < PIECES)
