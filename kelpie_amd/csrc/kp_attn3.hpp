@@ -459,7 +459,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           for (int m = 0; m < DB; ++m) {
 #if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
             if (SPREAD && t + 1 < ntiles) {
-              if (m < NPW) issue_piece(t + 1, (t + 1) & 1, m);
+              if (m < NPW) {
+                issue_piece(t + 1, (t + 1) & 1, m);
+#ifdef KP_DIAG_DMA_LGKM0
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // diagnostic: drain after each piece
+#endif
+              }
               if (m == DB - 1)
                 for (int k = DB; k < NPW; ++k) issue_piece(t + 1, (t + 1) & 1, k);
             }
