@@ -399,6 +399,22 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   const int hpbs = hp->batch_size;
   KP_REQUIRE(hpbs > 0 && hp->epochs >= 0, "ComplEx: bad batch_size/epochs");
   const int E = hp->epochs;
+  // every id is checked before it indexes a host vector or a device table (as ConvE / TransE)
+  KP_REQUIRE(ns >= 0 && bt->row_off[0] == 0, "ComplEx: bad row_off");
+  for (int s = 0; s < ns; ++s) {
+    KP_REQUIRE(bt->row_off[s + 1] >= bt->row_off[s], "ComplEx: bad row_off");
+    KP_REQUIRE(bt->pred[3 * s] == K, "ComplEx: the ranked triple must start at the kelpie entity");
+    KP_REQUIRE(bt->pred[3 * s + 1] >= 0 && bt->pred[3 * s + 1] < c->n_rel2, "ComplEx: ranked relation out of range");
+    KP_REQUIRE(bt->pred[3 * s + 2] >= 0 && bt->pred[3 * s + 2] <= K, "ComplEx: ranked object out of range");
+    KP_REQUIRE(bt->filt_off[s + 1] >= bt->filt_off[s], "ComplEx: bad filt_off");
+  }
+  for (int64_t i = 0; i < (int64_t)bt->row_off[ns]; ++i) {
+    const int32_t* rw = bt->rows + 3 * i;
+    KP_REQUIRE(rw[0] >= 0 && rw[0] <= K && rw[2] >= 0 && rw[2] <= K && rw[1] >= 0 && rw[1] < c->n_rel2,
+               "ComplEx: row id out of range");
+  }
+  for (int64_t i = 0; i < (int64_t)bt->filt_off[ns]; ++i)
+    KP_REQUIRE(bt->filt[i] >= 0 && bt->filt[i] <= K, "ComplEx: filter id out of range");
 
   std::vector<CxPlan> plans;
   std::vector<CxQuery> pqs;
@@ -503,6 +519,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       KP_REQUIRE(g1 - g0 >= (int64_t)E * R, "ComplEx: missing randperm draws for a multi-step slot");
       for (int e = 0; e < E; ++e) {
         const int32_t* perm = bt->rng + g0 + (int64_t)e * R;
+        for (int j = 0; j < R; ++j) KP_REQUIRE(perm[j] >= 0 && perm[j] < R, "ComplEx: randperm value out of range");
         for (int j = 0; j < nst; ++j) {
           const int st = j * hpbs;
           const int n = std::min(bs, R - st);
@@ -625,9 +642,17 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   opt.one_minus_b1 = (float)(1.0 - (double)hp->beta1);
   opt.one_minus_b2 = (float)(1.0 - (double)hp->beta2);
   opt.reg_w = hp->reg_weight;
-  hipEvent_t h0, h1;
-  KP_HIP(hipEventCreate(&h0));
-  KP_HIP(hipEventCreate(&h1));
+  // loop-interval events, destroyed on every exit path (a KP_HIP / KP_REQUIRE below throws)
+  struct LoopEvents {
+    hipEvent_t a = nullptr, b = nullptr;
+    ~LoopEvents() {
+      if (a) (void)hipEventDestroy(a);
+      if (b) (void)hipEventDestroy(b);
+    }
+  } lev;
+  KP_HIP(hipEventCreate(&lev.a));
+  KP_HIP(hipEventCreate(&lev.b));
+  hipEvent_t h0 = lev.a, h1 = lev.b;
   KP_HIP(hipEventRecord(h0, c->stream));
   int64_t hot_launches = 0;
   c->hot_pairs.clear();
@@ -690,8 +715,6 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float ms_all = 0.f, ms_loop = 0.f;
   KP_HIP(hipEventElapsedTime(&ms_all, c->ev0, c->ev1));
   KP_HIP(hipEventElapsedTime(&ms_loop, h0, h1));
-  (void)hipEventDestroy(h0);
-  (void)hipEventDestroy(h1);
   double hot = 0.0;
   for (size_t i = 0; i < c->hot_pairs.size(); ++i) {
     float ms = 0.f;

@@ -684,6 +684,8 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   std::vector<int32_t> po(ns);
   for (int s = 0; s < ns; ++s) {
     KP_REQUIRE(bt->pred[3 * s] == K, "ConvE: the ranked triple must start at the kelpie entity");
+    KP_REQUIRE(bt->pred[3 * s + 1] >= 0 && bt->pred[3 * s + 1] < c->n_rel2, "ConvE: ranked relation out of range");
+    KP_REQUIRE(bt->pred[3 * s + 2] >= 0 && bt->pred[3 * s + 2] <= K, "ConvE: ranked object out of range");
     rsrc[s] = make_int2(-s - 1, bt->pred[3 * s + 1]);
     po[s] = bt->pred[3 * s + 2];
   }
