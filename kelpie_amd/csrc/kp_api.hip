@@ -76,7 +76,8 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     // the fp32-MFMA kernel of kp_attn.hpp
     c->attn_mode = 1;
     if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "f32") == 0 ? 0 : 1;
-    if (const char* a = std::getenv("KP_ATTN_PART")) c->attn_ranges = std::strcmp(a, "streamk") != 0;
+    if (const char* a = std::getenv("KP_ATTN_PART"))
+      c->attn_part = std::strcmp(a, "streamk") == 0 ? 1 : std::strcmp(a, "ranges") == 0 ? 2 : 0;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     KP_HIP(hipEventCreate(&c->ev0));
     KP_HIP(hipEventCreate(&c->ev1));

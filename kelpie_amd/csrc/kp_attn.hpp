@@ -2,6 +2,9 @@
 // shared by the ComplEx (softmax cross-entropy) and ConvE (sigmoid BCE)
 // post-training steps.
 #pragma once
+#if defined(KP_ATTN_NODMA) && !defined(KP_DIAGNOSTIC_BUILD)
+#error "KP_ATTN_NODMA is a timing-only diagnostic (wrong results): build it with make diag"
+#endif
 #include <algorithm>
 
 #include "kp_common.hpp"

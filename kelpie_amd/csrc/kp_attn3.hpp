@@ -41,7 +41,14 @@
 #endif
 static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt holds at most 15)");
 // Diagnostic builds (timing only, wrong results): KP_DIAG_NO_S drops the S phase,
-// KP_DIAG_NO_O the O phase, to see how the phases add up per tile.
+// KP_DIAG_NO_O the O phase, to see how the phases add up per tile.  They (and
+// KP_ATTN_NODMA, KP_DIAG_DMA_LGKM0, KP_DMA_SPREAD_ALL) compile only together with
+// KP_DIAGNOSTIC_BUILD, which `make diag` sets for the variants/ libraries; the product
+// library can never carry one by a stray define.
+#if (defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O) || defined(KP_ATTN_NODMA) || defined(KP_DIAG_DMA_LGKM0) || \
+     defined(KP_DMA_SPREAD_ALL)) && !defined(KP_DIAGNOSTIC_BUILD)
+#error "kp_attn3 diagnostic define without KP_DIAGNOSTIC_BUILD (these builds compute wrong results: make diag)"
+#endif
 // KP_DMA_SPREAD: the next tile's LDS-DMA goes out one piece per O block instead of one
 // burst after the S phase, in the inline-asm read form (ASM) only: ComplEx D = 400
 // 1.795 -> 1.713 ms (necessary) and 0.512 -> 0.492 ms (sufficient) per launch.  With
@@ -58,6 +65,8 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 static_assert(KP_O_AHEAD >= 1 && KP_O_AHEAD <= 2, "KP_O_AHEAD: 1..2 (lgkmcnt holds at most 15)");
 
 namespace kpattn {
+
+constexpr float kPosInf = __builtin_huge_valf();
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                                                    const float* __restrict__ Qpre, int nq, AttnWork wk,
                                                    float* __restrict__ out_m, float* __restrict__ out_l,
                                                    float* __restrict__ out_O, const float* __restrict__ qscale,
-                                                   float ylo) {
+                                                   float ylo, const double* __restrict__ colpre) {
   constexpr bool WITH_O = MODE != ATT_SOFTMAX;
   constexpr int DP = 16 * DB;
   constexpr bool ASM = DB > 13;  // read form (see lds_rd_bf8)
@@ -298,6 +307,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
     }
     f32x4 O[WITH_O ? DB : 1];
     float m_ref = kNegInf, l_run = 0.f;
+    float csh = 0.f;  // the query's weight shift of this pass (centred accumulation, above)
 
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
@@ -434,11 +444,31 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             float mq = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
             m_ref = fmaxf(mq, __shfl_xor(mq, 32, 64));
           }
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pw[u][r] = __expf(v[u][r] - m_ref);
+        }
+        // centred accumulation: the first tile of a pass fixes the query's shift (the
+        // smallest valid weight of that tile); every valid weight is accumulated minus it
+        {
+          if (t == 0) {
+            float mn = kPosInf;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (k0 + 16 * u + 4 * g + r < key_end) mn = fminf(mn, pw[u][r]);
+            mn = fminf(mn, __shfl_xor(mn, 16, 64));
+            mn = fminf(mn, __shfl_xor(mn, 32, 64));
+            csh = (mn < kPosInf) ? mn : 0.f;
+          }
           float lt = 0.f;
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pw[u][r] = __expf(v[u][r] - m_ref);
+            for (int r = 0; r < 4; ++r)
+              pw[u][r] = (k0 + 16 * u + 4 * g + r < key_end) ? __fsub_rn(pw[u][r], csh) : 0.f;
             lt += (pw[u][0] + pw[u][1]) + (pw[u][2] + pw[u][3]);
           }
           l_run += lt;
@@ -504,6 +534,25 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 
     float l_tot = l_run + __shfl_xor(l_run, 16, 64);
     l_tot += __shfl_xor(l_tot, 32, 64);
+    if (ntiles > 0) {
+      // the shifted-out part: csh * (number of keys) and csh * (sum of the keys' rows),
+      // the latter from the fp64 prefix sums of the table over tiles
+      l_tot = __fmaf_rn(csh, (float)(key_end - key_begin), l_tot);
+      if (WITH_O) {
+        const double* p0 = colpre + (size_t)kt0 * DP;
+        const double* p1 = colpre + (size_t)kt1 * DP;
+#pragma unroll
+        for (int m = 0; m < DB; ++m) {
+          const int d = 16 * m + 4 * g;  // 32-byte aligned quad of dims
+          const double2 a0 = *reinterpret_cast<const double2*>(p0 + d), a1 = *reinterpret_cast<const double2*>(p0 + d + 2);
+          const double2 b0 = *reinterpret_cast<const double2*>(p1 + d), b1 = *reinterpret_cast<const double2*>(p1 + d + 2);
+          O[m][0] = __fmaf_rn(csh, (float)(b0.x - a0.x), O[m][0]);
+          O[m][1] = __fmaf_rn(csh, (float)(b0.y - a0.y), O[m][1]);
+          O[m][2] = __fmaf_rn(csh, (float)(b1.x - a1.x), O[m][2]);
+          O[m][3] = __fmaf_rn(csh, (float)(b1.y - a1.y), O[m][3]);
+        }
+      }
+    }
     if (valid) {
       const size_t o = (size_t)part * nq + q;
       if (g == 0 && MODE != ATT_BCE_O) {
@@ -553,6 +602,46 @@ const uint8_t* split3_image(kp_ctx* c) {
   return c->e3.as<uint8_t>();
 }
 
+// Prefix sums of the fp32 table over 32-entity tiles, in fp64: colpre[t][d] = sum of
+// E[e][d] over e < min(32 t, n_ent).  Tile sums first (one thread per (tile, dim)), then
+// one thread per dim scans the tiles.
+template <int DP>
+__global__ void kp_tile_sums(const float* __restrict__ E, int n_ent, double* __restrict__ ts) {
+  const int t = blockIdx.x, d = threadIdx.x;
+  if (d >= DP) return;
+  double s = 0.0;
+  const int e1 = min(n_ent, 32 * t + 32);
+  for (int e = 32 * t; e < e1; ++e) s += (double)E[(size_t)e * DP + d];
+  ts[(size_t)t * DP + d] = s;
+}
+template <int DP>
+__global__ void kp_tile_prefix(const double* __restrict__ ts, int ntiles, double* __restrict__ pre) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= DP) return;
+  double s = 0.0;
+  pre[d] = 0.0;
+  for (int t = 0; t < ntiles; ++t) {
+    s += ts[(size_t)t * DP + d];
+    pre[(size_t)(t + 1) * DP + d] = s;
+  }
+}
+template <int DB>
+const double* tile_prefix(kp_ctx* c) {
+  constexpr int DP = 16 * DB;
+  if (!c->e3pre_ready) {
+    const int ntiles = (c->n_ent + 31) / 32;
+    double* ts = reinterpret_cast<double*>(c->e3ts.ensure(sizeof(double) * (size_t)ntiles * DP));
+    double* pre = reinterpret_cast<double*>(c->e3pre.ensure(sizeof(double) * (size_t)(ntiles + 1) * DP));
+    hipLaunchKernelGGL((kp_tile_sums<DP>), dim3((unsigned)ntiles), dim3((DP + 63) / 64 * 64), 0, c->stream, c->dE,
+                       c->n_ent, ts);
+    KP_HIP(hipGetLastError());
+    hipLaunchKernelGGL((kp_tile_prefix<DP>), dim3((DP + 63) / 64), dim3(64), 0, c->stream, ts, ntiles, pre);
+    KP_HIP(hipGetLastError());
+    c->e3pre_ready = true;
+  }
+  return c->e3pre.as<double>();
+}
+
 // Host: co-resident kp_attn3 workgroups per CU (registers and LDS), cached per context.
 template <int DB>
 int attn3_wpc(kp_ctx* c) {
@@ -572,11 +661,13 @@ int attn3_wpc(kp_ctx* c) {
 // launch with the 35 MB FB15k-237 ComplEx image and 6 % with the 154 MB YAGO3-10 ConvE
 // image, which stream-K re-reads through the Infinity Cache at worse hit rates: slack
 // 5 % up to 64 MB of image, 15 % above.  KP_ATTN_PART=streamk
-// forces stream-K.  The fp32 kp_attn always uses stream-K.
+// forces stream-K, KP_ATTN_PART=ranges the ranges (parity tests run both).  The fp32
+// kp_attn always uses stream-K.
 inline AttnPlan attn_plan_ctx(const kp_ctx* c, int nq, int n_ent, int slots) {
   const AttnPlan sk = attn_plan(nq, n_ent, slots);
-  if (c->attn_mode != 1 || !c->attn_ranges) return sk;
+  if (c->attn_mode != 1 || c->attn_part == 1) return sk;
   const AttnPlan r = attn_plan_ranges(nq, n_ent, slots);
+  if (c->attn_part == 2) return r;
   const long long QT = (nq + 63) / 64, S = r.wk.ranges, ktq = r.wk.ktq;
   const long long n_wg = std::max(8, slots / 8 * 8);
   const long long cost_r = (QT * S + n_wg - 1) / n_wg * ((ktq + S - 1) / S + 2);
@@ -590,8 +681,10 @@ template <int DB, int MODE>
 void launch_attn3(kp_ctx* c, int n_ent, const float* Q, int nq, const AttnPlan& plan, float* m, float* l, float* O,
                   const float* qscale, float ylo) {
   const uint8_t* E3 = split3_image<DB>(c);
+  KP_REQUIRE(n_ent == c->n_ent, "attn3: key count differs from the table's (tile prefix sums)");
+  const double* pre = tile_prefix<DB>(c);
   hipLaunchKernelGGL((kp_attn3<DB, MODE>), dim3(plan.n_wg), dim3(256), attn3_lds_bytes(DB), c->stream, E3, n_ent, Q,
-                     nq, plan.wk, m, l, O, qscale, ylo);
+                     nq, plan.wk, m, l, O, qscale, ylo, pre);
   KP_HIP(hipGetLastError());
 }
 

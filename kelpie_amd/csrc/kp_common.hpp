@@ -93,9 +93,11 @@ struct kp_ctx {
   bool time_hot = true;
   // attention contraction: 0 = fp32 MFMA (kp_attn.hpp), 1 = bf16x3 MFMA (kp_attn3.hpp)
   int attn_mode = 0;
-  bool attn_ranges = true;  // kp_attn3 partition: XCD-grouped ranges (false: stream-K)
+  int attn_part = 0;  // kp_attn3 partition: 0 chosen per launch, 1 stream-K, 2 XCD-grouped ranges (KP_ATTN_PART)
   DevBuf e3;               // kp_attn3's split image of dE, built on first use
   bool e3_ready = false;
+  DevBuf e3ts, e3pre;      // kp_attn3's fp64 tile sums / prefix sums of dE over tiles
+  bool e3pre_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<double, double>> hot_pairs;  // (work units, seconds) per hot launch

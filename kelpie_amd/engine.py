@@ -99,7 +99,9 @@ class RelevanceEngine:
                     continue
             ents.append(e)
         if not ents:
-            self.entities_to_convert = []
+            # the reference returns here WITHOUT resetting entities_to_convert
+            # (engine.py:90-91): a sufficient pipeline then reuses the previous
+            # prediction's conversion entities
             return []
         fo, fl = [0], []
         for e in ents:

@@ -6,7 +6,11 @@ For three golden cases, on a low-degree subject:
     entity post-trains on zero rows);
   * necessary, an empty rule (the reference raises "No removal to undo." from
     KelpieDataset.undo_removal after the post-training);
-  * a regular call afterwards (checks the random stream stays in sync after both).
+  * a regular call afterwards (checks the random stream stays in sync after both);
+  * sufficient mode, "stale conversion entities": select_entities_to_convert on
+    prediction A, then on prediction B with a degree cap no entity meets; the
+    reference returns [] WITHOUT resetting ``entities_to_convert``
+    (engine.py:90-91), so B's relevance is computed on A's entities.
 
     python tests/golden/make_edge_golden.py
 """
@@ -32,6 +36,7 @@ def main():
 
     out = {}
     for name in EDGE_CASES:
+        out.setdefault("_stale_entities", {})[name] = stale_entities(src, name)
         g, _, dataset, model = build_case(src, name, CASES[name])
         ref_harness.seed_all(42)
         eng = NecessaryPostTrainingEngine(model, dataset, CASES[name]["hp"])
@@ -53,6 +58,28 @@ def main():
         print(name, rec["calls"], flush=True)
     with open(os.path.join(HERE, "edge_golden.json"), "w") as f:
         json.dump(out, f)
+
+
+def stale_entities(src, name):
+    from src.relevance_engines import SufficientPostTrainingEngine
+    g, _, dataset, model = build_case(src, name, CASES[name])
+    ref_harness.seed_all(42)
+    eng = SufficientPostTrainingEngine(model, dataset, CASES[name]["hp"])
+    eng.set_cache()
+    deg = dataset.entity_to_degree
+    test = [tuple(int(v) for v in t) for t in g.test if 3 <= deg.get(int(t[0]), 0) <= 20]
+    pa, pb = test[0], next(t for t in test[1:] if t[0] != test[0][0])
+    ret_a = eng.select_entities_to_convert(pa, 3, 200)
+    ents_a = [int(e) for e in eng.entities_to_convert]
+    ret_b = eng.select_entities_to_convert(pb, 3, 0.5)  # truthy cap below every degree: no candidate
+    ents_b = [int(e) for e in eng.entities_to_convert]
+    rule = [tuple(int(v) for v in dataset.entity_to_training_triples[pb[0]][0])]
+    rel = float(eng.compute_relevance(pb, rule))
+    rec = {"pred_a": list(pa), "pred_b": list(pb), "entities_a": ents_a, "returned_b": ret_b,
+           "entities_after_b": ents_b, "returned_a_is_none": ret_a is None, "rule": [list(t) for t in rule],
+           "relevance": rel}
+    print(name, "stale entities", rec, flush=True)
+    return rec
 
 
 if __name__ == "__main__":

@@ -55,15 +55,22 @@ HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 20, "lr": 0.043,
       "regularizer_name": "N3", "regularizer_weight": 0}
 
 
-@pytest.mark.parametrize("dim,hot", [(200, False), (8, False), (200, True)])
-def test_complex_vs_oracle_full_width(dim, hot):
+PARTS = ["streamk", "ranges"]
+
+
+@pytest.mark.parametrize("dim,hot,part", [(200, False, "streamk"), (200, False, "ranges"), (8, False, "auto"),
+                                          (200, True, "streamk"), (200, True, "ranges")])
+def test_complex_vs_oracle_full_width(dim, hot, part, monkeypatch):
     """D = 400 (the production kernel instantiation) and D = 16 on a 2,000-entity
     graph, including a hub subject with more rows than one minibatch.
 
     ``hot``: the last entity row is scaled so that its scores exceed every split's
     first-tile maximum by far more than kpattn::kMargin, which exercises the
-    attention kernel's exact-max second pass (step and frozen-pair queries)."""
+    attention kernel's exact-max second pass (step and frozen-pair queries).
+    ``part``: the attention's work partition, forced (KP_ATTN_PART): stream-K or the
+    XCD-grouped key ranges (multi-tile ranges of the 63 key tiles)."""
     from cpu_backend import OracleBackedContext
+    monkeypatch.setenv("KP_ATTN_PART", part)
     g, ds, w = _small_complex(dim=dim)
     init_scale = 1e-3
     if hot:
@@ -137,10 +144,12 @@ def test_transe_vs_oracle_full_width(dim):
 CV_HP = {"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.995, "epochs": 25}
 
 
-@pytest.mark.parametrize("dim,p_drop", [(200, 0.2), (60, 0.0)])
-def test_conve_vs_oracle_full_width(dim, p_drop):
-    """d = 200 (the production 20x10 image, FC 9728 -> 200) on a 2,000-entity graph."""
+@pytest.mark.parametrize("dim,p_drop,part", [(200, 0.2, "streamk"), (200, 0.2, "ranges"), (60, 0.0, "auto")])
+def test_conve_vs_oracle_full_width(dim, p_drop, part, monkeypatch):
+    """d = 200 (the production 20x10 image, FC 9728 -> 200) on a 2,000-entity graph,
+    with the attention partition forced (KP_ATTN_PART)."""
     from cpu_backend import OracleBackedContext
+    monkeypatch.setenv("KP_ATTN_PART", part)
     from kelpie_amd import synth
     g = synth.make_graph("small", seed=9)
     ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
@@ -243,10 +252,13 @@ DB_HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 83, "lr": 0.0
          "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0}  # ComplEx_DB100K_explanation.json
 
 
-def test_complex_db100k_necessary_vs_oracle(db100k):
+@pytest.mark.parametrize("part", PARTS)
+def test_complex_db100k_necessary_vs_oracle(db100k, part, monkeypatch):
     """ComplEx at the DB100K size (N = 99,605 rows in the rank, 83 Adagrad epochs) against
-    the oracle, on weights with a trained-like spread (ranks exact, scores within 1e-4)."""
+    the oracle, on weights with a trained-like spread (ranks exact, scores within 1e-4),
+    both attention partitions forced (multi-tile stream-K segments at this size)."""
     from cpu_backend import OracleBackedContext
+    monkeypatch.setenv("KP_ATTN_PART", part)
     from kelpie_amd import synth
     g, ds = db100k
     w = synth.make_weights("ComplEx", g.num_entities, g.num_relations, 200, seed=4, trained_scale=0.3)
@@ -339,3 +351,78 @@ def test_attention_contractions_agree(model_name, monkeypatch):
         assert abs(a[1] - b[1]) <= 1e-5 * max(1e-3, abs(b[1])), (a, b)
         assert abs(a[3] - b[3]) <= 1e-5 * max(1e-3, abs(b[3])), (a, b)
         assert a[0] == b[0] and a[2] == b[2], (a, b)
+
+
+@pytest.mark.parametrize("part", PARTS)
+def test_complex_sufficient_vs_oracle_full_width(part, monkeypatch):
+    """Sufficient mode at the production width (D = 400): every conversion entity's base
+    and pt post-training against the oracle (ranks exact, scores within 1e-4 relative),
+    relevances within 1e-4, for both attention partitions."""
+    from cpu_backend import OracleBackedContext
+    monkeypatch.setenv("KP_ATTN_PART", part)
+    g, ds, w = _small_complex(dim=200)
+    deg = ds.entity_to_degree
+    pred = next(tuple(int(v) for v in t) for t in g.test if 8 <= deg.get(int(t[0]), 0) <= 40)
+    cands = sorted(ds.entity_to_training_triples[pred[0]])[:3]
+    out = {}
+    for backend in ("gpu", "cpu"):
+        model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"], init_scale=1e-3)
+        if backend == "cpu":
+            model._ctx = OracleBackedContext(model)
+        seed_all(42)
+        eng = ka.SufficientPostTrainingEngine(model, ds, HP)
+        ents = eng.select_entities_to_convert(pred, 6, 200)
+        assert len(ents) == 6
+        rels = eng.compute_relevance_batch(pred, [[c] for c in cands])
+        det = [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+               for rj in eng.last_results for pt, b in rj]
+        out[backend] = (ents, rels, det)
+    assert out["gpu"][0] == out["cpu"][0]
+    assert len(out["gpu"][2]) == 6 * len(cands)
+    for a, b in zip(out["gpu"][2], out["cpu"][2]):
+        assert a[0] == b[0] and a[2] == b[2], (a, b)
+        assert abs(a[1] - b[1]) <= 1e-4 * max(1e-6, abs(b[1])) and abs(a[3] - b[3]) <= 1e-4 * max(1e-6, abs(b[3]))
+    assert np.allclose(out["gpu"][1], out["cpu"][1], rtol=0, atol=1e-4)
+
+
+@pytest.fixture(scope="module")
+def yago():
+    """BASELINE.json configs[4] shape: 123,182 entities, 37 relations, 1.08 M train triples."""
+    from kelpie_amd import synth
+    g = synth.make_graph("YAGO3-10", seed=0)
+    ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    return g, ds
+
+
+@pytest.mark.parametrize("part", PARTS)
+def test_conve_yago_shape_vs_oracle(yago, part, monkeypatch):
+    """ConvE at the YAGO3-10 size (123,183 ranked rows, a 154 MB split image: the size at
+    which the chooser takes the XCD-grouped ranges) against the oracle, both partitions
+    forced, hidden dropout 0.2, on weights with a trained-like spread."""
+    from cpu_backend import OracleBackedContext
+    from kelpie_amd import synth
+    monkeypatch.setenv("KP_ATTN_PART", part)
+    g, ds = yago
+    w = synth.make_weights("ConvE", g.num_entities, g.num_relations, 200, seed=9, conve_random_bn=True,
+                           trained_scale=0.5)
+    bn = {i: {"weight": w[f"bn{i}_weight"], "bias": w[f"bn{i}_bias"], "running_mean": w[f"bn{i}_mean"],
+              "running_var": w[f"bn{i}_var"]} for i in (1, 2, 3)}
+    pred = next(tuple(int(v) for v in t) for t in g.test if 10 <= ds.entity_to_degree.get(int(t[0]), 0) <= 25)
+    cands = sorted(ds.entity_to_training_triples[pred[0]])[:2]
+    hp = dict(CV_HP, epochs=12)
+    out = {}
+    for backend in ("gpu", "cpu"):
+        model = ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
+                         w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn, hidden_dropout_rate=0.2)
+        if backend == "cpu":
+            model._ctx = OracleBackedContext(model)
+        seed_all(42)
+        eng = ka.NecessaryPostTrainingEngine(model, ds, hp)
+        rels = eng.compute_relevance_batch(pred, [[c] for c in cands])
+        out[backend] = (rels, [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+                               for pt, b in eng.last_results])
+        model.close() if hasattr(model, "close") else None
+    for a, b in zip(out["gpu"][1], out["cpu"][1]):
+        assert a[0] == b[0] and a[2] == b[2], (a, b)
+        assert abs(a[1] - b[1]) <= 1e-4 * abs(b[1]) and abs(a[3] - b[3]) <= 1e-4 * abs(b[3]), (a, b)
+    assert np.allclose(out["gpu"][0], out["cpu"][0], rtol=0, atol=1e-4)

@@ -1,6 +1,6 @@
 """Run the HIP engine on the sample of a reference noise-floor record (GPU box).
 
-    python tools/gpu_sample.py profiles/noise_floor_<workload>.json
+    python tools/gpu_sample.py profiles/noise_floor_<workload>.json [run-name]
 
 Reads the prediction, candidates and conversion entities that
 ``tools/noise_floor.py`` ran through the reference (development container),
@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def main(path):
+def main(path, name="gpu"):
     with open(path) as f:
         rec = json.load(f)
     wl = bench.WORKLOADS[rec["workload"]]
@@ -40,19 +40,20 @@ def main(path):
     rels = eng.compute_relevance_batch(pred, [[c] for c in cands])
     pairs = [pb for rj in eng.last_results for pb in rj] if wl["mode"] == "sufficient" else eng.last_results
     deltas = [pt["target_rank"] - b["target_rank"] for pt, b in pairs]
-    rec["runs"]["gpu"] = {"relevances": [float(r) for r in rels], "rank_deltas": deltas,
+    rec["runs"][name] = {"relevances": [float(r) for r in rels], "rank_deltas": deltas,
                           "results": [{"pt": pt, "base": b} for pt, b in pairs]}
-    for name, run in rec["runs"].items():
-        if name == "gpu":
+    for other, run in rec["runs"].items():
+        if other == name:
             continue
         d = run["rank_deltas"]
-        rec["rank_delta_match_rates"][f"gpu vs {name}"] = float(np.mean([a == b for a, b in zip(deltas, d)]))
-        rec.setdefault("rank_delta_max_abs_diff", {})[f"gpu vs {name}"] = int(
+        rec["rank_delta_match_rates"][f"{name} vs {other}"] = float(np.mean([a == b for a, b in zip(deltas, d)]))
+        rec.setdefault("rank_delta_max_abs_diff", {})[f"{name} vs {other}"] = int(
             max(abs(a - b) for a, b in zip(deltas, d)))
-    print(json.dumps({"gpu": rec["runs"]["gpu"]["rank_deltas"], "rates": rec["rank_delta_match_rates"]}))
+    print(json.dumps({name: rec["runs"][name]["rank_deltas"], "rates": rec["rank_delta_match_rates"],
+                      "scores": [(pt["target_score"], b["target_score"]) for pt, b in pairs]}))
     with open(path, "w") as f:
         json.dump(rec, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *sys.argv[2:3])
