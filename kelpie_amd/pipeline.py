@@ -92,3 +92,57 @@ def explain_preds(pipeline, dataset, preds, prefilter_k, skip=-1, output_path=No
         if output_path is not None:
             write_explanations(output_path, explanations)
     return explanations
+
+
+def reference_construction_draws(model_name, num_entities, num_relations, model_params):
+    """Consume the process-global torch CPU generator exactly as the reference's
+    ``model_class(dataset=..., hp=..., init_random=True)`` does in explain.py:171-172,
+    before ``load_state_dict`` overwrites the tables (the reference run on CPU: ``.cuda()``
+    copies, so the xavier draws come from the CPU generator as well):
+
+    * TransE (transe.py:27-32): ``torch.rand(|E|, d)``, ``torch.rand(2|R|, d)``, then
+      ``xavier_normal_`` on both;
+    * ComplEx (complex.py:27-31): ``torch.rand(|E|, 2d)``, ``torch.rand(2|R|, 2d)``;
+    * ConvE (conve.py:44-61): the ``Conv2d(1, 32, 3x3)`` and ``Linear(hidden, d)``
+      ``reset_parameters`` draws, then as TransE.
+
+    The values are discarded; only the generator state matters (every later draw of the
+    run -- kelpie inits, permutations, negatives, dropout masks -- follows it)."""
+    import torch
+    n_rel2 = 2 * int(num_relations)
+    if model_name == "ComplEx":
+        d = 2 * int(model_params["dimension"])
+        torch.rand(int(num_entities), d)
+        torch.rand(n_rel2, d)
+        return
+    d = int(model_params["dimension"])
+    if model_name == "ConvE":
+        torch.nn.Conv2d(1, 32, (3, 3), 1, 0, bias=True)
+        torch.nn.Linear(int(model_params["hidden_layer_size"]), d)
+    elif model_name != "TransE":
+        raise ValueError(model_name)
+    e = torch.rand(int(num_entities), d)
+    r = torch.rand(n_rel2, d)
+    torch.nn.init.xavier_normal_(e)
+    torch.nn.init.xavier_normal_(r)
+
+
+def run_explain(model_name, dataset, state, model_params, hp, mode, preds, prefilter=None, prefilter_k=20,
+                xsi=None, skip=-1, output_path=None, device=0):
+    """explain.py main() (explain.py:143-203) without the CLI: seeds 42 (explain.py:144),
+    the reference model construction's random draws (:171-172), the checkpoint state dict
+    (``torch.load(path, weights_only=True)``, :174) as a frozen model on the MI355X, the
+    pipeline (:177-186) and the loop over ``preds`` writing ``output.json``."""
+    import random
+
+    import numpy as np
+    import torch
+
+    from .models import from_state_dict
+    random.seed(42)
+    np.random.seed(42)
+    torch.manual_seed(42)
+    reference_construction_draws(model_name, dataset.num_entities, dataset.num_relations, model_params)
+    model = from_state_dict(model_name, dataset, state, model_params, device=device)
+    pipe = build_pipeline(model, dataset, hp, mode, prefilter=prefilter, xsi=xsi)
+    return explain_preds(pipe, dataset, preds, prefilter_k=prefilter_k, skip=skip, output_path=output_path)

@@ -42,11 +42,11 @@ class _Split:
 
 
 class _MemDataset:
-    def __init__(self, n_ent, n_rel, train, valid, test):
+    def __init__(self, n_ent, n_rel, train, valid, test, entity_to_id=None, relation_to_id=None):
         self.num_entities = int(n_ent)
         self.num_relations = int(n_rel)
-        self.entity_to_id = {f"e{i:06d}": i for i in range(n_ent)}
-        self.relation_to_id = {f"r{i:04d}": i for i in range(n_rel)}
+        self.entity_to_id = entity_to_id or {f"e{i:06d}": i for i in range(n_ent)}
+        self.relation_to_id = relation_to_id or {f"r{i:04d}": i for i in range(n_rel)}
         self.training = _Split(train)
         self.validation = _Split(valid)
         self.testing = _Split(test)
@@ -55,8 +55,8 @@ class _MemDataset:
 _REGISTRY: dict[str, _MemDataset] = {}
 
 
-def register_dataset(name, n_ent, n_rel, train, valid, test):
-    _REGISTRY[name] = _MemDataset(n_ent, n_rel, train, valid, test)
+def register_dataset(name, n_ent, n_rel, train, valid, test, entity_to_id=None, relation_to_id=None):
+    _REGISTRY[name] = _MemDataset(n_ent, n_rel, train, valid, test, entity_to_id, relation_to_id)
 
 
 def _get_dataset(dataset=None, **kwargs):

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny", "conve60_tiny", "conve_tiny"]
 
 
-@pytest.mark.parametrize("name", GPU_CASES)
+@pytest.mark.parametrize("name", GPU_CASES + ["complex200_small", "transe200_small"])
 @pytest.mark.parametrize("batched", [False, True])
 def test_necessary_vs_reference_goldens(name, batched):
     check_necessary(name, "gpu", batched)

@@ -42,7 +42,10 @@ def test_oracle_necessary(name):
     rec, ds, model = _setup(name)
     seed_all(rec["seed"])
     eng = ko.OracleEngine(model, ds, rec["hp"])
-    for block in rec["necessary"]:
+    # the d = 200 cases: the first (moderate-degree) prediction only on the CPU; the hub
+    # prediction after it is checked against the same goldens by the GPU tests
+    blocks = rec["necessary"][:1] if name.endswith("_small") else rec["necessary"]
+    for block in blocks:
         eng.set_cache()
         pred = tuple(block["pred"])
         for ci, call in enumerate(block["calls"]):

@@ -160,18 +160,38 @@ def main():
     ap.add_argument("--workload", default="complex-db100k-necessary", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--variants", nargs="+", default=["fp32", "fp32_perm", "fp64"])
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--fixture-only", action="store_true", help="rewrite the fixture from the profiles record")
     args = ap.parse_args()
+    if args.fixture_only:
+        with open(os.path.join(ROOT, "profiles", f"conditioning_{args.workload}.json")) as f:
+            write_fixture(json.load(f))
+        return
     torch.set_num_threads(args.threads)
     wl = bench.WORKLOADS[args.workload]
     src = ref_harness.load_reference()
     nf_path = os.path.join(ROOT, "profiles", f"noise_floor_{args.workload}.json")
-    with open(nf_path) as f:
-        nf = json.load(f)  # the sample (pred, candidates, conversion entities) and its GPU run
+    g = synth.make_graph(wl["shape"], seed=0)
+    w0 = synth.make_weights(wl["model"], g.num_entities, g.num_relations, wl["dim"], seed=0)
+    if os.path.exists(nf_path):
+        with open(nf_path) as f:
+            nf = json.load(f)  # the sample (pred, candidates, conversion entities) and its GPU run
+    else:
+        # the same sample noise_floor.py takes: the bench's first prediction, its first candidates
+        from kelpie_amd import Dataset
+        ds = Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test, name=wl["shape"])
+        p0 = bench.pick_preds(ds, 1, seed=1234)[0]
+        nf = {"pred": list(p0), "candidates": [list(c) for c in bench.candidates_of(ds, p0, wl["candidates"])[:3]],
+              "entities_to_convert": None, "runs": {}}
+        if wl["mode"] == "sufficient":
+            from src.relevance_engines import SufficientPostTrainingEngine
+            dataset, model = noise_floor.reference_model(src, wl, g, w0)
+            ref_harness.seed_all(42)
+            se = SufficientPostTrainingEngine(model, dataset, wl["hp"])
+            se.select_entities_to_convert(tuple(p0), wl["convert"], 200)  # engine.py:125
+            nf["entities_to_convert"] = [int(e) for e in se.entities_to_convert]
     pred = tuple(nf["pred"])
     cands = [tuple(c) for c in nf["candidates"]]
     ents = nf.get("entities_to_convert")
-    g = synth.make_graph(wl["shape"], seed=0)
-    w0 = synth.make_weights(wl["model"], g.num_entities, g.num_relations, wl["dim"], seed=0)
     D = wl["dim"] * (2 if wl["model"] == "ComplEx" else 1)
     out_path = os.path.join(ROOT, "profiles", f"conditioning_{args.workload}.json")
     out = {"workload": args.workload, "pred": list(pred), "candidates": [list(c) for c in cands],
@@ -180,7 +200,7 @@ def main():
         with open(out_path) as f:
             out["runs"] = json.load(f).get("runs", {})
     for v in args.variants:
-        if v in out["runs"]:
+        if v in out["runs"] or (v == "fp32_perm" and wl["model"] == "TransE"):
             continue
         w, cols = (permuted_weights(wl, w0) if v == "fp32_perm" else (w0, None))
         dataset, model = noise_floor.reference_model(src, wl, g, w)
@@ -190,7 +210,8 @@ def main():
             t0 = time.time()
             rels, log = noise_floor.run_reference(src, wl, dataset, model, pred, cands, ents)
         deltas = noise_floor.deltas_of(log, wl["mode"])
-        out["runs"][v] = {"relevances": rels, "results": log, "rank_deltas": deltas, "seconds": time.time() - t0}
+        out["runs"][v] = {"relevances": rels, "results": log, "rank_deltas": deltas, "seconds": time.time() - t0,
+                          "cand_seconds": noise_floor.run_reference.cand_seconds}
         print(f"{v}: rels {rels} deltas {deltas} ({time.time() - t0:.0f}s)", flush=True)
         with open(out_path, "w") as f:
             json.dump(out, f, indent=1)
@@ -207,6 +228,25 @@ def main():
     print(json.dumps(diffs, indent=1))
     with open(out_path, "w") as f:
         json.dump(out, f, indent=1)
+    write_fixture(out)
+
+
+def write_fixture(rec):
+    """tests/golden/fullsize/<workload>.json: the sample and the reference runs on it (data
+    only), read by the full-size GPU parity test and by bench.py's match rate."""
+    fx = {k: rec[k] for k in ("workload", "pred", "candidates", "entities_to_convert", "threads")}
+    fx["generator"] = "tools/conditioning.py (reference imported through tests/golden/ref_harness.py, CPU)"
+    fx["runs"] = {}
+    for name, run in rec["runs"].items():
+        if name.startswith("gpu"):
+            continue
+        res = [[{"rank": r["target_rank"], "score": r["target_score"]} for r in call] for call in run["results"]]
+        fx["runs"][name] = {"relevances": run["relevances"], "rank_deltas": run["rank_deltas"], "results": res,
+                            "seconds": run.get("seconds"), "cand_seconds": run.get("cand_seconds")}
+    d = os.path.join(ROOT, "tests", "golden", "fullsize")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, rec["workload"] + ".json"), "w") as f:
+        json.dump(fx, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -46,7 +46,7 @@ def main(path, name="gpu"):
         if other == name:
             continue
         d = run["rank_deltas"]
-        rec["rank_delta_match_rates"][f"{name} vs {other}"] = float(np.mean([a == b for a, b in zip(deltas, d)]))
+        rec.setdefault("rank_delta_match_rates", {})[f"{name} vs {other}"] = float(np.mean([a == b for a, b in zip(deltas, d)]))
         rec.setdefault("rank_delta_max_abs_diff", {})[f"{name} vs {other}"] = int(
             max(abs(a - b) for a, b in zip(deltas, d)))
     print(json.dumps({name: rec["runs"][name]["rank_deltas"], "rates": rec["rank_delta_match_rates"],

@@ -92,9 +92,12 @@ def run_reference(src, wl, dataset, model, pred, cands, ents):
 
     eng.get_triple_results = wrapped
     rels, calls = [], []
+    run_reference.cand_seconds = []
     for c in cands:
         log.clear()
+        t0 = time.time()
         rels.append(float(eng.compute_relevance(pred, [c])))
+        run_reference.cand_seconds.append(time.time() - t0)
         calls.append(list(log))
     return rels, calls
 
