@@ -18,9 +18,13 @@ reference's random init, the ComplEx DBpedia50 explanation hp (Adagrad 0.043,
 43 epochs, batch 512), 20 candidates per prediction, 10 conversion entities
 (pipeline.py:36-39, degree cap 200).
 
-For N > 1 the driver launches one rank per GPU with torchrun; ranks take
-disjoint predictions (weak scaling), one all-gather of the result records
-at the end.  Rank 0 prints ONE JSON line.
+For N > 1 the driver launches one rank per GPU with torchrun.  A step then holds
+N times the predictions (weak scaling: the per-GPU work is fixed); every rank
+schedules every batch -- the reference's one global random stream, drawn in the same
+order on every rank -- and post-trains its share of the batch's slots, with one
+all-gather of the (slot, score, rank) records per batch
+(kelpie_amd.distributed.SlotSharding), so the results equal the 1-rank run.  Rank 0
+prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -290,10 +294,11 @@ def main():
     engine_cls = SufficientPostTrainingEngine if wl["mode"] == "sufficient" else NecessaryPostTrainingEngine
     eng = engine_cls(model, ds, wl["hp"])
 
+    if world > 1:
+        eng.sharding = kd.SlotSharding()
     n_steps = args.warmup + args.steps
-    per_step = args.preds_per_step or wl.get("preds_per_step", 1)
-    all_preds = pick_preds(ds, world * n_steps * per_step, seed=1234)
-    my_preds = kd.shard(all_preds, rank, world)
+    per_step = (args.preds_per_step or wl.get("preds_per_step", 1)) * world  # weak scaling
+    my_preds = pick_preds(ds, n_steps * per_step, seed=1234)  # every rank schedules every batch
     import random
     random.seed(42)
     np.random.seed(42)
@@ -356,8 +361,7 @@ def main():
     # kp_hot_intervals); with nothing overlapping it is the plain sum of durations.
     hot_union = union_seconds(np.concatenate(ivs)) if ivs else hot[0]
     elapsed_max = kd.max_over_ranks(elapsed)
-    all_recs = kd.gather_records(np.array(recs, dtype=np.float64).reshape(-1, kd.RECORD))
-    total_units = len(all_recs)
+    total_units = len(recs)  # every rank holds every result (counted once)
 
     # roofline of the dominant kernel, from its HIP-event launch durations inside the library
     if wl["model"] == "TransE":
@@ -403,6 +407,7 @@ def main():
         # prediction and candidates, run through the engine after the timed region
         fixture = load_fixture(args.workload)
         pred, cands, ents = jobs[-1][0]
+        eng.sharding = None  # rank 0 alone: no collective on this path
         pred, cands_s, ents, parity = parity_sample(eng, wl, fixture, (pred, cands, ents))
         log(f"[rank 0] parity sample vs reference: {json.dumps(parity)}")
         if not args.no_cpu_baseline:
@@ -427,8 +432,10 @@ def main():
                 "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
                 "config": {"workload": args.workload, "model": wl["model"], "graph": wl["shape"] + " (synthetic)",
                            "dim": wl["dim"], "mode": wl["mode"], "candidates_per_step": wl["candidates"] * per_step,
+                           "predictions_per_step": per_step,
                            "conversion_entities": wl.get("convert"), "epochs": wl["hp"]["epochs"],
-                           "parallelism": f"candidates sharded over {world} rank(s)"},
+                           "parallelism": f"each batch's post-trainings sharded over {world} rank(s), "
+                                          f"host schedule replicated, one all-gather per batch"},
                 "rank_delta_match_rate": (parity.get("fp32") or {}).get("match_rate"),
                 "rank_delta_max_abs_diff": (parity.get("fp32") or {}).get("max_abs_diff"),
                 "rank_delta_vs": "the reference (fp32, CPU) on the fixture tests/golden/fullsize/<workload>.json",

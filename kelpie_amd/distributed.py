@@ -1,11 +1,22 @@
 """One process per GPU: shard candidate explanations across ranks, gather results.
 
 The post-training path partitions naturally: each candidate
-evaluation needs only the frozen tables (a full replica per rank), its rows
-and its random draws.  Ranks therefore take disjoint predictions and never
-exchange data on the hot path; the only collective is one gather of the
-fixed-size result records (relevance, scores, ranks) to rank 0 at the end
-(RCCL over xGMI with the ``nccl`` backend, or ``gloo`` on CPU).
+evaluation needs only the frozen tables (a full replica per rank), its rows and its
+random draws.  What does not partition is the reference's random stream: one
+process-global generator state, seeded once (explain.py:144) and consumed in call
+order across every prediction (post_training_engine.py:52, the optimizers' per-epoch
+draws, engine.py:125, stochastic_builder.py:161-165).  A rank that starts a later
+prediction from a fresh seed returns different results than the sequential run.
+
+``SlotSharding`` keeps the results identical to the 1-rank (and reference) run: every
+rank schedules every engine batch -- the same host-side draws in the same order, so
+every generator stays in lockstep -- and post-trains only its share of the batch's
+slots on its GPU (longest-processing-time assignment by row count, the same on every
+rank); one all-gather of fixed-size (slot, score, rank) records per batch (RCCL over
+xGMI with the ``nccl`` backend, ``gloo`` on CPU) gives every rank every result, so
+the builder's accept / early-exit / ``random.random()`` replay runs identically on all
+ranks.  ``select_entities_to_convert`` shards its conversion test by entity range and
+all-gathers the keep mask.
 """
 from __future__ import annotations
 
@@ -80,3 +91,81 @@ def max_over_ranks(value: float, device=None) -> float:
 def barrier():
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
+
+
+def _device():
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+
+
+class SlotSharding:
+    """Split each engine batch's slots over the ranks (see the module docstring)."""
+
+    def __init__(self, rank=None, world=None, device=None):
+        init = dist.is_initialized()
+        self.rank = dist.get_rank() if rank is None and init else (rank or 0)
+        self.world = dist.get_world_size() if world is None and init else (world or 1)
+        self.device = device
+        self.gathers = 0
+
+    def owners(self, costs):
+        """Owner rank of every slot: longest processing time first, ties to the lowest
+        index / rank, so every rank computes the same assignment."""
+        order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+        loads = [0] * self.world
+        own = [0] * len(costs)
+        for i in order:
+            r = min(range(self.world), key=lambda k: (loads[k], k))
+            own[i] = r
+            loads[r] += costs[i]
+        return own
+
+    def mine(self, costs):
+        own = self.owners(costs)
+        return [i for i, r in enumerate(own) if r == self.rank]
+
+    def gather_slots(self, idx, score, rank, n):
+        """Every rank's (slot index, score, rank) records -> full [n] score / rank arrays."""
+        recs = np.zeros((len(idx), 3), np.float64)
+        if len(idx):
+            recs[:, 0] = idx
+            recs[:, 1] = np.asarray(score, np.float64)
+            recs[:, 2] = np.asarray(rank, np.float64)
+        allr = self._gather(recs, 3)
+        out_s = np.zeros(n, np.float32)
+        out_r = np.zeros(n, np.int64)
+        seen = np.zeros(n, np.int32)
+        for i, sc, rk in allr:
+            i = int(i)
+            out_s[i], out_r[i] = sc, int(rk)
+            seen[i] += 1
+        if not np.all(seen == 1):
+            raise RuntimeError("slot sharding: a slot was not post-trained exactly once")
+        return out_s, out_r
+
+    def gather_mask(self, lo, hi, keep, n):
+        """Keep flags of the entity range [lo, hi) from every rank -> the full [n] mask."""
+        recs = np.zeros((hi - lo, 2), np.float64)
+        recs[:, 0] = np.arange(lo, hi)
+        recs[:, 1] = np.asarray(keep, np.float64)
+        allr = self._gather(recs, 2)
+        out = np.zeros(n, bool)
+        out[allr[:, 0].astype(np.int64)] = allr[:, 1] != 0
+        return out
+
+    def _gather(self, recs, width):
+        self.gathers += 1
+        if self.world == 1 or not dist.is_initialized():
+            return recs
+        device = self.device or _device()
+        cnt = torch.tensor([recs.shape[0]], dtype=torch.int64, device=device)
+        counts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(counts, cnt)
+        counts = [int(c.item()) for c in counts]
+        m = max(counts)
+        buf = torch.zeros((max(m, 1), width), dtype=torch.float64, device=device)
+        if recs.shape[0]:
+            buf[:recs.shape[0]] = torch.from_numpy(recs).to(device)
+        out = torch.zeros((self.world * max(m, 1), width), dtype=torch.float64, device=device)
+        dist.all_gather_into_tensor(out, buf)
+        out = out.cpu().numpy().reshape(self.world, max(m, 1), width)
+        return np.concatenate([out[r, :counts[r]] for r in range(self.world)])

@@ -68,6 +68,9 @@ class RelevanceEngine:
         self.model = model
         self.dataset = dataset
         self._o_to_training = None
+        # kelpie_amd.distributed.SlotSharding: every rank schedules every batch and
+        # post-trains its share of the slots; None = this process does all of them
+        self.sharding = None
 
     @property
     def o_to_training_triples(self):
@@ -108,7 +111,17 @@ class RelevanceEngine:
             F = ds.to_filter.get((e, p), [])
             fl.extend(F)
             fo.append(len(fl))
-        keep = self.model.ctx.convertible(np.array(ents), p, o, np.array(fo), np.array(fl, dtype=np.int64))
+        sh = self.sharding
+        if sh is not None and sh.world > 1:
+            # entity-range shard of the conversion test, keep mask all-gathered
+            lo, hi = len(ents) * sh.rank // sh.world, len(ents) * (sh.rank + 1) // sh.world
+            part = np.zeros(0, bool)
+            if hi > lo:
+                part = self.model.ctx.convertible(np.array(ents[lo:hi]), p, o, np.array(fo[lo:hi + 1]) - fo[lo],
+                                                  np.array(fl[fo[lo]:fo[hi]], dtype=np.int64))
+            keep = sh.gather_mask(lo, hi, part, len(ents))
+        else:
+            keep = self.model.ctx.convertible(np.array(ents), p, o, np.array(fo), np.array(fl, dtype=np.int64))
         overall = [e for e, kflag in zip(ents, keep) if kflag]
         chosen = random.sample(overall, k=min(k, len(overall)))  # engine.py:125 (python RNG)
         self.entities_to_convert = chosen
@@ -165,8 +178,37 @@ class PostTrainingEngine(RelevanceEngine):
         return len(slots) - 1, pred
 
     def _run(self, slots, ctx=None):
+        """Post-train and rank ``slots`` on the device.  With ``self.sharding`` only this
+        rank's share runs; ``_collect`` then gathers every rank's results."""
         if not slots:
             return {}
+        sh = self.sharding
+        if sh is not None and sh.world > 1:
+            mine = sh.mine([max(1, len(s.rows)) for s in slots])
+            if not mine:
+                stats = {"slots": 0, "rows": 0, "pack_s": 0.0, "lib_s": 0.0, "_local": (mine, [], [], len(slots))}
+                self.last_batch_stats = stats
+                return stats
+            sub = [slots[i] for i in mine]
+            stats = self._run_slots(sub, ctx, fill=False)
+            stats["_local"] = (mine, stats.pop("_score"), stats.pop("_rank"), len(slots))
+            self.last_batch_stats = stats
+            return stats
+        return self._run_slots(slots, ctx, fill=True)
+
+    def _collect(self, slots, stats):
+        """All-gather the ranks' slot results of a sharded batch (in batch order on every rank)."""
+        local = stats.pop("_local", None) if stats else None
+        if local is None:
+            return
+        mine, score, rank, n = local
+        t0 = time.perf_counter()
+        all_s, all_r = self.sharding.gather_slots(mine, score, rank, n)
+        for i, s in enumerate(slots):
+            s.result = {"target_score": float(all_s[i]), "target_rank": int(all_r[i])}
+        stats["gather_s"] = time.perf_counter() - t0
+
+    def _run_slots(self, slots, ctx, fill):
         t_run = time.perf_counter()
         n = len(slots)
         D = self.model.dimension
@@ -187,10 +229,13 @@ class PostTrainingEngine(RelevanceEngine):
         ctx = ctx or self.model.ctx
         score, rank, _ = ctx.posttrain_rank(self._kp_hp, x0, row_off, rows, rng_off, rng, pred, filt_off, filt)
         t_end = time.perf_counter()
-        for i, s in enumerate(slots):
-            s.result = {"target_score": float(score[i]), "target_rank": int(rank[i])}
+        if fill:
+            for i, s in enumerate(slots):
+                s.result = {"target_score": float(score[i]), "target_rank": int(rank[i])}
         stats = {"slots": n, "rows": int(row_off[-1]), "pack_s": t_lib - t_run, "lib_s": t_end - t_lib,
                  **ctx.last_timing()}
+        if not fill:
+            stats["_score"], stats["_rank"] = np.array(score), np.array(rank)
         if hasattr(ctx, "hot_intervals"):
             stats["hot_iv"] = ctx.hot_intervals()
         self.last_batch_stats = stats
@@ -223,6 +268,7 @@ class PostTrainingEngine(RelevanceEngine):
             slots, pending, jobs = self._schedule_multi(items, checkpoints)
         t_sched = time.perf_counter() - t0
         self._run(slots)
+        self._collect(slots, self.last_batch_stats)
         self.last_batch_stats["schedule_s"] = t_sched
         outs = self._finalize_multi(slots, pending, jobs)
         self._raise_deferred(slots, pending)
@@ -296,6 +342,7 @@ class PostTrainingEngine(RelevanceEngine):
             if state.get("error") is not None:
                 raise state["error"]
             self.base_pt_results = {}
+            self._collect(state["slots"], state["stats"])
             o = self._finalize_multi(state["slots"], state["pending"], state["jobs"])
             st = state["stats"]
             st["schedule_s"] = state["schedule_s"]

@@ -3,6 +3,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 
@@ -53,3 +54,133 @@ def test_shard_single_rank():
     assert kd.shard([1, 2, 3], 0, 1) == [1, 2, 3]
     recs = np.zeros((2, kd.RECORD))
     assert kd.gather_records(recs).shape == (2, kd.RECORD)
+
+
+# ---------------------------------------------------------------------------
+# engine-level sharding: world-2 results == world-1 results, bit for bit
+# ---------------------------------------------------------------------------
+ENGINE_CASES = ["complex_tiny", "transe_tiny", "conve60_tiny"]
+
+
+def _engine_run(name, sharding, backend="cpu"):
+    """necessary batches (every golden block), sufficient with select_entities_to_convert,
+    the two-context batch pipeline and the builder pipeline, on the CPU stand-in engine."""
+    import sys
+    import tempfile
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from engine_cases import build_product
+    from golden_io import seed_all
+    import kelpie_amd as ka
+    from kelpie_amd.pipeline import build_pipeline, explain_preds
+    rec, ds, model = build_product(name, backend)
+    out = {}
+    seed_all(rec["seed"])
+    eng = ka.NecessaryPostTrainingEngine(model, ds, rec["hp"])
+    eng.sharding = sharding
+    out["necessary"] = []
+    for block in rec["necessary"]:
+        eng.set_cache()
+        rules = [[tuple(t) for t in c["rule"]] for c in block["calls"]]
+        out["necessary"].append(eng.compute_relevance_batch(tuple(block["pred"]), rules))
+    items = [(tuple(b["pred"]), [[tuple(t) for t in c["rule"]] for c in b["calls"][:4]]) for b in rec["necessary"]]
+    out["pipeline"] = eng.compute_relevance_pipeline([[it] for it in items], depth=2)
+    seed_all(rec["seed"])
+    seng = ka.SufficientPostTrainingEngine(model, ds, rec["hp"])
+    seng.sharding = sharding
+    blk = rec["sufficient"][0]
+    out["entities"] = seng.select_entities_to_convert(tuple(blk["pred"]), 3, 200)
+    out["sufficient"] = seng.compute_relevance_batch(tuple(blk["pred"]),
+                                                     [[tuple(t) for t in c["rule"]] for c in blk["calls"]])
+    b = rec.get("builder")
+    if b:
+        seed_all(rec["seed"])
+        pipe = build_pipeline(model, ds, rec["hp"], "necessary", xsi=b["xsi"], window=4)
+        pipe.engine.sharding = sharding
+        with tempfile.TemporaryDirectory() as tmp:
+            preds = [list(ds.labels_triple(tuple(b["pred"])))]
+            res = explain_preds(pipe, ds, preds, prefilter_k=len(b["candidates"]))
+        out["builder"] = [(r["rule_to_relevance"], r["#relevances"]) for r in res]
+    out["gathers"] = sharding.gathers if sharding is not None else 0
+    return out
+
+
+def _engine_worker(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    from kelpie_amd import distributed as kd
+    kd.init_from_env(backend="gloo")
+    try:
+        res = {name: _engine_run(name, kd.SlotSharding(device="cpu")) for name in ENGINE_CASES}
+        q.put((rank, res))
+    except BaseException as e:  # report instead of hanging the other rank's gather
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def test_engine_sharding_world2_equals_world1():
+    """Every rank schedules every batch (the one global random stream stays in lockstep)
+    and post-trains its share of the slots; the gathered relevances, conversion entities
+    and builder explanations equal the single-process run bit for bit (CPU stand-in for
+    the HIP context)."""
+    single = {name: _engine_run(name, None) for name in ENGINE_CASES}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res in out:
+        assert not isinstance(res, str), res
+        for name in ENGINE_CASES:
+            got, exp = dict(res[name]), dict(single[name])
+            assert got.pop("gathers") > 0
+            exp.pop("gathers")
+            assert got == exp, (rank, name)
+
+
+def _engine_worker_gpu(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    from kelpie_amd import distributed as kd
+    kd.init_from_env(backend="gloo")  # two ranks share the box's one GPU
+    try:
+        res = {name: _engine_run(name, kd.SlotSharding(device="cpu"), backend="gpu") for name in ENGINE_CASES}
+        q.put((rank, res))
+    except BaseException as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_engine_sharding_world2_gpu():
+    """The same on the MI355X: two ranks (one GPU, gloo) each post-train their share of
+    every batch through the HIP library; results equal the single-process run.  The
+    goldens here are well conditioned, so ranks and relevances match exactly."""
+    single = {name: _engine_run(name, None, backend="gpu") for name in ENGINE_CASES}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker_gpu, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res in out:
+        assert not isinstance(res, str), res
+        for name in ENGINE_CASES:
+            got, exp = dict(res[name]), dict(single[name])
+            got.pop("gathers"), exp.pop("gathers")
+            assert got == exp, (rank, name)
