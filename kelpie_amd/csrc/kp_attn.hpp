@@ -48,8 +48,16 @@ __device__ __forceinline__ float cx_q(const float* __restrict__ lhs, const float
 // read of the OTHER buffer.  The kernel owns the wait: `s_waitcnt vmcnt(0)`
 // before the barrier that hands the buffer to the readers.
 // ----------------------------------------------------------------------------
+#ifndef KP_GLDS_BUILTIN
+#define KP_GLDS_BUILTIN 0
+#endif
 __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
+#if KP_GLDS_BUILTIN
+  // compiler-owned form: hipcc sets M0 itself and counts the copy in vmcnt
+  __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(uintptr_t)lds_base, 16, 0, 0);
+#else
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
+#endif
 }
 
 // LDS reads issued through inline asm, so their placement is the source order:

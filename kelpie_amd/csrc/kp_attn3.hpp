@@ -57,6 +57,12 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_DMA_SPREAD
 #define KP_DMA_SPREAD 1
 #endif
+#ifndef KP_ILV
+#define KP_ILV 1
+#endif
+#ifndef KP_ASM_ALL
+#define KP_ASM_ALL 0  // 1: the asm read form for every DB (ConvE included)
+#endif
 #ifdef KP_DIAG_NO_O
 #define KP_DIAG_O false
 #else
@@ -98,35 +104,37 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
 //    kernel's own counted waits, at the price of a v_add per read (best for the
 //    register-bound one-wave-per-SIMD ComplEx d = 200 kernel: 0.383 vs 0.408 ms).
 typedef __bf16 bf16v4 __attribute__((__vector_size__(8)));
+// `off` is a compile-time constant after unrolling (< 64 KiB): the asm form carries it
+// in the instruction's offset field, so a read costs no address arithmetic.
 template <bool ASM>
-__device__ __forceinline__ bf16x8 lds_rd_bf8(uint32_t addr) {
+__device__ __forceinline__ bf16x8 lds_rd_bf8(uint32_t addr, int off) {
   if constexpr (ASM) {
     bf16x8 v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
     return v;
   } else {
-    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>((uintptr_t)addr);
+    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>((uintptr_t)(addr + off));
   }
 }
 template <bool ASM>
-__device__ __forceinline__ bf16x4 lds_rd_bf4(uint32_t addr) {
+__device__ __forceinline__ bf16x4 lds_rd_bf4(uint32_t addr, int off) {
   if constexpr (ASM) {
     bf16x4 v;
-    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
     return v;
   } else {
-    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x4*>((uintptr_t)addr);
+    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x4*>((uintptr_t)(addr + off));
   }
 }
 template <bool ASM>
-__device__ __forceinline__ bf16x4 lds_rd_tr(uint32_t addr) {
+__device__ __forceinline__ bf16x4 lds_rd_tr(uint32_t addr, int off) {
   if constexpr (ASM) {
     bf16x4 v;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(off));
     return v;
   } else {
     const bf16v4 v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-        reinterpret_cast<__attribute__((address_space(3))) bf16v4*>((uintptr_t)addr));
+        reinterpret_cast<__attribute__((address_space(3))) bf16v4*>((uintptr_t)(addr + off)));
     return __builtin_bit_cast(bf16x4, v);
   }
 }
@@ -144,6 +152,10 @@ template <bool ASM, int N>
 __device__ __forceinline__ void lgkm_wait3() {
   if constexpr (ASM) lgkm_wait<N>();
 }
+
+// the six products of mfma3, in its order: piece of a, piece of b
+constexpr int kPA[6] = {2, 1, 0, 1, 0, 0};
+constexpr int kPB[6] = {0, 1, 2, 0, 1, 0};
 
 // six-product a.b on one accumulator (smallest terms first)
 __device__ __forceinline__ f32x4 mfma3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
@@ -195,7 +207,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                                                    float ylo, const double* __restrict__ colpre) {
   constexpr bool WITH_O = MODE != ATT_SOFTMAX;
   constexpr int DP = 16 * DB;
-  constexpr bool ASM = DB > 13;  // read form (see lds_rd_bf8)
+  constexpr bool ASM = DB > 13 || KP_ASM_ALL;  // read form (see lds_rd_bf8)
+  // interleaved schedule of the asm read form (KP_ILV, default on): reads two k-steps /
+  // O blocks ahead, one per MFMA issue gap, order pinned by sched_barrier
+  constexpr bool ILV = ASM && KP_ILV;
   constexpr int NK = DP / 32;         // full 32-deep k-steps of the S phase
   constexpr int TAIL = (DP % 32) / 16;  // one 16-deep k-step (16x16x16 MFMA) when DP % 32 == 16
   constexpr int KT = 32;
@@ -330,10 +345,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         // ahead of its MFMAs (LDS returns in order: a counted lgkmcnt wait).
         f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
         const uint32_t rb = tb + (uint32_t)(c * ROW_B + 16 * g);
+        const uint32_t rbt = rb - 8u * g;        // tail reads: 8 bytes per lane group
         constexpr uint32_t SUB_B = 16u * ROW_B;  // the second sub-tile's rows
+        static_assert(SUB_B + 3 * PART_B + 64 * NK < 65536, "LDS read offsets exceed the 16-bit offset field");
         // k-step j < NK: six ds_read_b128 into buffer j % (SA + 1); step NK (TAIL): six
         // ds_read_b64.  Reads run KP_S_AHEAD steps ahead of their MFMAs.
-        constexpr int SA = KP_S_AHEAD;
+        constexpr int SA = ILV ? 2 : KP_S_AHEAD;
         constexpr int LAST = NK + TAIL - 1;  // index of the last k-step
         bf16x8 ra[SA + 1][2][3];
         bf16x4 rt[2][3];
@@ -341,14 +358,14 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #pragma unroll
           for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) ra[b][u][p] = lds_rd_bf8<ASM>(rb + u * SUB_B + (uint32_t)(p * PART_B + 64 * s));
+            for (int p = 0; p < 3; ++p) ra[b][u][p] = lds_rd_bf8<ASM>(rb, (int)(u * SUB_B) + p * PART_B + 64 * s);
         };
         auto load_tail = [&]() {
 #pragma unroll
           for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-              rt[u][p] = lds_rd_bf4<ASM>(rb - 8u * g + u * SUB_B + (uint32_t)(p * PART_B + 64 * NK));  // dims 32 NK + 4g ..
+              rt[u][p] = lds_rd_bf4<ASM>(rbt, (int)(u * SUB_B) + p * PART_B + 64 * NK);  // dims 32 NK + 4g ..
         };
         auto load_step = [&](int j) {
           if (j < NK)
@@ -357,6 +374,47 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             load_tail();
         };
 #ifndef KP_DIAG_NO_S
+        if constexpr (ILV) {
+          // Interleaved form: step s's twelve MFMAs (the two sub-tiles' chains
+          // alternating, each chain in mfma3's smallest-first order) carry step s + 2's
+          // six reads in every other issue gap; sched_barrier pins that order, so the
+          // reads never bunch up behind an MFMA group and a read has a whole step of
+          // MFMAs (192 cycles) to land.  Before step s: wait until only step s + 1's
+          // reads are pending.
+          load_step(0);
+          if (LAST >= 1) load_step(1);
+#pragma unroll
+          for (int s = 0; s <= LAST; ++s) {
+            if (s < LAST)
+              lgkm_wait<6>();
+            else
+              lgkm_wait<0>();
+            __builtin_amdgcn_sched_barrier(0);
+            const int b = s % 3;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                if (s < NK)
+                  sc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[b][u][kPA[k]], qb[s < NK ? s : 0][kPB[k]], sc[u], 0,
+                                                                 0, 0);
+                else
+                  sc[u] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, rt[u][kPA[k]]),
+                                                                    __builtin_bit_cast(s16x4, qt4[kPB[k]]), sc[u], 0, 0,
+                                                                    0);
+                if (u == 0 && s + 2 <= LAST) {
+                  // read k of step s + 2: (sub-tile k % 2, piece k / 2)
+                  const int j = s + 2, uu = k & 1, pp = k >> 1;
+                  if (j < NK)
+                    ra[j % 3][uu][pp] = lds_rd_bf8<true>(rb, (int)(uu * SUB_B) + pp * PART_B + 64 * j);
+                  else
+                    rt[uu][pp] = lds_rd_bf4<true>(rbt, (int)(uu * SUB_B) + pp * PART_B + 64 * NK);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+          }
+        } else {
 #pragma unroll
         for (int j = 0; j < SA && j <= LAST; ++j) load_step(j);
 #pragma unroll
@@ -390,6 +448,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             sc[u] = mfma3_k16(a, qt4, sc[u]);
           }
         }
+        }
 #endif
 #if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
         // one burst here, or (KP_DMA_SPREAD, with an O phase) one piece per O block below:
@@ -404,13 +463,13 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         const uint32_t ob = tb + (uint32_t)((4 * g + (c >> 2)) * ROW_B + 8 * (c & 3));
         // O-phase read-ahead depth: KP_O_AHEAD blocks (one block is 6 MFMAs = 96 cycles,
         // less than an LDS read's latency with four waves reading)
-        constexpr int OA = KP_O_AHEAD;
+        constexpr int OA = ILV ? 2 : KP_O_AHEAD;
         bf16x4 ol[OA + 1][3], oh[OA + 1][3];
         auto load_o = [&](int m, int b) {
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
-            ol[b][p] = lds_rd_tr<ASM>(ob + (uint32_t)(p * PART_B + 32 * m));
-            oh[b][p] = lds_rd_tr<ASM>(ob + (uint32_t)(16 * ROW_B + p * PART_B + 32 * m));
+            ol[b][p] = lds_rd_tr<ASM>(ob, p * PART_B + 32 * m);
+            oh[b][p] = lds_rd_tr<ASM>(ob, 16 * ROW_B + p * PART_B + 32 * m);
           }
         };
         if (WITH_O && KP_DIAG_O) {
@@ -499,6 +558,34 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                 for (int k = DB; k < NPW; ++k) issue_piece(t + 1, (t + 1) & 1, k);
             }
 #endif
+            if constexpr (ILV) {
+              // block m + 2's six reads ride in block m's MFMA issue gaps (sched_barrier
+              // pins the order); before block m only block m + 1's reads may be pending
+              if (m + 1 < DB)
+                lgkm_wait<6>();
+              else
+                lgkm_wait<0>();
+              __builtin_amdgcn_sched_barrier(0);
+              bf16x8 a[3];
+#pragma unroll
+              for (int p = 0; p < 3; ++p) {
+                const bf16x4 x = ol[m % 3][p], y = oh[m % 3][p];
+                a[p] = (bf16x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+              }
+#pragma unroll
+              for (int k = 0; k < 6; ++k) {
+                O[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kPA[k]], pb[kPB[k]], O[m], 0, 0, 0);
+                if (m + 2 < DB) {
+                  const int mm = m + 2, pp = k >> 1;
+                  if (k & 1)
+                    oh[mm % 3][pp] = lds_rd_tr<true>(ob, 16 * ROW_B + pp * PART_B + 32 * mm);
+                  else
+                    ol[mm % 3][pp] = lds_rd_tr<true>(ob, pp * PART_B + 32 * mm);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+              }
+              continue;
+            }
             // block m's reads are complete once at most (issued after them) reads are pending
             if (m + OA < DB) {
               load_o(m + OA, (m + OA) % (OA + 1));

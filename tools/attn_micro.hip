@@ -1,0 +1,147 @@
+// attn_micro.hip -- standalone timing + fp64 check of kp_attn3 (the ComplEx / ConvE
+// attention pass) on one synthetic problem, for A/B of kernel variants built with
+// different defines (tools/attn_micro.sh).  Not part of the product library.
+//
+//   attn_micro <DB 25|13> <mode 0|2> <n_ent> <nq> <iters> [scale] [part 0|1|2]
+//
+// Prints one JSON line: per-launch ms (HIP events around `iters` back-to-back launches),
+// fp32-equivalent TF/s (4 D per (query, entity) with O, 2 D without), and the largest
+// relative error of the merged (m, l, O) of 16 sampled queries against fp64.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+
+#include "kp_attn3.hpp"  // -I selects the source tree under test (tools/attn_micro.sh)
+
+using namespace kpattn;
+
+template <int DB, int MODE>
+static int run(int n_ent, int nq, int iters, float scale, int part) {
+  constexpr int DP = 16 * DB;
+  kp_ctx c;
+  KP_HIP(hipStreamCreate(&c.stream));
+  hipDeviceProp_t prop;
+  KP_HIP(hipGetDeviceProperties(&prop, 0));
+  c.n_cu = prop.multiProcessorCount;
+  c.n_ent = n_ent;
+  c.dp = DP;
+  c.attn_mode = 1;
+  c.attn_part = part;
+  std::mt19937 gen(1234);
+  std::normal_distribution<float> nd(0.f, 1.f);
+  std::vector<float> E((size_t)n_ent * DP, 0.f), Q((size_t)nq * DP, 0.f), qs(nq);
+  for (int e = 0; e < n_ent; ++e)
+    for (int d = 0; d < DP; ++d) E[(size_t)e * DP + d] = scale * nd(gen);
+  for (int q = 0; q < nq; ++q) {
+    for (int d = 0; d < DP; ++d) Q[(size_t)q * DP + d] = scale * nd(gen);
+    qs[q] = 1.0f / (float)n_ent;
+  }
+  KP_HIP(hipMalloc(&c.dE, E.size() * 4));
+  KP_HIP(hipMemcpy(c.dE, E.data(), E.size() * 4, hipMemcpyHostToDevice));
+  float *dQ, *dqs;
+  KP_HIP(hipMalloc(&dQ, Q.size() * 4));
+  KP_HIP(hipMalloc(&dqs, nq * 4));
+  KP_HIP(hipMemcpy(dQ, Q.data(), Q.size() * 4, hipMemcpyHostToDevice));
+  KP_HIP(hipMemcpy(dqs, qs.data(), nq * 4, hipMemcpyHostToDevice));
+  const int slots = c.n_cu * attn3_wpc<DB>(&c);
+  const AttnPlan plan = attn_plan_ctx(&c, nq, n_ent, slots);
+  const int parts = plan.wk.n_parts;
+  float *dm, *dl, *dO;
+  KP_HIP(hipMalloc(&dm, (size_t)parts * nq * 4));
+  KP_HIP(hipMalloc(&dl, (size_t)parts * nq * 4));
+  KP_HIP(hipMalloc(&dO, (size_t)parts * nq * DP * 4));
+  const float ylo = 0.05f;
+  auto launch = [&]() { launch_attn3<DB, MODE>(&c, n_ent, dQ, nq, plan, dm, dl, dO, dqs, ylo); };
+  launch();
+  KP_HIP(hipStreamSynchronize(c.stream));
+  hipEvent_t e0, e1;
+  KP_HIP(hipEventCreate(&e0));
+  KP_HIP(hipEventCreate(&e1));
+  for (int i = 0; i < 3; ++i) launch();
+  KP_HIP(hipEventRecord(e0, c.stream));
+  for (int i = 0; i < iters; ++i) launch();
+  KP_HIP(hipEventRecord(e1, c.stream));
+  KP_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  KP_HIP(hipEventElapsedTime(&ms, e0, e1));
+  ms /= iters;
+  std::vector<float> hm((size_t)parts * nq), hl((size_t)parts * nq), hO((size_t)parts * nq * DP);
+  if (MODE != ATT_BCE_O) {
+    KP_HIP(hipMemcpy(hm.data(), dm, hm.size() * 4, hipMemcpyDeviceToHost));
+    KP_HIP(hipMemcpy(hl.data(), dl, hl.size() * 4, hipMemcpyDeviceToHost));
+  }
+  KP_HIP(hipMemcpy(hO.data(), dO, hO.size() * 4, hipMemcpyDeviceToHost));
+  // fp64 check of 16 sampled queries
+  double err_l = 0, err_o = 0;
+  for (int k = 0; k < 16; ++k) {
+    const int q = (int)((long long)k * 7919 % nq);
+    std::vector<double> s(n_ent);
+    double M = -1e300;
+    for (int e = 0; e < n_ent; ++e) {
+      double a = 0;
+      for (int d = 0; d < DP; ++d) a += (double)Q[(size_t)q * DP + d] * E[(size_t)e * DP + d];
+      s[e] = a;
+      M = std::max(M, a);
+    }
+    std::vector<double> O(DP, 0.0);
+    double L = 0;
+    double onorm = 0;
+    for (int e = 0; e < n_ent; ++e) {
+      double w;
+      if (MODE == ATT_BCE_O) {
+        const double p = 1.0 / (1.0 + std::exp(-s[e]));
+        const double w0 = (1 - p) * p;
+        w = ((p - ylo) / std::max(w0, 1e-12) * qs[q]) * w0;
+      } else {
+        w = std::exp(s[e] - M);
+      }
+      L += w;
+      for (int d = 0; d < DP; ++d) O[d] += w * E[(size_t)e * DP + d];
+    }
+    for (int d = 0; d < DP; ++d) onorm = std::max(onorm, std::fabs(O[d]));
+    // merge the GPU partials
+    double gM = -1e300;
+    if (MODE != ATT_BCE_O)
+      for (int p = 0; p < parts; ++p) gM = std::max(gM, (double)hm[(size_t)p * nq + q]);
+    double gL = 0;
+    std::vector<double> gO(DP, 0.0);
+    for (int p = 0; p < parts; ++p) {
+      const double f = MODE == ATT_BCE_O ? 1.0 : std::exp((double)hm[(size_t)p * nq + q] - gM);
+      if (MODE != ATT_BCE_O) gL += f * hl[(size_t)p * nq + q];
+      for (int d = 0; d < DP; ++d) gO[d] += f * hO[((size_t)p * nq + q) * DP + d];
+    }
+    if (MODE != ATT_BCE_O) {
+      const double sc = std::exp(gM - M);  // GPU stats relative to its own max
+      err_l = std::max(err_l, std::fabs(gL * sc - L) / L);
+      for (int d = 0; d < DP; ++d) err_o = std::max(err_o, std::fabs(gO[d] * sc - O[d]) / onorm);
+    } else {
+      for (int d = 0; d < DP; ++d) err_o = std::max(err_o, std::fabs(gO[d] - O[d]) / onorm);
+    }
+  }
+  const double flops = (MODE == ATT_SOFTMAX ? 2.0 : 4.0) * DP * (double)nq * n_ent;
+  printf("{\"DB\": %d, \"mode\": %d, \"n_ent\": %d, \"nq\": %d, \"parts\": %d, \"ranges\": %d, \"n_wg\": %d, "
+         "\"ms\": %.5f, \"tflops\": %.2f, \"frac_bf16x6\": %.4f, \"err_l\": %.3e, \"err_o\": %.3e}\n",
+         DB, MODE, n_ent, nq, parts, plan.wk.ranges, plan.n_wg, ms, flops / ms / 1e9, flops / ms / 1e9 / 419.43,
+         err_l, err_o);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 6) {
+    fprintf(stderr, "usage: attn_micro DB mode n_ent nq iters [scale] [part]\n");
+    return 2;
+  }
+  const int DB = atoi(argv[1]), mode = atoi(argv[2]), n_ent = atoi(argv[3]), nq = atoi(argv[4]), iters = atoi(argv[5]);
+  const float scale = argc > 6 ? (float)atof(argv[6]) : 0.05f;
+  const int part = argc > 7 ? atoi(argv[7]) : 0;
+  try {
+    if (DB == 25 && mode == 0) return run<25, ATT_SOFTMAX_O>(n_ent, nq, iters, scale, part);
+    if (DB == 13 && mode == 2) return run<13, ATT_BCE_O>(n_ent, nq, iters, scale, part);
+    fprintf(stderr, "unsupported DB/mode\n");
+    return 2;
+  } catch (const KpError& e) {
+    fprintf(stderr, "error: %s\n", e.msg.c_str());
+    return 1;
+  }
+}
