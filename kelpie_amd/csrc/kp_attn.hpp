@@ -42,22 +42,25 @@ __device__ __forceinline__ float cx_q(const float* __restrict__ lhs, const float
 
 // ----------------------------------------------------------------------------
 // LDS-DMA: one wave-instruction copies 64 lanes x 16 B from per-lane global
-// addresses to the wave-uniform LDS byte address `lds_base` (+16 B per lane).
-// Issued through inline asm so the compiler does not track the asynchronous LDS
-// write: it would otherwise drain it (s_waitcnt vmcnt(0)) before the first LDS
-// read of the OTHER buffer.  The kernel owns the wait: `s_waitcnt vmcnt(0)`
-// before the barrier that hands the buffer to the readers.
+// addresses to the wave-uniform LDS byte address `lds_base` (+16 B per lane).  Two
+// forms (template flag BUILTIN):
+//  - __builtin_amdgcn_global_load_lds: hipcc sets M0 itself and counts the copy, and
+//    waits for it (vmcnt(0)) before any later LDS read the compiler can see.  Used
+//    where every LDS read is inline asm (kp_attn, the asm read form of kp_attn3): the
+//    compiler sees no read to serialise, so the copy streams under the MFMAs.
+//  - inline asm (M0 written inside the statement): for the compiler-visible read form
+//    of kp_attn3 (ConvE), where the builtin's waits would drain every copy before the
+//    next O-phase read (4.18 vs 2.05 ms per launch measured with the spread schedule).
+// Either way the kernel owns the hand-off: `s_waitcnt vmcnt(0)` before the barrier
+// that gives the buffer to the readers.
 // ----------------------------------------------------------------------------
-#ifndef KP_GLDS_BUILTIN
-#define KP_GLDS_BUILTIN 0
-#endif
+template <bool BUILTIN>
 __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
-#if KP_GLDS_BUILTIN
-  // compiler-owned form: hipcc sets M0 itself and counts the copy in vmcnt
-  __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(uintptr_t)lds_base, 16, 0, 0);
-#else
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
-#endif
+  if constexpr (BUILTIN) {
+    __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(uintptr_t)lds_base, 16, 0, 0);
+  } else {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
+  }
 }
 
 // LDS reads issued through inline asm, so their placement is the source order:
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn(const float* __restrict__ E, i
     const int row = (w + 4 * p) / SEGS;
     const int grow = min(key_begin + tile * KT + row, n_ent - 1);
     const uint32_t dst = lds0 + 4u * (uint32_t)(buf * (KT * S) + row * S + my_seg * 256);
-    glds16(lane_src + (size_t)grow * DP, __builtin_amdgcn_readfirstlane(dst));
+    glds16<true>(lane_src + (size_t)grow * DP, __builtin_amdgcn_readfirstlane(dst));
   };
   auto issue = [&](int tile, int buf) {
 #pragma unroll

@@ -33,6 +33,21 @@
 #pragma once
 #include "kp_attn.hpp"
 
+#ifdef KP_ATTN3_STAMPS
+#ifndef KP_DIAGNOSTIC_BUILD
+#error "KP_ATTN3_STAMPS is a diagnostic build (make diag / tools/attn_micro.sh)"
+#endif
+// diagnostic: per-phase issue cycles of kp_attn3 summed over waves (s_memtime; its
+// lgkmcnt return also perturbs the kernel's counted LDS waits, so this build's results
+// are not checked): [S, softmax + split, O, tile end (DMA wait + barrier), tiles]
+__device__ unsigned long long g_attn3_stamps[8];
+#define KP3_STAMP(v) v = __builtin_amdgcn_s_memtime()
+#define KP3_ACC(i, a, b) st_acc[i] += (b) - (a)
+#else
+#define KP3_STAMP(v) (void)0
+#define KP3_ACC(i, a, b) (void)0
+#endif
+
 #ifndef KP_O_AHEAD
 #define KP_O_AHEAD 1
 #endif
@@ -46,7 +61,7 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 // KP_DIAGNOSTIC_BUILD, which `make diag` sets for the variants/ libraries; the product
 // library can never carry one by a stray define.
 #if (defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O) || defined(KP_ATTN_NODMA) || defined(KP_DIAG_DMA_LGKM0) || \
-     defined(KP_DMA_SPREAD_ALL)) && !defined(KP_DIAGNOSTIC_BUILD)
+     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4)) && !defined(KP_DIAGNOSTIC_BUILD)
 #error "kp_attn3 diagnostic define without KP_DIAGNOSTIC_BUILD (these builds compute wrong results: make diag)"
 #endif
 // KP_DMA_SPREAD: the next tile's LDS-DMA goes out one piece per O block instead of one
@@ -226,6 +241,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   const int g = lane >> 4, c = lane & 15;
   int key_begin = 0, key_end = 0;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds3;
+#ifdef KP_ATTN3_STAMPS
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0;
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
+#endif
 
   // linear LDS-DMA of a tile: piece p = bytes [1024 p, 1024 p + 1024) of the tile,
   // wave w issues p = w, w + 4, ... (the image has >= 1 KiB of slack past its end)
@@ -235,7 +254,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
     for (int p0 = 0; p0 < PIECES; p0 += 4) {
       const int p = p0 + w;
       if (p < PIECES)
-        glds16(reinterpret_cast<const float*>(src + 1024 * p),
+        glds16<ASM>(reinterpret_cast<const float*>(src + 1024 * p),
                __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)));
     }
   };
@@ -247,11 +266,22 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #else
   constexpr bool SPREAD = KP_DMA_SPREAD && ASM && WITH_O && KP_DIAG_O;
 #endif
+  // KP_DMA_SPREAD == 2 (interleaved schedule): the pieces go out evenly over the S steps
+  // and the O blocks (slot k of NSLOT), so the copy's LDS writes share the LDS with the
+  // lighter S-phase reads instead of piling onto the O phase's transposed reads
+  // (== 3: over the S steps only)
+  constexpr int NSLOT = (DP / 32 + (DP % 32) / 16) + (KP_DMA_SPREAD == 3 ? 0 : DB);
+  constexpr bool SPREAD2 = SPREAD && ILV && KP_DMA_SPREAD >= 2;
   auto issue_piece = [&](int tile, int buf, int k) {
     const int p = 4 * k + w;
     if (p < PIECES)
-      glds16(reinterpret_cast<const float*>(E3 + (size_t)(key_begin + tile * KT) * ROW_B + 16 * lane + 1024 * p),
+      glds16<ASM>(reinterpret_cast<const float*>(E3 + (size_t)(key_begin + tile * KT) * ROW_B + 16 * lane + 1024 * p),
              __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)));
+  };
+  auto dma_slot = [&](int tile, int buf, int slot) {
+#pragma unroll
+    for (int k = 0; k < NPW; ++k)
+      if ((k * NSLOT) / NPW == slot) issue_piece(tile, buf, k);
   };
   const int QT = (nq + 63) / 64;
   // work segments: stream-K ranges (wk.ranges == 0) or XCD-grouped units (attn_plan_ranges)
@@ -335,6 +365,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 
       for (int t = 0; t < ntiles; ++t) {
         const int k0 = key_begin + t * KT;
+        KP3_STAMP(st0);
         const uint32_t tb = lds0 + (uint32_t)((t & 1) * BUF_B);
 #if !defined(KP_ATTN_NODMA) && defined(KP_DMA_EARLY)
         // the other buffer was released by the previous tile's closing barrier
@@ -344,6 +375,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         // Both sub-tiles per k-step; each step's six operand reads are issued one step
         // ahead of its MFMAs (LDS returns in order: a counted lgkmcnt wait).
         f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#ifdef KP_DIAG_S4
+        f32x4 sc4[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#endif
         const uint32_t rb = tb + (uint32_t)(c * ROW_B + 16 * g);
         const uint32_t rbt = rb - 8u * g;        // tail reads: 8 bytes per lane group
         constexpr uint32_t SUB_B = 16u * ROW_B;  // the second sub-tile's rows
@@ -390,18 +424,28 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             else
               lgkm_wait<0>();
             __builtin_amdgcn_sched_barrier(0);
+#if !defined(KP_ATTN_NODMA)
+            if (SPREAD2 && t + 1 < ntiles) {
+              dma_slot(t + 1, (t + 1) & 1, s);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+#endif
             const int b = s % 3;
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
 #pragma unroll
               for (int u = 0; u < 2; ++u) {
+#ifdef KP_DIAG_S4
+                f32x4& acc = (s & 1) ? sc4[u] : sc[u];  // diagnostic: four accumulation chains
+#else
+                f32x4& acc = sc[u];
+#endif
                 if (s < NK)
-                  sc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[b][u][kPA[k]], qb[s < NK ? s : 0][kPB[k]], sc[u], 0,
-                                                                 0, 0);
+                  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[b][u][kPA[k]], qb[s < NK ? s : 0][kPB[k]], acc, 0, 0,
+                                                               0);
                 else
-                  sc[u] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, rt[u][kPA[k]]),
-                                                                    __builtin_bit_cast(s16x4, qt4[kPB[k]]), sc[u], 0, 0,
-                                                                    0);
+                  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, rt[u][kPA[k]]),
+                                                                  __builtin_bit_cast(s16x4, qt4[kPB[k]]), acc, 0, 0, 0);
                 if (u == 0 && s + 2 <= LAST) {
                   // read k of step s + 2: (sub-tile k % 2, piece k / 2)
                   const int j = s + 2, uu = k & 1, pp = k >> 1;
@@ -414,6 +458,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
               }
             }
           }
+#ifdef KP_DIAG_S4
+          sc[0] += sc4[0];
+          sc[1] += sc4[1];
+#endif
         } else {
 #pragma unroll
         for (int j = 0; j < SA && j <= LAST; ++j) load_step(j);
@@ -472,6 +520,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             oh[b][p] = lds_rd_tr<ASM>(ob, 16 * ROW_B + p * PART_B + 32 * m);
           }
         };
+        KP3_STAMP(st1);
         if (WITH_O && KP_DIAG_O) {
 #pragma unroll
           for (int m = 0; m < OA && m < DB; ++m) load_o(m, m);
@@ -544,10 +593,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             pb[1][j] = m;
             pb[2][j] = l;
           }
+          KP3_STAMP(st2);
 #pragma unroll
           for (int m = 0; m < DB; ++m) {
 #if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
-            if (SPREAD && t + 1 < ntiles) {
+            if (SPREAD && !SPREAD2 && t + 1 < ntiles) {
               if (m < NPW) {
                 issue_piece(t + 1, (t + 1) & 1, m);
 #ifdef KP_DIAG_DMA_LGKM0
@@ -566,6 +616,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
               else
                 lgkm_wait<0>();
               __builtin_amdgcn_sched_barrier(0);
+#if !defined(KP_ATTN_NODMA)
+              if (SPREAD2 && t + 1 < ntiles) {
+                dma_slot(t + 1, (t + 1) & 1, NK + TAIL + m);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+#endif
               bf16x8 a[3];
 #pragma unroll
               for (int p = 0; p < 3; ++p) {
@@ -606,8 +662,17 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             O[m] = mfma3(a, pb, O[m]);
           }
         }
+        KP3_STAMP(st3);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        KP3_STAMP(st4);
+        KP3_ACC(0, st0, st1);
+        KP3_ACC(1, st1, st2);
+        KP3_ACC(2, st2, st3);
+        KP3_ACC(3, st3, st4);
+#ifdef KP_ATTN3_STAMPS
+        st_acc[4] += 1;
+#endif
       }
       if (MODE == ATT_BCE_O) break;
       float mq = fmaxf(m_seen, __shfl_xor(m_seen, 16, 64));
@@ -668,6 +733,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
       }
     }
   }
+#ifdef KP_ATTN3_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_attn3_stamps[i], st_acc[i]);
+#endif
 }
 
 // Host: the split image of c->dE (row stride DP = c->dp), built once per context.

@@ -120,6 +120,19 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
     }
   }
   const double flops = (MODE == ATT_SOFTMAX ? 2.0 : 4.0) * DP * (double)nq * n_ent;
+#ifdef KP_ATTN3_STAMPS
+  {
+    // one more launch with zeroed counters: cycles per (wave, tile) of each phase
+    unsigned long long z[8] = {0}, st[8];
+    KP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_attn3_stamps), z, sizeof(z)));
+    launch();
+    KP_HIP(hipStreamSynchronize(c.stream));
+    KP_HIP(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_attn3_stamps), sizeof(st)));
+    const double n = (double)(st[4] ? st[4] : 1);
+    printf("{\"stamps\": {\"S\": %.0f, \"softmax\": %.0f, \"O\": %.0f, \"tile_end\": %.0f, \"wave_tiles\": %llu}}\n",
+           st[0] / n, st[1] / n, st[2] / n, st[3] / n, st[4]);
+  }
+#endif
   printf("{\"DB\": %d, \"mode\": %d, \"n_ent\": %d, \"nq\": %d, \"parts\": %d, \"ranges\": %d, \"n_wg\": %d, "
          "\"ms\": %.5f, \"tflops\": %.2f, \"frac_bf16x6\": %.4f, \"err_l\": %.3e, \"err_o\": %.3e}\n",
          DB, MODE, n_ent, nq, parts, plan.wk.ranges, plan.n_wg, ms, flops / ms / 1e9, flops / ms / 1e9 / 419.43,
