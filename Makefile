@@ -18,7 +18,7 @@ build/%.o: kelpie_amd/csrc/%.hip kelpie_amd/csrc/kp_common.hpp kelpie_amd/csrc/k
 # host-only C++ (prefilter graphs)
 build/%.cpp.o: kelpie_amd/csrc/%.cpp include/kelpie_hip.h
 	@mkdir -p build
-	$(CXX) -O3 -std=c++17 -fPIC -Wall -mavx2 -pthread -Iinclude -c $< -o $@
+	$(CXX) -O3 -std=c++17 -fPIC -Wall -mavx2 -pthread -Iinclude $(if $(findstring kp_rng,$<),-ffp-contract=off -mfma) -c $< -o $@
 
 $(LIB): $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $(OBJ)

@@ -192,6 +192,13 @@ int kp_criage_relevance(kp_ctx* ctx, int32_t n, const int32_t* items, int32_t n_
  * construction makes (conve.py:46-52 via :202) without materialising them. */
 int kp_mt19937_discard(uint8_t* state, size_t state_len, uint64_t n);
 
+/* torch.empty(n).normal_(mean, std) on the CPU generator for float32, n >= 16
+ * (ATen normal_fill / normal_fill_AVX2, aten/src/ATen/native/cpu/DistributionTemplates.h),
+ * bit for bit, advancing the state blob like torch.  cap = 1 for torch's AVX2 / AVX512 CPU
+ * kernels (torch.backends.cpu.get_cpu_capability()), 0 for its scalar default kernel.
+ * Replaces the xavier_normal_ of KelpieTransE (src/link_prediction/models/transe.py:93-95). */
+int kp_rng_normal(uint8_t* state, size_t state_len, int64_t n, float mean, float std, int32_t cap, float* out);
+
 /* Keep-mask of torch.empty(n).bernoulli_(p) on the CPU generator (ATen draws
  * one random64 = (hi << 32) | lo per element; keep iff u53 * 2^-53 < p), written
  * as packed bits (bit i of word i/32) and advancing the state blob in place.
@@ -218,6 +225,21 @@ int kp_rng_transe_epochs(uint8_t* torch_state, size_t torch_len, uint32_t* np_ke
  * Same draws, same final states as calling kp_rng_transe_epochs per slot. */
 int kp_rng_transe_enqueue(uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos, int32_t R,
                           int32_t epochs, int32_t ratio, int64_t n_entities, int32_t* out);
+
+/* The torch / numpy draws of n TransE compute_relevance calls, in the reference's order
+ * (post_training_engine.py:46-62 with transe.py:93-95 and
+ * pairwise_ranking_optimizer.py:166-181), in one library call.  Per call i:
+ * torch.rand(1, D) (its values are overwritten, only the state advances), xavier_normal_
+ * of the base kelpie row -> x_base[i] (kp_rng_normal, std = xavier_std), the base
+ * post-training's epoch draws if R_base[i] >= 0, xavier_normal_ of the post-trained row
+ * -> x_pt[i], and its epoch draws if R_pt[i] >= 0 (R = -1: the call schedules no such
+ * post-training).  The epoch draws (as kp_rng_transe_epochs, deferred as
+ * kp_rng_transe_enqueue: complete after kp_rng_wait) go to `out` back to back in that
+ * order.  d >= 16; x_base / x_pt are [n][d]. */
+int kp_rng_transe_calls(uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos, int32_t cap,
+                        int32_t D, int32_t d, float xavier_std, int32_t n, const int32_t* R_base,
+                        const int32_t* R_pt, int32_t epochs, int32_t ratio, int64_t n_entities, float* x_base,
+                        float* x_pt, int32_t* out);
 
 /* Block until every slot queued by kp_rng_transe_enqueue is written. */
 int kp_rng_wait(void);

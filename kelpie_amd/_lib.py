@@ -21,7 +21,8 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
            "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_rng_conve_masks_enqueue", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
-           "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals"]
+           "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals", "kp_rng_normal",
+           "kp_rng_transe_calls"]
 
 
 class ModelDesc(C.Structure):
@@ -84,6 +85,10 @@ def lib():
                                            C.c_int32, C.c_int64, C.c_void_p]
         L.kp_rng_transe_enqueue.argtypes = L.kp_rng_transe_epochs.argtypes
         L.kp_rng_wait.argtypes = []
+        L.kp_rng_normal.argtypes = [C.c_void_p, C.c_size_t, C.c_int64, C.c_float, C.c_float, C.c_int32, C.c_void_p]
+        L.kp_rng_transe_calls.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                          C.c_int32, C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
+                                          C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_rng_conve_masks.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_int32, C.c_double,
                                          C.c_void_p]
         L.kp_rng_conve_masks_enqueue.argtypes = L.kp_rng_conve_masks.argtypes
@@ -152,6 +157,38 @@ def transe_enqueue(torch_state: np.ndarray, np_key: int, np_pos: int, R: int, ep
     check(lib().kp_rng_transe_enqueue(_ptr(torch_state), torch_state.size, C.c_void_p(np_key), C.c_void_p(np_pos),
                                       int(R), int(epochs), int(ratio), int(n_entities), _ptr(out)))
     return out[:epochs * 3 * R]
+
+
+def normal_cap() -> int:
+    """Which ATen normal_ kernel this torch runs: 1 for its AVX2 / AVX512 builds, 0 for
+    the scalar default one (kp_rng_normal's ``cap``)."""
+    import torch
+    return 0 if torch.backends.cpu.get_cpu_capability() == "DEFAULT" else 1
+
+
+def rng_normal(state: np.ndarray, n: int, mean: float, std: float, cap: int | None = None) -> np.ndarray:
+    """``torch.empty(n).normal_(mean, std)`` values (n >= 16) from the state blob, advanced in place."""
+    assert state.dtype == np.uint8 and state.flags.c_contiguous
+    out = np.empty(n, np.float32)
+    check(lib().kp_rng_normal(_ptr(state), state.size, int(n), float(mean), float(std),
+                              normal_cap() if cap is None else int(cap), _ptr(out)))
+    return out
+
+
+def transe_calls(state: np.ndarray, np_key: int, np_pos: int, cap: int, D: int, d: int, std: float,
+                 R_base: np.ndarray, R_pt: np.ndarray, epochs: int, ratio: int, n_entities: int,
+                 out: np.ndarray | None):
+    """kp_rng_transe_calls for len(R_base) calls: returns (x_base [n][d], x_pt [n][d]); the
+    epoch draws land in ``out`` back to back (complete after :func:`rng_wait`)."""
+    n = len(R_base)
+    rb = np.ascontiguousarray(R_base, dtype=np.int32)
+    rp = np.ascontiguousarray(R_pt, dtype=np.int32)
+    xb = np.empty((n, d), np.float32)
+    xp = np.empty((n, d), np.float32)
+    check(lib().kp_rng_transe_calls(_ptr(state), state.size, C.c_void_p(np_key), C.c_void_p(np_pos), int(cap),
+                                    int(D), int(d), float(std), n, _ptr(rb), _ptr(rp), int(epochs), int(ratio),
+                                    int(n_entities), _ptr(xb), _ptr(xp), _ptr(out)))
+    return xb, xp
 
 
 def rng_wait():

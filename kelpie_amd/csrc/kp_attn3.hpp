@@ -78,6 +78,9 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_ASM_ALL
 #define KP_ASM_ALL 0  // 1: the asm read form for every DB (ConvE included)
 #endif
+#ifndef KP_BUF_DMA
+#define KP_BUF_DMA 1  // interleaved schedule: LDS-DMA by buffer_load ... lds with scalar offsets
+#endif
 #ifdef KP_DIAG_NO_O
 #define KP_DIAG_O false
 #else
@@ -101,7 +104,15 @@ __host__ __device__ constexpr int split3_row_bytes(int DP) { return 3 * 2 * DP +
 __host__ __device__ constexpr int split3_tile_bytes(int DP) { return 32 * split3_row_bytes(DP); }
 // LDS-DMA pieces (1 KiB) per tile and the LDS bytes of kp_attn3 (two tile buffers)
 __host__ __device__ constexpr int split3_pieces(int DP) { return (split3_tile_bytes(DP) + 1023) / 1024; }
-constexpr size_t attn3_lds_bytes(int DB) { return 2u * 1024u * (size_t)split3_pieces(16 * DB); }
+// the asm read form (see lds_rd_bf8) and, with it, the interleaved schedule and the
+// buffer-descriptor LDS-DMA (KP_BUF_DMA): every wave issues the same number of whole
+// pieces, so a tile buffer is rounded up to a multiple of 4 pieces
+__host__ __device__ constexpr bool attn3_asm(int DB) { return DB > 13 || KP_ASM_ALL; }
+__host__ __device__ constexpr bool attn3_bufdma(int DB) { return attn3_asm(DB) && KP_ILV && KP_BUF_DMA; }
+__host__ __device__ constexpr int attn3_buf_pieces(int DB) {
+  return attn3_bufdma(DB) ? (split3_pieces(16 * DB) + 3) / 4 * 4 : split3_pieces(16 * DB);
+}
+constexpr size_t attn3_lds_bytes(int DB) { return 2u * 1024u * (size_t)attn3_buf_pieces(DB); }
 
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
   h = (__bf16)x;
@@ -222,7 +233,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                                                    float ylo, const double* __restrict__ colpre) {
   constexpr bool WITH_O = MODE != ATT_SOFTMAX;
   constexpr int DP = 16 * DB;
-  constexpr bool ASM = DB > 13 || KP_ASM_ALL;  // read form (see lds_rd_bf8)
+  constexpr bool ASM = attn3_asm(DB);  // read form (see lds_rd_bf8)
   // interleaved schedule of the asm read form (KP_ILV, default on): reads two k-steps /
   // O blocks ahead, one per MFMA issue gap, order pinned by sched_barrier
   constexpr bool ILV = ASM && KP_ILV;
@@ -231,7 +242,8 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   constexpr int KT = 32;
   constexpr int PART_B = 2 * DP;
   constexpr int ROW_B = split3_row_bytes(DP);
-  constexpr int PIECES = split3_pieces(DP);
+  constexpr bool BUFDMA = attn3_bufdma(DB);
+  constexpr int PIECES = attn3_buf_pieces(DB);  // whole 1-KiB LDS-DMA pieces per tile buffer
   constexpr int BUF_B = 1024 * PIECES;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds3[];  // [2][BUF_B]
 
@@ -248,12 +260,24 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 
   // linear LDS-DMA of a tile: piece p = bytes [1024 p, 1024 p + 1024) of the tile,
   // wave w issues p = w, w + 4, ... (the image has >= 1 KiB of slack past its end)
+  // buffer-descriptor form (BUFDMA): the descriptor covers the whole image (rows padded to
+  // whole tiles plus 1 KiB of slack), the per-lane part is the constant voffset 16 lane and
+  // everything that varies per piece is scalar (soffset, M0): no VALU per piece
+  const __amdgpu_buffer_rsrc_t e3rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(E3), (short)0, (int)((n_ent + 31) / 32 * 32 * ROW_B + 1024), 0x00020000);
+  auto bdma = [&](int tile, int buf, int p) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        e3rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)), 16,
+        16 * lane, (key_begin + tile * KT) * ROW_B + 1024 * p, 0, 0);
+  };
   auto issue = [&](int tile, int buf) {
     const uint8_t* src = E3 + (size_t)(key_begin + tile * KT) * ROW_B + 16 * lane;
 #pragma unroll
     for (int p0 = 0; p0 < PIECES; p0 += 4) {
       const int p = p0 + w;
-      if (p < PIECES)
+      if constexpr (BUFDMA)
+        bdma(tile, buf, p);
+      else if (p < PIECES)
         glds16<ASM>(reinterpret_cast<const float*>(src + 1024 * p),
                __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)));
     }
@@ -274,7 +298,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   constexpr bool SPREAD2 = SPREAD && ILV && KP_DMA_SPREAD >= 2;
   auto issue_piece = [&](int tile, int buf, int k) {
     const int p = 4 * k + w;
-    if (p < PIECES)
+    if constexpr (BUFDMA)
+      bdma(tile, buf, p);
+    else if (p < PIECES)
       glds16<ASM>(reinterpret_cast<const float*>(E3 + (size_t)(key_begin + tile * KT) * ROW_B + 16 * lane + 1024 * p),
              __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)));
   };
@@ -366,6 +392,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
       for (int t = 0; t < ntiles; ++t) {
         const int k0 = key_begin + t * KT;
         KP3_STAMP(st0);
+        // next tile's DMA: with BUFDMA every tile issues it (the last one re-reads its own
+        // rows into the idle buffer) so no piece sits behind a branch
+        const bool dma_on = BUFDMA || t + 1 < ntiles;
+        const int tn = t + 1 < ntiles ? t + 1 : t;
         const uint32_t tb = lds0 + (uint32_t)((t & 1) * BUF_B);
 #if !defined(KP_ATTN_NODMA) && defined(KP_DMA_EARLY)
         // the other buffer was released by the previous tile's closing barrier
@@ -425,8 +455,8 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
               lgkm_wait<0>();
             __builtin_amdgcn_sched_barrier(0);
 #if !defined(KP_ATTN_NODMA)
-            if (SPREAD2 && t + 1 < ntiles) {
-              dma_slot(t + 1, (t + 1) & 1, s);
+            if (SPREAD2 && dma_on) {
+              dma_slot(tn, (t + 1) & 1, s);
               __builtin_amdgcn_sched_barrier(0);
             }
 #endif
@@ -597,15 +627,15 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #pragma unroll
           for (int m = 0; m < DB; ++m) {
 #if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
-            if (SPREAD && !SPREAD2 && t + 1 < ntiles) {
+            if (SPREAD && !SPREAD2 && dma_on) {
               if (m < NPW) {
-                issue_piece(t + 1, (t + 1) & 1, m);
+                issue_piece(tn, (t + 1) & 1, m);
 #ifdef KP_DIAG_DMA_LGKM0
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // diagnostic: drain after each piece
 #endif
               }
               if (m == DB - 1)
-                for (int k = DB; k < NPW; ++k) issue_piece(t + 1, (t + 1) & 1, k);
+                for (int k = DB; k < NPW; ++k) issue_piece(tn, (t + 1) & 1, k);
             }
 #endif
             if constexpr (ILV) {
@@ -617,8 +647,8 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                 lgkm_wait<0>();
               __builtin_amdgcn_sched_barrier(0);
 #if !defined(KP_ATTN_NODMA)
-              if (SPREAD2 && t + 1 < ntiles) {
-                dma_slot(t + 1, (t + 1) & 1, NK + TAIL + m);
+              if (SPREAD2 && dma_on) {
+                dma_slot(tn, (t + 1) & 1, NK + TAIL + m);
                 __builtin_amdgcn_sched_barrier(0);
               }
 #endif

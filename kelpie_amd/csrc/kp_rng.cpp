@@ -37,6 +37,7 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
 #include <unistd.h>
 
 #include "kelpie_hip.h"
@@ -124,6 +125,129 @@ struct TorchMt {
     }
   }
 };
+
+// ---------------------------------------------------------------------------------
+// torch.Tensor.normal_ on the CPU generator, float32, contiguous, n >= 16
+// (aten/src/ATen/native/cpu/DistributionTemplates.h normal_fill / normal_fill_AVX2):
+// n uniforms u = (random() & 0xFFFFFF) * 2^-24, Box-Muller over each block of 16
+// (u1 = 1 - u[j], u2 = u[j + 8]), and when 16 does not divide n the last 16 values
+// are redrawn (16 more uniforms) and transformed again.
+//  * cap 1 -- torch built for AVX2 / AVX512 (torch.backends.cpu.get_cpu_capability()):
+//    normal_fill_16_AVX2 with avx_mathfun's log256_ps / sincos256_ps (Cephes
+//    polynomials), every multiply feeding an add contracted to an FMA as the build
+//    does; pinned value for value against torch (tests/test_rng_protocol.py);
+//  * cap 0 -- the scalar kernel: logf / cosf / sinf / sqrtf of libm, no contraction.
+// This file is compiled with -ffp-contract=off: every fused operation below is an
+// explicit fmadd.
+// ---------------------------------------------------------------------------------
+// avx_mathfun's log256_ps and sincos256_ps as torch's AVX2 build runs them: each
+// multiply that feeds an add fused (an explicit fmadd; the rest stay separate, and this
+// file is built with -ffp-contract=off so nothing else is fused)
+inline __m256 v_log(__m256 x) {
+  const __m256 one = _mm256_set1_ps(1.0f);
+  const __m256 invalid = _mm256_cmp_ps(x, _mm256_setzero_ps(), _CMP_LE_OS);
+  x = _mm256_max_ps(x, _mm256_castsi256_ps(_mm256_set1_epi32(0x00800000)));
+  __m256i imm0 = _mm256_srli_epi32(_mm256_castps_si256(x), 23);
+  x = _mm256_and_ps(x, _mm256_castsi256_ps(_mm256_set1_epi32(~0x7f800000)));
+  x = _mm256_or_ps(x, _mm256_set1_ps(0.5f));
+  imm0 = _mm256_sub_epi32(imm0, _mm256_set1_epi32(0x7f));
+  __m256 e = _mm256_add_ps(_mm256_cvtepi32_ps(imm0), one);
+  const __m256 mask = _mm256_cmp_ps(x, _mm256_set1_ps(0.707106781186547524f), _CMP_LT_OS);
+  const __m256 tmp = _mm256_and_ps(x, mask);
+  x = _mm256_sub_ps(x, one);
+  e = _mm256_sub_ps(e, _mm256_and_ps(one, mask));
+  x = _mm256_add_ps(x, tmp);
+  const __m256 z = _mm256_mul_ps(x, x);
+  __m256 y = _mm256_set1_ps(7.0376836292E-2f);
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(-1.1514610310E-1f));
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(1.1676998740E-1f));
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(-1.2420140846E-1f));
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(1.4249322787E-1f));
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(-1.6668057665E-1f));
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(2.0000714765E-1f));
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(-2.4999993993E-1f));
+  y = _mm256_fmadd_ps(y, x, _mm256_set1_ps(3.3333331174E-1f));
+  y = _mm256_mul_ps(y, x);
+  y = _mm256_fmadd_ps(y, z, _mm256_mul_ps(e, _mm256_set1_ps(-2.12194440e-4f)));
+  y = _mm256_fmadd_ps(z, _mm256_set1_ps(-0.5f), y);
+  x = _mm256_add_ps(x, y);
+  x = _mm256_fmadd_ps(e, _mm256_set1_ps(0.693359375f), x);
+  return _mm256_or_ps(x, invalid);
+}
+inline void v_sincos(__m256 x, __m256& s, __m256& c) {
+  __m256 sign_sin = _mm256_and_ps(x, _mm256_castsi256_ps(_mm256_set1_epi32((int)0x80000000)));
+  x = _mm256_and_ps(x, _mm256_castsi256_ps(_mm256_set1_epi32(0x7fffffff)));
+  __m256 y = _mm256_mul_ps(x, _mm256_set1_ps(1.27323954473516f));
+  __m256i imm2 = _mm256_cvttps_epi32(y);
+  imm2 = _mm256_add_epi32(imm2, _mm256_set1_epi32(1));
+  imm2 = _mm256_and_si256(imm2, _mm256_set1_epi32(~1));
+  y = _mm256_cvtepi32_ps(imm2);
+  __m256i imm4 = imm2;
+  const __m256 swap_sign_sin = _mm256_castsi256_ps(_mm256_slli_epi32(_mm256_and_si256(imm2, _mm256_set1_epi32(4)), 29));
+  const __m256 poly = _mm256_castsi256_ps(
+      _mm256_cmpeq_epi32(_mm256_and_si256(imm2, _mm256_set1_epi32(2)), _mm256_setzero_si256()));
+  x = _mm256_fmadd_ps(y, _mm256_set1_ps(-0.78515625f), x);
+  x = _mm256_fmadd_ps(y, _mm256_set1_ps(-2.4187564849853515625e-4f), x);
+  x = _mm256_fmadd_ps(y, _mm256_set1_ps(-3.77489497744594108e-8f), x);
+  imm4 = _mm256_sub_epi32(imm4, _mm256_set1_epi32(2));
+  imm4 = _mm256_andnot_si256(imm4, _mm256_set1_epi32(4));
+  const __m256 sign_cos = _mm256_castsi256_ps(_mm256_slli_epi32(imm4, 29));
+  sign_sin = _mm256_xor_ps(sign_sin, swap_sign_sin);
+  const __m256 z = _mm256_mul_ps(x, x);
+  __m256 yc = _mm256_set1_ps(2.443315711809948E-005f);
+  yc = _mm256_fmadd_ps(yc, z, _mm256_set1_ps(-1.388731625493765E-003f));
+  yc = _mm256_fmadd_ps(yc, z, _mm256_set1_ps(4.166664568298827E-002f));
+  yc = _mm256_mul_ps(yc, z);
+  yc = _mm256_fmadd_ps(yc, z, _mm256_sub_ps(_mm256_setzero_ps(), _mm256_mul_ps(z, _mm256_set1_ps(0.5f))));
+  yc = _mm256_add_ps(yc, _mm256_set1_ps(1.0f));
+  __m256 ys = _mm256_set1_ps(-1.9515295891E-4f);
+  ys = _mm256_fmadd_ps(ys, z, _mm256_set1_ps(8.3321608736E-3f));
+  ys = _mm256_fmadd_ps(ys, z, _mm256_set1_ps(-1.6666654611E-1f));
+  ys = _mm256_mul_ps(ys, z);
+  ys = _mm256_fmadd_ps(ys, x, x);
+  const __m256 ysin2 = _mm256_and_ps(poly, ys), ysin1 = _mm256_andnot_ps(poly, yc);
+  ys = _mm256_sub_ps(ys, ysin2);
+  yc = _mm256_sub_ps(yc, ysin1);
+  s = _mm256_xor_ps(_mm256_add_ps(ysin1, ysin2), sign_sin);
+  c = _mm256_xor_ps(_mm256_add_ps(yc, ys), sign_cos);
+}
+
+inline void normal_fill16(float* d, float mean, float std_, int cap) {
+  if (cap) {
+    const __m256 u1 = _mm256_sub_ps(_mm256_set1_ps(1.0f), _mm256_loadu_ps(d));
+    const __m256 u2 = _mm256_loadu_ps(d + 8);
+    const __m256 radius = _mm256_sqrt_ps(_mm256_mul_ps(_mm256_set1_ps(-2.0f), v_log(u1)));
+    const __m256 theta = _mm256_mul_ps(_mm256_set1_ps((float)(2.0f * 3.14159265358979323846)), u2);
+    __m256 sn, cs;
+    v_sincos(theta, sn, cs);
+    _mm256_storeu_ps(d, _mm256_fmadd_ps(_mm256_mul_ps(radius, cs), _mm256_set1_ps(std_), _mm256_set1_ps(mean)));
+    _mm256_storeu_ps(d + 8, _mm256_fmadd_ps(_mm256_mul_ps(radius, sn), _mm256_set1_ps(std_), _mm256_set1_ps(mean)));
+    return;
+  }
+  for (int j = 0; j < 8; ++j) {
+    const float u1 = 1.0f - d[j], u2 = d[j + 8];
+    const float radius = std::sqrt(-2.0f * std::log(u1));
+    const float theta = (float)(2.0f * 3.14159265358979323846 * (double)u2);
+    d[j] = radius * std::cos(theta) * std_ + mean;
+    d[j + 8] = radius * std::sin(theta) * std_ + mean;
+  }
+}
+
+// torch.empty(n).normal_(mean, std) for n >= 16 (normal_fill): advances mt like torch
+template <class Mt>
+void normal_draw(Mt& mt, int64_t n, float mean, float std_, int cap, float* out) {
+  std::vector<uint32_t> r((size_t)n);
+  mt.fill(r.data(), (size_t)n);
+  for (int64_t i = 0; i < n; ++i) out[i] = (float)(r[(size_t)i] & 0xFFFFFFu) * (1.0f / 16777216.0f);
+  for (int64_t i = 0; i + 16 <= n; i += 16) normal_fill16(out + i, mean, std_, cap);
+  if (n % 16) {
+    uint32_t t[16];
+    mt.fill(t, 16);
+    float* d = out + n - 16;
+    for (int i = 0; i < 16; ++i) d[i] = (float)(t[i] & 0xFFFFFFu) * (1.0f / 16777216.0f);
+    normal_fill16(d, mean, std_, cap);
+  }
+}
 
 // numpy's legacy MT19937 (numpy/random/src/mt19937/mt19937.h: {uint32 key[624]; int pos}):
 // regenerate when pos reaches 624.  Works on a local copy; the current block is kept
@@ -429,6 +553,29 @@ class DrawQueue {
   pid_t pid_ = 0;
 };
 
+// Queue one slot's TransE epoch draws (see the deferred protocol above) from the torch
+// generator `mt`, which is advanced past the slot's randints.
+int te_enqueue(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t ratio, uint32_t nent,
+               int32_t* out) {
+  if (R == 0 || epochs == 0) return KP_OK;  // np.random.shuffle of an empty array draws nothing
+  const TorchMt snap = mt;
+  mt.skip((uint64_t)epochs * 2u * (uint64_t)ratio * (uint64_t)R);
+  Task seq = [=](Scratch& sc) { te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx); };
+  Task fill = [=](Scratch& sc) {
+    TorchMt m = snap;
+    te_randints(m, R, epochs, ratio, nent, out, sc.draw);
+  };
+  if (!DrawQueue::get().enqueue(seq, fill)) {
+    // no worker threads: finish every queued task first (numpy order), then this one
+    const int rc = DrawQueue::get().wait();
+    if (rc != KP_OK) return rc;
+    Scratch sc;
+    seq(sc);
+    fill(sc);
+  }
+  return KP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -475,23 +622,51 @@ int kp_rng_transe_enqueue(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* n
   try {
     TorchMt mt;
     mt.load(ts);
-    TorchMt adv = mt;
-    adv.skip((uint64_t)epochs * 2u * (uint64_t)ratio * (uint64_t)R);
+    const int rc = te_enqueue(mt, np_key, np_pos, R, epochs, ratio, (uint32_t)n_entities, out);
+    if (rc != KP_OK) return rc;
+    mt.store(ts);
+  } catch (...) {
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t cap, int32_t D,
+                        int32_t d, float xavier_std, int32_t n, const int32_t* R_base, const int32_t* R_pt,
+                        int32_t epochs, int32_t ratio, int64_t n_entities, float* x_base, float* x_pt,
+                        int32_t* out) {
+  if (!ts || tlen < 24 + kN * 8 || !np_key || !np_pos || (cap != 0 && cap != 1) || D < 0 || d < 16 || n < 0 ||
+      (n > 0 && (!R_base || !R_pt || !x_base || !x_pt)) || epochs < 0 || ratio < 1 || n_entities < 1 ||
+      n_entities >= (1LL << 32))
+    return KP_EINVAL;
+  if (*np_pos < 0 || *np_pos > kN) return KP_EINVAL;
+  int64_t words = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if (R_base[i] < -1 || R_pt[i] < -1) return KP_EINVAL;
+    words += (int64_t)epochs * 3 * (std::max(R_base[i], 0) + std::max(R_pt[i], 0));
+  }
+  if (words > 0 && !out) return KP_EINVAL;
+  try {
+    TorchMt mt;
+    mt.load(ts);
     const uint32_t nent = (uint32_t)n_entities;
-    Task seq = [=](Scratch& sc) { te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx); };
-    Task fill = [=](Scratch& sc) {
-      TorchMt m = mt;
-      te_randints(m, R, epochs, ratio, nent, out, sc.draw);
-    };
-    if (!DrawQueue::get().enqueue(seq, fill)) {
-      // no worker threads: finish every queued task first (numpy order), then this one
-      const int rc = DrawQueue::get().wait();
-      if (rc != KP_OK) return rc;
-      Scratch sc;
-      seq(sc);
-      fill(sc);
+    int32_t* o = out;
+    for (int32_t i = 0; i < n; ++i) {
+      mt.skip((uint64_t)D);  // torch.rand(1, D): one output per element, values unused
+      normal_draw(mt, d, 0.0f, xavier_std, cap, x_base + (size_t)i * d);  // base KelpieTransE's xavier_normal_
+      if (R_base[i] >= 0) {
+        const int rc = te_enqueue(mt, np_key, np_pos, R_base[i], epochs, ratio, nent, o);
+        if (rc != KP_OK) return rc;
+        o += (size_t)epochs * 3 * R_base[i];
+      }
+      normal_draw(mt, d, 0.0f, xavier_std, cap, x_pt + (size_t)i * d);  // the post-trained one's
+      if (R_pt[i] >= 0) {
+        const int rc = te_enqueue(mt, np_key, np_pos, R_pt[i], epochs, ratio, nent, o);
+        if (rc != KP_OK) return rc;
+        o += (size_t)epochs * 3 * R_pt[i];
+      }
     }
-    adv.store(ts);
+    mt.store(ts);
   } catch (...) {
     return KP_ENOMEM;
   }
@@ -568,6 +743,15 @@ int kp_rng_bernoulli_bits(uint8_t* st, size_t len, uint64_t n, double p, uint32_
   } catch (...) {
     return KP_ENOMEM;
   }
+  return KP_OK;
+}
+
+int kp_rng_normal(uint8_t* ts, size_t tlen, int64_t n, float mean, float std_, int32_t cap, float* out) {
+  if (!ts || tlen < 24 + kN * 8 || n < 16 || !out || (cap != 0 && cap != 1)) return KP_EINVAL;
+  TorchMt mt;
+  mt.load(ts);
+  normal_draw(mt, n, mean, std_, cap, out);
+  mt.store(ts);
   return KP_OK;
 }
 

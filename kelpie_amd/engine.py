@@ -135,6 +135,7 @@ class PostTrainingEngine(RelevanceEngine):
         RelevanceEngine.__init__(self, model=model, dataset=dataset)
         self.hp = hp
         self.rng = rng or ReferenceRNG()
+        self._fused = []  # TransE calls whose draws _flush_fused makes in one library call
         self._kp_hp = model.kp_hp(hp)
         if getattr(model, "is_kelpie", False):
             raise Exception("Already a post-trainable KelpieModel.")
@@ -165,6 +166,8 @@ class PostTrainingEngine(RelevanceEngine):
         and append its slots.  Returns (pt_slot, base_key)."""
         pred = tuple(int(v) for v in pred)
         view = self._get_kelpie_dataset(pred[0])
+        if getattr(self.model, "fused_call_draws", False):
+            return self._schedule_fused(pred, view, triples, mode, slots, pending_base)
         init = self.rng.rand_init(self.model.dimension)
         x_base = self.model.kelpie_init(init, self.rng)  # base KelpieModel is built every call (A-Q6)
         kp = view.as_kelpie_triple(pred)
@@ -176,6 +179,55 @@ class PostTrainingEngine(RelevanceEngine):
         filt = view.filter_for(kp[1], delta.get(kp[1]))
         slots.append(self._slot(x_pt, rows, kp, filt))
         return len(slots) - 1, pred
+
+    def _schedule_fused(self, pred, view, triples, mode, slots, pending_base):
+        """_schedule for TransE: the call's slots are appended now and its draws are
+        queued; :meth:`_flush_fused` makes every queued call's draws in one library call
+        (ReferenceRNG.transe_calls), in order.  The row edit draws nothing, so it runs
+        first; if it raises, the draws the reference makes before raising (everything but
+        the post-trained model's epochs) are consumed, then the error propagates."""
+        kp = view.as_kelpie_triple(pred)
+        need_base = pred not in self.base_pt_results and pred not in pending_base
+        err = None
+        try:
+            rows, delta = view.removed(triples) if mode == "necessary" else view.added(triples)
+        except Exception as e:  # noqa: BLE001 -- re-raised below, after the reference's draws
+            err, rows = e, None
+        call = {"R_base": len(view.base_rows) if need_base else -1, "R_pt": -1 if err else len(rows),
+                "base": None, "pt": None}
+        if need_base:
+            pending_base[pred] = len(slots)
+            call["base"] = _Slot(x0=None, rows=view.base_rows, rng=None, pred=kp, filt=list(view.filter_for(kp[1])))
+            slots.append(call["base"])
+        self._fused.append(call)
+        if err is not None:
+            self._flush_fused()
+            raise err
+        call["pt"] = _Slot(x0=None, rows=rows, rng=None, pred=kp, filt=list(view.filter_for(kp[1], delta.get(kp[1]))))
+        slots.append(call["pt"])
+        return len(slots) - 1, pred
+
+    def _flush_fused(self):
+        calls, self._fused = self._fused, []
+        if not calls:
+            return
+        m, hp = self.model, self.hp
+        xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, [c["R_base"] for c in calls],
+                                              [c["R_pt"] for c in calls], int(hp["epochs"]),
+                                              int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1)
+        for i, c in enumerate(calls):
+            db, dp = draws[i]
+            if c["base"] is not None:
+                c["base"].x0, c["base"].rng = xb[i], db
+            if c["pt"] is not None:
+                c["pt"].x0, c["pt"].rng = xp[i], dp
+
+    def _schedule_all(self, items, checkpoints):
+        """_schedule_multi, with every queued TransE call's draws made before it returns or raises."""
+        try:
+            return self._schedule_multi(items, checkpoints)
+        finally:
+            self._flush_fused()
 
     def _run(self, slots, ctx=None):
         """Post-train and rank ``slots`` on the device.  With ``self.sharding`` only this
@@ -265,7 +317,7 @@ class PostTrainingEngine(RelevanceEngine):
         t0 = time.perf_counter()
         self._deferred_error = None
         with self.rng.deferred():
-            slots, pending, jobs = self._schedule_multi(items, checkpoints)
+            slots, pending, jobs = self._schedule_all(items, checkpoints)
         t_sched = time.perf_counter() - t0
         self._run(slots)
         self._collect(slots, self.last_batch_stats)
@@ -299,7 +351,7 @@ class PostTrainingEngine(RelevanceEngine):
             self.set_cache()
             self._deferred_error = None
             with self.rng.deferred():
-                slots, _, _ = self._schedule_multi(items, None)
+                slots, _, _ = self._schedule_all(items, None)
             self._deferred_error = None
             for ctx in ctxs[1:]:
                 self._run(slots, ctx=ctx)
@@ -357,7 +409,7 @@ class PostTrainingEngine(RelevanceEngine):
                 t0 = time.perf_counter()
                 self._deferred_error = None
                 with self.rng.deferred():
-                    slots, pending, jobs = self._schedule_multi(items, None)
+                    slots, pending, jobs = self._schedule_all(items, None)
                 err, self._deferred_error = self._deferred_error, None
                 t_sched = time.perf_counter() - t0
                 # batch b uses context b % depth: the batch before it on that context is done
@@ -408,6 +460,7 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
                     return slots, pending, jobs
                 pj.append(idx)
                 if checkpoints is not None:
+                    self._flush_fused()
                     checkpoints.append(StateCheckpoint())
             jobs.append(pj)
         return slots, pending, jobs
@@ -471,6 +524,7 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
                         return slots, pending, jobs
                 pj.append(rj)
                 if checkpoints is not None:
+                    self._flush_fused()
                     checkpoints.append(StateCheckpoint())
             jobs.append(pj)
         return slots, pending, jobs

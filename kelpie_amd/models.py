@@ -147,6 +147,12 @@ class TransE(FrozenModel):
         # KelpieTransE: xavier_normal_ overwrites the init copy (transe.py:93-95)
         return rng.xavier_row(self.dimension)
 
+    @property
+    def fused_call_draws(self):
+        """Every draw of a compute_relevance call can come from one library call
+        (ReferenceRNG.transe_call): its normal_ replica needs rows of >= 16 values."""
+        return self.dimension >= 16
+
     def kp_hp(self, hp):
         return _lib.HP(optimizer=_lib.KP_OPT["Adam"], epochs=int(hp["epochs"]), batch_size=int(hp["batch_size"]),
                        lr=float(hp["lr"]), beta1=0.9, beta2=0.999, eps=1e-8,

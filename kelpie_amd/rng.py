@@ -56,12 +56,19 @@ def _np_mt_state_address() -> int:
 _outstanding = False
 
 
+# every arena the library's workers may still be writing into stays referenced here
+# until sync(): a caller that drops its draw arrays early must not free them under the
+# workers
+_inflight = []
+
+
 def sync():
     """Wait for every queued TransE draw (the numpy global state is then current)."""
     global _outstanding
     if _outstanding:
         _outstanding = False
         _lib.rng_wait()
+    _inflight.clear()
 
 
 class ReferenceRNG:
@@ -95,6 +102,7 @@ class ReferenceRNG:
     def _take(self, n: int) -> np.ndarray:
         if self._arena is None or self._arena_pos + n > self._arena.size:
             self._arena, self._arena_pos = np.empty(max(self._ARENA, n), np.int32), 0
+            _inflight.append(self._arena)
         out = self._arena[self._arena_pos:self._arena_pos + n]
         self._arena_pos += n
         return out
@@ -150,6 +158,34 @@ class ReferenceRNG:
             out = _lib.transe_epochs(st, addr, addr + 4 * 624, R, epochs, ratio, n_entities)
         _set_state(st)
         return out
+
+    def transe_calls(self, D: int, d: int, R_base, R_pt, epochs: int, ratio: int, n_entities: int):
+        """Every draw of n TransE compute_relevance calls in one library call
+        (kp_rng_transe_calls).  Per call: ``torch.rand(1, D)``, the base row's
+        ``xavier_normal_``, the base post-training's epoch draws (``R_base[i]`` >= 0),
+        the post-trained row's ``xavier_normal_`` and its epoch draws (``R_pt[i]`` >= 0).
+        Returns ``(x_base [n][d], x_pt [n][d], [(draws_base, draws_pt)] * n)``; the draws
+        are complete on leaving :meth:`deferred` (or at once outside it)."""
+        global _outstanding
+        st = _get_state()
+        addr = _np_mt_state_address()
+        if not self._defer_depth:
+            sync()
+        sizes = [(epochs * 3 * max(rb, 0), epochs * 3 * max(rp, 0)) for rb, rp in zip(R_base, R_pt)]
+        total = sum(a + b for a, b in sizes)
+        out = (self._take(total) if self._defer_depth else np.empty(total, np.int32)) if total else None
+        xb, xp = _lib.transe_calls(st, addr, addr + 4 * 624, _lib.normal_cap(), D, d,
+                                   float(np.float32(math.sqrt(2.0 / float(d + 1)))), R_base, R_pt, epochs, ratio,
+                                   n_entities, out)
+        _outstanding = True
+        if not self._defer_depth:
+            sync()
+        _set_state(st)
+        draws, off, empty = [], 0, np.zeros(0, np.int32)
+        for a, b in sizes:
+            draws.append((out[off:off + a] if a else empty, out[off + a:off + a + b] if b else empty))
+            off += a + b
+        return xb, xp, draws
 
     def conve_masks(self, n_rows_per_step, dim: int, p_drop: float) -> np.ndarray:
         """Hidden-dropout keep bits for every step, packed per step in uint32 words."""

@@ -178,3 +178,90 @@ def test_deferred_conve_masks_match_torch_dropout_sequence():
             off += nw
         assert off == words.size
     assert torch.equal(torch.rand(2), after)
+
+
+_NORMAL_CHECK = r"""
+import math, random, sys
+import numpy as np, torch
+from kelpie_amd import _lib
+cap = _lib.normal_cap()
+bad = 0
+for trial in range(int(sys.argv[1])):
+    rr = random.Random(trial)
+    torch.manual_seed(trial)
+    torch.rand(rr.randint(0, 1500))
+    st = torch.get_rng_state().numpy().copy()
+    d = rr.choice([16, 17, 33, 50, 100, 200, 256, 400])
+    std = math.sqrt(2.0 / (d + 1))
+    ref = torch.empty(1, d).normal_(0.0, std).numpy()[0]
+    out = _lib.rng_normal(st, d, 0.0, std, cap)
+    bad += int((out != ref).sum()) + int(not np.array_equal(st, torch.get_rng_state().numpy()))
+print(cap, bad)
+"""
+
+
+@pytest.mark.parametrize("capability", [None, "default"])
+def test_normal_matches_torch_bit_for_bit(capability):
+    """kp_rng_normal equals torch's normal_ value for value and leaves the same generator
+    state, for the CPU kernel this torch runs (AVX2 / AVX512: avx_mathfun with FMA
+    contraction) and, in a child process with ATEN_CPU_CAPABILITY=default, for the
+    scalar kernel (libm)."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    if capability:
+        env["ATEN_CPU_CAPABILITY"] = capability
+    out = subprocess.run([sys.executable, "-c", _NORMAL_CHECK, "400"], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    cap, bad = out.stdout.split()
+    if capability == "default":
+        assert cap == "0"
+    assert bad == "0", out.stdout
+
+
+def test_fused_transe_calls_match_reference_sequence():
+    """ReferenceRNG.transe_calls (one library call for several compute_relevance calls)
+    equals the reference's sequence per call, rand(1, D) -> xavier_normal_ -> base epochs
+    -> xavier_normal_ -> pt epochs, inside and outside deferred(), with and without the
+    base slot, and leaves both generators where the sequence does."""
+    import math
+    ratio, N, E, d = 5, 301, 4, 40
+    batches = [[(12, 7), (-1, 30)], [(0, 5)], [(33, -1), (-1, 0), (-1, 9)]]
+    torch.manual_seed(11)
+    np.random.seed(11)
+    rng = ReferenceRNG()
+    got = []
+    with rng.deferred():
+        for b in batches[:2]:
+            got.append(rng.transe_calls(d, d, [x[0] for x in b], [x[1] for x in b], E, ratio, N))
+    got.append(rng.transe_calls(d, d, [x[0] for x in batches[2]], [x[1] for x in batches[2]], E, ratio, N))
+    after = (torch.rand(3), np.random.randint(0, 1 << 30, 4))
+    torch.manual_seed(11)
+    np.random.seed(11)
+    std = math.sqrt(2.0 / (d + 1))
+
+    def epochs(R):
+        out = []
+        rows = np.arange(R * 3).reshape(R, 3)
+        for _ in range(E):
+            np.random.shuffle(rows)
+            ents = torch.randint(high=N, size=(ratio * R,))
+            hot = torch.randint(high=2, size=(ratio * R,))
+            out.append(np.stack([rows[:, 0] // 3, ents[:R].numpy(), hot[:R].numpy()]))
+        return np.concatenate(out).reshape(-1) if R > 0 else np.zeros(0, np.int64)
+
+    for b, (xb, xp, draws) in zip(batches, got):
+        for i, (Rb, Rp) in enumerate(b):
+            torch.rand(1, d)
+            assert np.array_equal(torch.empty(1, d).normal_(0.0, std).numpy()[0], xb[i])
+            if Rb >= 0:
+                assert np.array_equal(epochs(Rb), draws[i][0])
+            assert np.array_equal(torch.empty(1, d).normal_(0.0, std).numpy()[0], xp[i])
+            if Rp >= 0:
+                assert np.array_equal(epochs(Rp), draws[i][1])
+    assert torch.equal(torch.rand(3), after[0])
+    assert np.array_equal(np.random.randint(0, 1 << 30, 4), after[1])

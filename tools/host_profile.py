@@ -61,7 +61,7 @@ def main():
         if prof:
             prof.enable()
         with eng.rng.deferred():
-            slots, _, _ = eng._schedule_multi(batches[k], None)
+            slots, _, _ = eng._schedule_all(batches[k], None)
         if prof:
             prof.disable()
         dt = time.perf_counter() - t0
