@@ -119,6 +119,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _heartbeat(every_s=30.0):
+    """A line on stderr every ``every_s`` seconds from a daemon thread, so a long silent
+    phase (graph building, the CPU-baseline leg at YAGO3-10 size) shows progress."""
+    import threading
+    import time
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(every_s)
+            log(f"[bench] alive {time.time() - t0:.0f}s")
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def build(wl, device, rank):
     from kelpie_amd import ComplEx, ConvE, Dataset, TransE, synth
     t0 = time.time()
@@ -282,6 +298,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--preds-per-step", type=int, default=None, help="override the workload's predictions per step")
     args = ap.parse_args()
+    _heartbeat()
 
     import torch
     from kelpie_amd import distributed as kd

@@ -164,6 +164,22 @@ int kp_convertible(kp_ctx* ctx, int32_t n, const int32_t* heads, int32_t rel, in
 int kp_predict_tails(kp_ctx* ctx, int32_t n, const int32_t* triples, const int32_t* filt_off, const int32_t* filt,
                      float* out_score, int64_t* out_rank);
 
+/* One epoch of MultiClassNLLOptimizer.epoch (src/link_prediction/optimization/
+ * multiclass_nll_optimizer.py:101-135; ComplEx.forward complex.py:58-86, N3
+ * regularizers.py) on the context's OWN tables, for the retraining of
+ * verify_explanations.py:141-143 / :230-232: triples [n][3] are train()'s stack of the
+ * training triples and their inverses (:66-67), perm [n] this epoch's
+ * torch.randperm(n) (:102; RNG-as-input), batches of min(hp->batch_size, n) starting
+ * every hp->batch_size rows (:112-118).  The optimizer state (Adagrad / Adam / SGD,
+ * hp->optimizer) persists across calls and restarts at epoch == 0.  ComplEx contexts
+ * only (KP_EINVAL otherwise). */
+int kp_train_epoch(kp_ctx* ctx, const kp_hp* hp, int32_t n, const int32_t* triples, const int32_t* perm,
+                   int32_t epoch);
+
+/* Copy the context's tables to the host: entity [n_ent][dim], relation [n_rel2][dim]
+ * (the trained model's state_dict tensors). */
+int kp_read_tables(kp_ctx* ctx, float* entity, float* relation);
+
 /* Data-poisoning relevance, ComplEx (src/relevance_engines/data_poisoning_engine.py:
  * DPEngine.get_gradient :21-49, NecessaryDPEngine.compute_relevance :52-94,
  * SufficientDPEngine.compute_individual_relevance :97-137; the other models have no

@@ -22,7 +22,7 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_rng_conve_masks_enqueue", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
            "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals", "kp_rng_normal",
-           "kp_rng_transe_calls"]
+           "kp_rng_transe_calls", "kp_train_epoch", "kp_read_tables"]
 
 
 class ModelDesc(C.Structure):
@@ -85,6 +85,8 @@ def lib():
                                            C.c_int32, C.c_int64, C.c_void_p]
         L.kp_rng_transe_enqueue.argtypes = L.kp_rng_transe_epochs.argtypes
         L.kp_rng_wait.argtypes = []
+        L.kp_train_epoch.argtypes = [C.c_void_p, C.POINTER(HP), C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
+        L.kp_read_tables.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_rng_normal.argtypes = [C.c_void_p, C.c_size_t, C.c_int64, C.c_float, C.c_float, C.c_int32, C.c_void_p]
         L.kp_rng_transe_calls.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                           C.c_int32, C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
@@ -298,6 +300,20 @@ class Context:
         check(lib().kp_predict_tails(self.h, len(t), _ptr(t), _ptr(filt_off), _ptr(filt), _ptr(score), _ptr(rank)),
               self.h)
         return score, rank
+
+    def train_epoch(self, hp: HP, triples, perm, epoch: int):
+        """kp_train_epoch: one optimizer epoch on this context's own tables."""
+        t = np.ascontiguousarray(np.asarray(triples, dtype=np.int32).reshape(-1, 3))
+        pm = np.ascontiguousarray(perm, dtype=np.int32)
+        assert len(pm) == len(t)
+        check(lib().kp_train_epoch(self.h, C.byref(hp), len(t), _ptr(t), _ptr(pm), int(epoch)), self.h)
+
+    def read_tables(self, n_rel2: int):
+        """kp_read_tables: (entity [n_ent][dim], relation [n_rel2][dim]) float32."""
+        E = np.zeros((self.n_ent, self.dim), np.float32)
+        R = np.zeros((n_rel2, self.dim), np.float32)
+        check(lib().kp_read_tables(self.h, _ptr(E), _ptr(R)), self.h)
+        return E, R
 
     def dp_relevance(self, items, epsilon, lambd, step_sign, rel_sign):
         """kp_dp_relevance: items int [n, 7] -> float32 [n]."""

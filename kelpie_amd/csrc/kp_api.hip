@@ -112,6 +112,7 @@ int kp_ctx_destroy(kp_ctx* c) {
     if (p) (void)hipFree(p);
   for (auto& b : c->ws) b.release();
   c->e3.release();
+  train_state_free(c);
   for (auto e : c->evpool) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -187,6 +188,27 @@ int kp_convertible(kp_ctx* c, int32_t n, const int32_t* heads, int32_t rel, int3
       KP_HIP(hipStreamSynchronize(c->stream));
     }
     for (DevBuf* b : {&bS, &bH, &bR, &bFo, &bF, &bK}) b->release();
+  });
+}
+
+int kp_train_epoch(kp_ctx* c, const kp_hp* hp, int32_t n, const int32_t* triples, const int32_t* perm,
+                   int32_t epoch) {
+  if (!c || !hp || n <= 0 || !triples || !perm || epoch < 0) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_HIP(hipSetDevice(c->device));
+    complex_train_epoch(c, hp, n, triples, perm, epoch);
+  });
+}
+
+int kp_read_tables(kp_ctx* c, float* entity, float* relation) {
+  if (!c || !entity || !relation) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_HIP(hipSetDevice(c->device));
+    KP_HIP(hipStreamSynchronize(c->stream));
+    KP_HIP(hipMemcpy2D(entity, sizeof(float) * c->dim, c->dE, sizeof(float) * c->dp, sizeof(float) * c->dim,
+                       c->n_ent, hipMemcpyDeviceToHost));
+    KP_HIP(hipMemcpy2D(relation, sizeof(float) * c->dim, c->dR, sizeof(float) * c->dp, sizeof(float) * c->dim,
+                       c->n_rel2, hipMemcpyDeviceToHost));
   });
 }
 

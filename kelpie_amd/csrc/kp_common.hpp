@@ -68,6 +68,8 @@ struct Timing {
   double hot_work = 0.0;  // work units of the dominant kernel (see kp_last_timing)
 };
 
+struct kp_train_state;  // kp_train.hip: optimizer state of a full-model training run
+
 struct kp_ctx {
   int device = 0;
   int n_cu = 256;  // compute units of the device (one attention workgroup per CU)
@@ -99,6 +101,7 @@ struct kp_ctx {
   DevBuf e3ts, e3pre;      // kp_attn3's fp64 tile sums / prefix sums of dE over tiles
   bool e3pre_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
+  kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<double, double>> hot_pairs;  // (work units, seconds) per hot launch
   std::vector<double> hot_iv;  // [start, end] per hot launch, seconds since the device's time base
@@ -174,6 +177,9 @@ void criage_relevance(kp_ctx* c, int n, const int32_t* items, int n_ents, const 
 // shared rank kernel launcher (kp_rank.hip): scores [n][ld] already on device,
 // column `kcol` = kelpie score (or -1 when absent)
 void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld, int act);
+// kp_train.hip: one MultiClassNLLOptimizer epoch on the context's tables (ComplEx)
+void complex_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* triples, const int32_t* perm, int epoch);
+void train_state_free(kp_ctx* c);
 // out[z][m][n] = act(sum_{k in split z} A[m][k] B[n][k] + (z == 0 ? bias[n] : 0)), fp32 MFMA
 void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
                      int ldo, const float* bias, int act, int ksplit);

@@ -172,6 +172,45 @@ class Dataset:
     def replace_entity_in_triples(triples, old_entity, new_entity):
         return [Dataset.replace_entity_in_triple(t, old_entity, new_entity) for t in triples]
 
+    # ------------------------------------------------------------------ edits (verification)
+    # dataset.py:242-280, the edits verify_explanations.py makes on a deep copy: the
+    # training rows are filtered / appended, and the DIRECT (s, p) filter keys and the
+    # training-triple index follow; the inverse keys are left as they are, as there.
+    def copy(self):
+        import copy
+        return copy.deepcopy(self)
+
+    def add_training_triple(self, triple):
+        s, p, o = (int(v) for v in triple)
+        self._train = np.vstack([self._train, np.array([[s, p, o]], dtype=np.int64)])
+        self.entity_to_training_triples[s].append((s, p, o))
+        self.entity_to_training_triples[o].append((s, p, o))
+        self.entity_to_degree[s] = self.entity_to_degree.get(s, 0) + 1
+        self.entity_to_degree[o] = self.entity_to_degree.get(o, 0) + 1
+        self.to_filter[(s, p)].append(o)
+        self.train_to_filter[(s, p)].append(o)
+
+    def add_training_triples(self, triples):
+        for t in triples:
+            self.add_training_triple(t)
+
+    def remove_training_triple(self, triple):
+        s, p, o = (int(v) for v in triple)
+        t = self._train
+        self._train = np.ascontiguousarray(t[~((t[:, 0] == s) & (t[:, 1] == p) & (t[:, 2] == o))])
+        self.entity_to_training_triples[s].remove((s, p, o))  # ValueError when absent, as there
+        if s != o:
+            self.entity_to_training_triples[o].remove((s, p, o))
+        self.entity_to_degree[s] -= 1
+        if s != o:
+            self.entity_to_degree[o] -= 1
+        self.to_filter[(s, p)].remove(o)
+        self.train_to_filter[(s, p)].remove(o)
+
+    def remove_training_triples(self, triples):
+        for t in set(tuple(int(v) for v in x) for x in triples):  # set(triples) order, as there
+            self.remove_training_triple(t)
+
     def labels_triple(self, t):
         s, p, o = t
         return (self.id_to_entity[s], self.id_to_relation[p], self.id_to_entity[o])

@@ -205,7 +205,13 @@ class PostTrainingEngine(RelevanceEngine):
             raise err
         call["pt"] = _Slot(x0=None, rows=rows, rng=None, pred=kp, filt=list(view.filter_for(kp[1], delta.get(kp[1]))))
         slots.append(call["pt"])
+        if len(self._fused) >= self._FUSED_FLUSH:
+            # hand the draws to the library's workers early: their numpy shuffles then run
+            # while this thread edits the next calls' rows
+            self._flush_fused()
         return len(slots) - 1, pred
+
+    _FUSED_FLUSH = 24  # queued TransE calls per library call
 
     def _flush_fused(self):
         calls, self._fused = self._fused, []

@@ -1,0 +1,187 @@
+"""End-to-end verification of explanations (``src/verify_explanations.py``): retrain
+the model from scratch on the training set with the explanations removed (necessary)
+or added for every conversion entity (sufficient), then compare the predictions.
+
+The retraining runs on the device (``kp_train_epoch``, ``csrc/kp_train.hip``); the
+host keeps the reference's random protocol (RNG-as-input): after ``set_seeds(42)``
+the original model's ``init_random=True`` construction (verify_explanations.py:59,
+its draws are consumed before ``load_state_dict``), the new model's initialisation
+(complex.py:28-36: ``torch.rand`` tables scaled by ``init_scale``) and one
+``torch.randperm`` per epoch (multiclass_nll_optimizer.py:102) come from the same
+torch CPU generator, in that order.  Supported: ComplEx with its
+MultiClassNLLOptimizer (Adagrad / Adam / SGD, N3); other models raise
+``NotImplementedError``.
+"""
+from __future__ import annotations
+
+import random
+from collections import defaultdict
+
+import numpy as np
+import torch
+
+from .data import MANY_TO_ONE, ONE_TO_ONE, Dataset
+from .models import ComplEx
+
+
+def set_seeds(seed: int = 42):
+    """utils.set_seeds (src/utils/utils.py:16-21) for the CPU generators."""
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+
+
+def _complex_init(dataset: Dataset, dimension: int, init_scale: float):
+    """ComplEx(dataset, hp, init_random=True) tables (complex.py:28-36), float32."""
+    D = 2 * int(dimension)
+    E = torch.rand(dataset.num_entities, D)
+    R = torch.rand(2 * dataset.num_relations, D)
+    E *= init_scale
+    R *= init_scale
+    return E.numpy(), R.numpy()
+
+
+def retrain(model_name: str, dataset: Dataset, model_params: dict, training: dict, device: int = 0,
+            context_factory=None):
+    """A fresh model (``init_random=True``) trained by its optimizer on
+    ``dataset.training_triples`` (``optimizer.train``, multiclass_nll_optimizer.py:57-99),
+    on the device.  Consumes the torch generator like the reference.
+    ``context_factory(model)``, if given, supplies the model's context (tests)."""
+    if model_name != "ComplEx":
+        raise NotImplementedError(f"device retraining supports ComplEx, not {model_name}")
+    E, R = _complex_init(dataset, model_params["dimension"], model_params["init_scale"])
+    model = ComplEx(dataset, E, R, init_scale=model_params["init_scale"], device=device)
+    if context_factory is not None:
+        model._ctx = context_factory(model)
+    hp = model.kp_hp(training)
+    train = dataset.training_triples
+    triples = np.vstack([train, dataset.invert_triples(train)]).astype(np.int32)
+    ctx = model.ctx
+    for epoch in range(int(training["epochs"])):
+        perm = torch.randperm(triples.shape[0]).numpy()
+        ctx.train_epoch(hp, triples, perm, epoch)
+    E2, R2 = ctx.read_tables(2 * dataset.num_relations)
+    model.entity_embeddings, model.relation_embeddings = E2, R2
+    return model
+
+
+def _fmt(score) -> str:
+    """str() of the reference's float32 numpy score (verify_explanations.py:190-193)."""
+    return str(np.float32(score))
+
+
+def _best_rule(explanation, dataset):
+    tmp = explanation["rule_to_relevance"][0]
+    best = tmp[1] if len(tmp) == 3 else tmp[0]
+    return [dataset.ids_triple(t) for t in best]
+
+
+def verify_explanations(explanations: list, dataset: Dataset, model, model_config: dict, mode: str,
+                        device: int = 0, context_factory=None) -> list:
+    """``verify_explanations.main`` (verify_explanations.py:42-268) after its file loading:
+    ``explanations`` is the pipeline's ``output.json`` list, ``model`` the trained
+    model being explained, ``model_config`` the reference config (``model``,
+    ``model_params``, ``training``).  Returns the ``output_end_to_end.json`` list."""
+    if mode not in ("necessary", "sufficient"):
+        raise ValueError(mode)
+    name = model_config["model"]
+    if name != "ComplEx":
+        raise NotImplementedError(f"device retraining supports ComplEx, not {name}")
+    set_seeds(42)
+    # the original model's init_random=True construction (verify_explanations.py:59)
+    _complex_init(dataset, model_config["model_params"]["dimension"], model_config["model_params"]["init_scale"])
+    preds = []
+    if mode == "sufficient":
+        convert_set, best = {}, {}
+        for ex in explanations:
+            pred = dataset.ids_triple(ex["triple"])
+            preds.append(pred)
+            convert_set[pred] = [dataset.entity_to_id[e] for e in ex["entities_to_convert"]]
+            best[pred] = _best_rule(ex, dataset)
+        to_add, to_convert, added_for = [], [], {}
+        for pred in preds:
+            s = pred[0]
+            cur = []
+            for e in convert_set[pred]:
+                tc = Dataset.replace_entity_in_triple(pred, s, e)
+                cur.append(tc)
+                adds = Dataset.replace_entity_in_triples(best[pred], s, e)
+                to_add.extend(adds)
+                added_for[tc] = adds
+            to_convert.extend(cur)
+            convert_set[pred] = cur
+        new_ds = dataset.copy()
+        for s, p, o in to_add:
+            if new_ds.relation_to_type[p] in (MANY_TO_ONE, ONE_TO_ONE):
+                # iterates the list it removes from, like the reference (:114-116)
+                for existing_o in new_ds.train_to_filter[(s, p)]:
+                    new_ds.remove_training_triple((s, p, existing_o))
+        new_ds.add_training_triples(to_add)
+        results = dict(zip(to_convert, model.predict_triples(np.array(to_convert))))
+        new_model = retrain(name, new_ds, model_config["model_params"], model_config["training"], device,
+                            context_factory)
+        new_results = dict(zip(to_convert, new_model.predict_triples(np.array(to_convert))))
+        evaluations = []
+        for pred in preds:
+            conversions = []
+            for tc in convert_set[pred]:
+                r, nr = results[tc], new_results[tc]
+                conversions.append({
+                    "triples_to_add": [dataset.labels_triple(t) for t in added_for[tc]],
+                    "score": _fmt(r["score"]["tail"]), "rank": str(r["rank"]["tail"]),
+                    "new_score": _fmt(nr["score"]["tail"]), "new_rank": str(nr["rank"]["tail"]),
+                })
+            evaluations.append({"triple_to_explain": dataset.labels_triple(pred), "conversions": conversions})
+        return evaluations
+    best = defaultdict(list)
+    for ex in explanations:
+        pred = dataset.ids_triple(ex["triple"])
+        preds.append(pred)
+        best[pred] = _best_rule(ex, dataset)
+    to_remove = []
+    for pred in preds:
+        to_remove += best[pred]
+    new_ds = dataset.copy()
+    new_ds.remove_training_triples(to_remove)
+    results = dict(zip(preds, model.predict_triples(np.array(preds))))
+    new_model = retrain(name, new_ds, model_config["model_params"], model_config["training"], device,
+                            context_factory)
+    new_results = dict(zip(preds, new_model.predict_triples(np.array(preds))))
+    evaluations = []
+    for pred in preds:
+        r, nr = results[pred], new_results[pred]
+        evaluations.append({
+            "triple_to_explain": dataset.labels_triple(pred),
+            "rule": [dataset.labels_triple(t) for t in best[pred]],
+            "score": _fmt(r["score"]["tail"]), "rank": str(r["rank"]["tail"]),
+            "new_score": _fmt(nr["score"]["tail"]), "new_rank": str(nr["rank"]["tail"]),
+        })
+    return evaluations
+
+
+def compute_metrics(evaluations: list, mode: str, explanations: list | None = None) -> dict:
+    """``compute_metrics.main`` (compute_metrics.py:27-85): MRR and H@1 of the explained
+    predictions before and after the retraining, their deltas (each rounded to 3
+    decimals, the deltas of the rounded values), and ``rels`` = the summed
+    ``#relevances`` of ``output.json`` when ``explanations`` is given."""
+    def hits1(ranks):
+        return round(sum(1.0 for r in ranks if r <= 1) / float(len(ranks)), 3)
+
+    def mrr(ranks):
+        acc = 0.0
+        for r in ranks:
+            acc += 1.0 / float(r)
+        return round(acc / float(len(ranks)), 3)
+
+    if mode == "necessary":
+        ranks = [float(d["rank"]) for d in evaluations]
+        new_ranks = [float(d["new_rank"]) for d in evaluations]
+    else:
+        ranks = [float(c["rank"]) for d in evaluations for c in d["conversions"]]
+        new_ranks = [float(c["new_rank"]) for d in evaluations for c in d["conversions"]]
+    out = {"mrr": mrr(ranks), "h1": hits1(ranks), "new_mrr": mrr(new_ranks), "new_h1": hits1(new_ranks)}
+    out["mrr_delta"] = round(out["new_mrr"] - out["mrr"], 3)
+    out["h1_delta"] = round(out["new_h1"] - out["h1"], 3)
+    if explanations is not None:
+        out["rels"] = sum(x["#relevances"] for x in explanations)
+    return out

@@ -363,6 +363,71 @@ class SGDState:
 
 
 # =============================================================================
+# full-model training (the retraining of verify_explanations.py:141-143,230-232)
+# =============================================================================
+class ComplExTrainer:
+    """MultiClassNLLOptimizer.train / epoch / step_on_batch
+    (src/link_prediction/optimization/multiclass_nll_optimizer.py:57-135) for ComplEx
+    (models/complex.py:58-86 forward, regularizers.py N3), numpy float32 over the whole
+    tables.  The gradients come from the full score matrix and autograd's rules written
+    out: CE(mean) -> (softmax - onehot) / B, the complex product's partials, and
+    d |f|^3 through f = sqrt(re^2 + im^2)."""
+
+    def __init__(self, E, R, hp: dict):
+        self.E = np.array(E, dtype=F32)
+        self.R = np.array(R, dtype=F32)
+        self.hp = hp
+        self.half = self.E.shape[1] // 2
+        name = hp["optimizer_name"]
+        mk = {"Adagrad": lambda n: AdagradState(n, hp["lr"]),
+              "Adam": lambda n: AdamState(n, hp["lr"], (hp.get("decay1", 0.9), hp.get("decay2", 0.999))),
+              "SGD": lambda n: SGDState(n, hp["lr"])}[name]
+        self.oE, self.oR = mk(self.E.size), mk(self.R.size)
+
+    def _step(self, batch):
+        E, R, h = self.E, self.R, self.half
+        B = len(batch)
+        lhs, rel, rhs = E[batch[:, 0]], R[batch[:, 1]], E[batch[:, 2]]
+        a, b, c, e = lhs[:, :h], lhs[:, h:], rel[:, :h], rel[:, h:]
+        Q = np.hstack([a * c - b * e, a * e + b * c]).astype(F32)
+        S = (Q[:, :h] @ E[:, :h].T + Q[:, h:] @ E[:, h:].T).astype(F32)
+        S = S - S.max(1, keepdims=True)
+        P = np.exp(S)
+        P = (P / P.sum(1, keepdims=True)).astype(F32)
+        P[np.arange(B), batch[:, 2]] -= F32(1)
+        dS = (P / F32(B)).astype(F32)
+        dQ = (dS @ E).astype(F32)
+        gE = (dS.T @ Q).astype(F32)
+        dr, di = dQ[:, :h], dQ[:, h:]
+        gl = np.hstack([dr * c + di * e, di * c - dr * e]).astype(F32)
+        gr = np.hstack([dr * a + di * b, di * a - dr * b]).astype(F32)
+        gt = np.zeros_like(gl)
+        w = F32(self.hp.get("regularizer_weight", 0.0))
+        if w != 0:
+            k = F32(3) * w / F32(B)
+            for g, (x, y) in ((gl, (a, b)), (gr, (c, e)), (gt, (rhs[:, :h], rhs[:, h:]))):
+                m = np.sqrt(x * x + y * y).astype(F32)
+                g[:, :h] += (k * m) * x
+                g[:, h:] += (k * m) * y
+        gR = np.zeros_like(R)
+        for i in range(B):  # per-key sums in batch order
+            gE[batch[i, 0]] += gl[i]
+            gE[batch[i, 2]] += gt[i]
+            gR[batch[i, 1]] += gr[i]
+        self.E = self.oE.step(E.reshape(-1), gE.reshape(-1)).reshape(E.shape)
+        self.R = self.oR.step(R.reshape(-1), gR.reshape(-1)).reshape(R.shape)
+
+    def epoch(self, triples, perm):
+        t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)[np.asarray(perm, dtype=np.int64)]
+        n = len(t)
+        bs = min(int(self.hp["batch_size"]), n)
+        start = 0
+        while start < n:
+            self._step(t[start:min(start + bs, n)])
+            start += int(self.hp["batch_size"])
+
+
+# =============================================================================
 # post-training (one trainable kelpie row; SURVEY App. C gradients)
 # =============================================================================
 def _rows_with_inverses(ds, triples):
