@@ -164,16 +164,23 @@ int kp_convertible(kp_ctx* ctx, int32_t n, const int32_t* heads, int32_t rel, in
 int kp_predict_tails(kp_ctx* ctx, int32_t n, const int32_t* triples, const int32_t* filt_off, const int32_t* filt,
                      float* out_score, int64_t* out_rank);
 
-/* One epoch of MultiClassNLLOptimizer.epoch (src/link_prediction/optimization/
- * multiclass_nll_optimizer.py:101-135; ComplEx.forward complex.py:58-86, N3
- * regularizers.py) on the context's OWN tables, for the retraining of
- * verify_explanations.py:141-143 / :230-232: triples [n][3] are train()'s stack of the
- * training triples and their inverses (:66-67), perm [n] this epoch's
- * torch.randperm(n) (:102; RNG-as-input), batches of min(hp->batch_size, n) starting
- * every hp->batch_size rows (:112-118).  The optimizer state (Adagrad / Adam / SGD,
- * hp->optimizer) persists across calls and restarts at epoch == 0.  ComplEx contexts
- * only (KP_EINVAL otherwise). */
-int kp_train_epoch(kp_ctx* ctx, const kp_hp* hp, int32_t n, const int32_t* triples, const int32_t* perm,
+/* One training epoch of the context's OWN tables, for the retraining of
+ * verify_explanations.py:141-143 / :230-232 (RNG-as-input: the host draws what the
+ * optimizer draws).  The optimizer state persists across calls and restarts at
+ * epoch == 0.
+ *  ComplEx: MultiClassNLLOptimizer.epoch (src/link_prediction/optimization/
+ *    multiclass_nll_optimizer.py:101-135; ComplEx.forward complex.py:58-86, N3
+ *    regularizers.py): triples [n][3] are train()'s stack of the training triples and
+ *    their inverses (:66-67), aux [n] this epoch's torch.randperm(n) (:102); batches of
+ *    min(hp->batch_size, n) start every hp->batch_size rows (:112-118); Adagrad / Adam /
+ *    SGD (hp->optimizer).
+ *  TransE: PairwiseRankingOptimizer.epoch (pairwise_ranking_optimizer.py:102-157;
+ *    TransE.forward transe.py:67-75, L2 regularizers.py): triples [n][3] are this
+ *    epoch's positive rows in order (the stack after its in-place np.random.shuffle),
+ *    aux [n][3] the matching corrupted rows (the first n of the epoch's ratio * n
+ *    torch.randint draws); MarginRankingLoss(hp->margin), L2 (hp->reg_weight), Adam.
+ * ConvE contexts: KP_EINVAL. */
+int kp_train_epoch(kp_ctx* ctx, const kp_hp* hp, int32_t n, const int32_t* triples, const int32_t* aux,
                    int32_t epoch);
 
 /* Copy the context's tables to the host: entity [n_ent][dim], relation [n_rel2][dim]

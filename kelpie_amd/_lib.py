@@ -301,10 +301,11 @@ class Context:
               self.h)
         return score, rank
 
-    def train_epoch(self, hp: HP, triples, perm, epoch: int):
-        """kp_train_epoch: one optimizer epoch on this context's own tables."""
+    def train_epoch(self, hp: HP, triples, aux, epoch: int):
+        """kp_train_epoch: one optimizer epoch on this context's own tables (ComplEx: aux =
+        the epoch's permutation; TransE: triples / aux = positive / corrupted rows)."""
         t = np.ascontiguousarray(np.asarray(triples, dtype=np.int32).reshape(-1, 3))
-        pm = np.ascontiguousarray(perm, dtype=np.int32)
+        pm = np.ascontiguousarray(aux, dtype=np.int32)
         assert len(pm) == len(t)
         check(lib().kp_train_epoch(self.h, C.byref(hp), len(t), _ptr(t), _ptr(pm), int(epoch)), self.h)
 

@@ -191,12 +191,15 @@ int kp_convertible(kp_ctx* c, int32_t n, const int32_t* heads, int32_t rel, int3
   });
 }
 
-int kp_train_epoch(kp_ctx* c, const kp_hp* hp, int32_t n, const int32_t* triples, const int32_t* perm,
+int kp_train_epoch(kp_ctx* c, const kp_hp* hp, int32_t n, const int32_t* triples, const int32_t* aux,
                    int32_t epoch) {
-  if (!c || !hp || n <= 0 || !triples || !perm || epoch < 0) return KP_EINVAL;
+  if (!c || !hp || n <= 0 || !triples || !aux || epoch < 0) return KP_EINVAL;
   return guarded(c, [&] {
     KP_HIP(hipSetDevice(c->device));
-    complex_train_epoch(c, hp, n, triples, perm, epoch);
+    if (c->model == KP_MODEL_TRANSE)
+      transe_train_epoch(c, hp, n, triples, aux, epoch);
+    else
+      complex_train_epoch(c, hp, n, triples, aux, epoch);
   });
 }
 

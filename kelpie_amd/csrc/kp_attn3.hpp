@@ -842,11 +842,9 @@ int attn3_wpc(kp_ctx* c) {
 }
 
 // Host: the partition of the context's attention kernel.  kp_attn3 takes the XCD-grouped
-// aligned ranges unless their quantisation costs more than a slack over stream-K's
-// balanced split.  The L2 reuse they buy (FETCH_SIZE 14x lower) was worth 2-7 % per
-// launch with the 35 MB FB15k-237 ComplEx image and 6 % with the 154 MB YAGO3-10 ConvE
-// image, which stream-K re-reads through the Infinity Cache at worse hit rates: slack
-// 5 % up to 64 MB of image, 15 % above.  KP_ATTN_PART=streamk
+// aligned ranges unless their quantisation costs more than 40 % over stream-K's
+// balanced split: the L2 reuse they buy (FETCH_SIZE 14x lower, L2 hit rate 2 -> 91 %)
+// outweighs a worse balance.  KP_ATTN_PART=streamk
 // forces stream-K, KP_ATTN_PART=ranges the ranges (parity tests run both).  The fp32
 // kp_attn always uses stream-K.
 inline AttnPlan attn_plan_ctx(const kp_ctx* c, int nq, int n_ent, int slots) {
@@ -858,9 +856,11 @@ inline AttnPlan attn_plan_ctx(const kp_ctx* c, int nq, int n_ent, int slots) {
   const long long n_wg = std::max(8, slots / 8 * 8);
   const long long cost_r = (QT * S + n_wg - 1) / n_wg * ((ktq + S - 1) / S + 2);
   const long long cost_sk = (long long)sk.wk.per_wg + 2;
-  const long long image = (long long)n_ent * split3_row_bytes(c->dp);
-  const long long slack = image > (64ll << 20) ? 115 : 105;
-  return 100 * cost_r <= slack * cost_sk ? r : sk;
+  // measured on the interleaved kernel (tools/attn_micro.hip, FB15k-237 ComplEx, nq 800 -
+  // 5,000): the ranges ran 9-21 % faster than stream-K at every size although their
+  // quantisation was up to 25 % worse (profiles/r02o_attn_partition.jsonl)
+  (void)n_ent;
+  return 100 * cost_r <= 140 * cost_sk ? r : sk;
 }
 
 template <int DB, int MODE>

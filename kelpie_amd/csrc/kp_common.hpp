@@ -179,6 +179,8 @@ void criage_relevance(kp_ctx* c, int n, const int32_t* items, int n_ents, const 
 void launch_score_gemm(kp_ctx* c, const float* dQ, int nq, float* d_out, int ld, int act);
 // kp_train.hip: one MultiClassNLLOptimizer epoch on the context's tables (ComplEx)
 void complex_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* triples, const int32_t* perm, int epoch);
+// kp_train.hip: one PairwiseRankingOptimizer epoch (TransE): positive and corrupted rows in order
+void transe_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* pos, const int32_t* neg, int epoch);
 void train_state_free(kp_ctx* c);
 // out[z][m][n] = act(sum_{k in split z} A[m][k] B[n][k] + (z == 0 ? bias[n] : 0)), fp32 MFMA
 void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,

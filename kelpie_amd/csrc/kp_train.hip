@@ -175,6 +175,68 @@ __global__ void kp_tr_opt(float* __restrict__ X, float* __restrict__ S1, float* 
   X[i] = x;
 }
 
+// TransE: per row i of the batch (positive row pos[i], corrupted row neg[i]) the
+// gradients of MarginRankingLoss(margin, mean) on the L2 distances and of the L2
+// regulariser (mean of each factor squared, times w / 3, averaged over the positive and
+// negative factors): roles 0..2 = positive lhs, rel, rhs; 3..5 = negative ones.
+//   score = ||lhs + rel - rhs||,  hinge_i = score_pos - score_neg + margin > 0
+//   d lhs = (+-1 / B) (lhs + rel - rhs) / score [hinge] + (w / (3 B d)) lhs, etc.
+__global__ void kp_tr_te_rowgrads(const float* __restrict__ E, const float* __restrict__ R, int dp, int dim,
+                                  const int32_t* __restrict__ pos, const int32_t* __restrict__ neg, int B,
+                                  float margin, float inv_b, float wl, float* __restrict__ grads) {
+  const int i = blockIdx.x;
+  if (i >= B) return;
+  const int lane = threadIdx.x;  // one wave per row
+  const float *ph = E + (size_t)pos[3 * i] * dp, *pr = R + (size_t)pos[3 * i + 1] * dp,
+              *pt = E + (size_t)pos[3 * i + 2] * dp;
+  const float *nh = E + (size_t)neg[3 * i] * dp, *nr = R + (size_t)neg[3 * i + 1] * dp,
+              *nt = E + (size_t)neg[3 * i + 2] * dp;
+  float sp = 0.f, sn = 0.f;
+  for (int d = lane; d < dim; d += 64) {
+    const float a = (ph[d] + pr[d]) - pt[d], b = (nh[d] + nr[d]) - nt[d];
+    sp += a * a;
+    sn += b * b;
+  }
+  sp = wave_sum(sp);
+  sn = wave_sum(sn);
+  const float np_ = sqrtf(sp), nn = sqrtf(sn);
+  const bool hinge = (np_ - nn) + margin > 0.f;
+  const float cp = hinge ? inv_b / np_ : 0.f, cn = hinge ? -inv_b / nn : 0.f;
+  float* g = grads + (size_t)i * 6 * dp;
+  for (int d = lane; d < dp; d += 64) {
+    float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (d < dim) {
+      const float a = (ph[d] + pr[d]) - pt[d], b = (nh[d] + nr[d]) - nt[d];
+      v[0] = cp * a + wl * ph[d];
+      v[1] = cp * a + wl * pr[d];
+      v[2] = -cp * a + wl * pt[d];
+      v[3] = cn * b + wl * nh[d];
+      v[4] = cn * b + wl * nr[d];
+      v[5] = -cn * b + wl * nt[d];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) g[(size_t)k * dp + d] = v[k];
+  }
+}
+
+// G[key] += the key's row gradients in batch order (items: 8 row + role, rows of
+// kp_tr_te_rowgrads' [B][6][dp] output)
+__global__ void kp_tr_scatter6(float* __restrict__ G, int dp, const int32_t* __restrict__ keys,
+                               const int32_t* __restrict__ off, const int32_t* __restrict__ items,
+                               const float* __restrict__ grads) {
+  const int k = blockIdx.x;
+  const int i0 = off[k], i1 = off[k + 1];
+  float* g = G + (size_t)keys[k] * dp;
+  for (int d = threadIdx.x; d < dp; d += blockDim.x) {
+    float acc = 0.f;
+    for (int i = i0; i < i1; ++i) {
+      const int it = items[i];
+      acc += grads[((size_t)(it >> 3) * 6 + (it & 7)) * dp + d];
+    }
+    g[d] += acc;
+  }
+}
+
 }  // namespace
 
 // Optimizer state and scratch of a training run, owned by the context.
@@ -247,6 +309,9 @@ void complex_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* tripl
   std::vector<std::pair<int64_t, int32_t>> ek;  // (key, item) sorted stably by key
   // batch_start advances by hp->batch_size (multiclass_nll_optimizer.py:118)
   for (int start = 0; start < n; start += hp->batch_size) {
+    // the host vectors below are refilled per batch: the previous batch's copies from
+    // them must have left
+    if (start) KP_HIP(hipStreamSynchronize(c->stream));
     const int B = std::min(bs, n - start);
     const int Bp = (B + 3) / 4 * 4;
     for (int b = 0; b < B; ++b) std::memcpy(&hbt[3 * (size_t)b], triples + 3 * (size_t)perm[start + b], 12);
@@ -339,6 +404,123 @@ void complex_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* tripl
   }
   KP_HIP(hipStreamSynchronize(c->stream));
   // the tables changed: the attention image and its prefix sums are stale
+  c->e3_ready = false;
+  c->e3pre_ready = false;
+}
+
+// One PairwiseRankingOptimizer epoch (TransE) on the context's own tables: positive
+// rows pos[n][3] and corrupted rows neg[n][3] in the epoch's order, batches of
+// hp->batch_size, Adam over both whole tables.
+void transe_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* pos, const int32_t* neg, int epoch) {
+  KP_REQUIRE(c->model == KP_MODEL_TRANSE, "kp_train_epoch: TransE contexts only");
+  KP_REQUIRE(n > 0 && hp->batch_size > 0, "kp_train_epoch: empty training set or batch");
+  for (int i = 0; i < 3 * n; i += 3)
+    for (const int32_t* t : {pos + i, neg + i})
+      KP_REQUIRE(t[0] >= 0 && t[0] < c->n_ent && t[2] >= 0 && t[2] < c->n_ent && t[1] >= 0 && t[1] < c->n_rel2,
+                 "kp_train_epoch: triple id out of range");
+  if (epoch == 0 || !c->train) {
+    delete c->train;
+    c->train = new kp_train_state();
+  }
+  kp_train_state& st = *c->train;
+  const int dp = c->dp, dim = c->dim, N = c->n_ent, NR = c->n_rel2;
+  const size_t nE = (size_t)N * dp, nR = (size_t)NR * dp;
+  if (st.step == 0) {
+    for (DevBuf* b : {&st.s1E, &st.s2E}) {
+      b->ensure(4 * nE);
+      KP_HIP(hipMemsetAsync(b->p, 0, 4 * nE, c->stream));
+    }
+    for (DevBuf* b : {&st.s1R, &st.s2R}) {
+      b->ensure(4 * nR);
+      KP_HIP(hipMemsetAsync(b->p, 0, 4 * nR, c->stream));
+    }
+  }
+  const int bs = hp->batch_size;
+  const int Bmax = std::min(bs, n);
+  float* gE = reinterpret_cast<float*>(st.gE.ensure(4 * nE));
+  float* gR = reinterpret_cast<float*>(st.gR.ensure(4 * nR));
+  int32_t* dpos = reinterpret_cast<int32_t*>(st.bt.ensure(4 * 3 * (size_t)n));
+  int32_t* dneg = reinterpret_cast<int32_t*>(st.Q.ensure(4 * 3 * (size_t)n));
+  float* grads = reinterpret_cast<float*>(st.gl.ensure(4 * 6 * (size_t)Bmax * dp));
+  int32_t* dkeys = reinterpret_cast<int32_t*>(st.keys.ensure(4 * 6 * (size_t)Bmax));
+  int32_t* doff = reinterpret_cast<int32_t*>(st.off.ensure(4 * (6 * (size_t)Bmax + 2)));
+  int32_t* ditems = reinterpret_cast<int32_t*>(st.items.ensure(4 * 6 * (size_t)Bmax));
+  KP_HIP(hipMemcpyAsync(dpos, pos, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+  KP_HIP(hipMemcpyAsync(dneg, neg, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+
+  TrOpt o{};
+  o.kind = KP_OPT_ADAM;
+  o.lr = hp->lr;
+  o.b2 = hp->beta2;
+  o.eps = hp->eps;
+  o.one_minus_b1 = (float)(1.0 - (double)hp->beta1);
+  o.one_minus_b2 = (float)(1.0 - (double)hp->beta2);
+  std::vector<int32_t> keys, off, items;
+  std::vector<std::pair<int64_t, int32_t>> ek;
+  for (int start = 0; start < n; start += bs) {
+    if (start) KP_HIP(hipStreamSynchronize(c->stream));  // host CSR vectors are refilled
+    const int B = std::min(bs, n - start);
+    const int32_t* P = pos + 3 * (size_t)start;
+    const int32_t* Ng = neg + 3 * (size_t)start;
+    // per-key CSR, entity keys (roles 0, 2, 3, 5) then relation keys (roles 1, 4), batch order
+    int n_ek = 0;
+    keys.clear();
+    off.clear();
+    items.clear();
+    for (int pass = 0; pass < 2; ++pass) {
+      ek.clear();
+      for (int b = 0; b < B; ++b) {
+        if (pass == 0) {
+          ek.emplace_back(P[3 * b], 8 * b + 0);
+          ek.emplace_back(P[3 * b + 2], 8 * b + 2);
+          ek.emplace_back(Ng[3 * b], 8 * b + 3);
+          ek.emplace_back(Ng[3 * b + 2], 8 * b + 5);
+        } else {
+          ek.emplace_back(P[3 * b + 1], 8 * b + 1);
+          ek.emplace_back(Ng[3 * b + 1], 8 * b + 4);
+        }
+      }
+      std::stable_sort(ek.begin(), ek.end(),
+                       [](const std::pair<int64_t, int32_t>& x, const std::pair<int64_t, int32_t>& y) {
+                         return x.first < y.first;
+                       });
+      for (size_t i = 0; i < ek.size(); ++i) {
+        if (i == 0 || ek[i].first != ek[i - 1].first) {
+          keys.push_back((int32_t)ek[i].first);
+          off.push_back((int32_t)items.size());
+        }
+        items.push_back(ek[i].second);
+      }
+      off.push_back((int32_t)items.size());
+      if (pass == 0) n_ek = (int)keys.size();  // the relation part's keys and offsets follow
+    }
+    const int n_rk = (int)keys.size() - n_ek;
+    KP_HIP(hipMemcpyAsync(dkeys, keys.data(), 4 * keys.size(), hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(doff, off.data(), 4 * off.size(), hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(ditems, items.data(), 4 * items.size(), hipMemcpyHostToDevice, c->stream));
+    const float inv_b = 1.0f / (float)B;
+    const float wl = hp->reg_weight / (3.0f * (float)B * (float)dim);
+    hipLaunchKernelGGL(kp_tr_te_rowgrads, dim3(B), dim3(64), 0, c->stream, c->dE, c->dR, dp, dim,
+                       dpos + 3 * (size_t)start, dneg + 3 * (size_t)start, B, hp->margin, inv_b, wl, grads);
+    KP_HIP(hipGetLastError());
+    KP_HIP(hipMemsetAsync(gE, 0, 4 * nE, c->stream));
+    KP_HIP(hipMemsetAsync(gR, 0, 4 * nR, c->stream));
+    hipLaunchKernelGGL(kp_tr_scatter6, dim3(n_ek), dim3(128), 0, c->stream, gE, dp, dkeys, doff, ditems, grads);
+    KP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(kp_tr_scatter6, dim3(n_rk), dim3(128), 0, c->stream, gR, dp, dkeys + n_ek, doff + n_ek + 1,
+                       ditems, grads);
+    KP_HIP(hipGetLastError());
+    ++st.step;
+    o.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, (double)st.step)));
+    o.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)hp->beta2, (double)st.step));
+    hipLaunchKernelGGL(kp_tr_opt, dim3((unsigned)((nE + 255) / 256)), dim3(256), 0, c->stream, c->dE,
+                       st.s1E.as<float>(), st.s2E.as<float>(), gE, nE, o);
+    KP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(kp_tr_opt, dim3((unsigned)((nR + 255) / 256)), dim3(256), 0, c->stream, c->dR,
+                       st.s1R.as<float>(), st.s2R.as<float>(), gR, nR, o);
+    KP_HIP(hipGetLastError());
+  }
+  KP_HIP(hipStreamSynchronize(c->stream));
   c->e3_ready = false;
   c->e3pre_ready = false;
 }

@@ -8,8 +8,10 @@ the original model's ``init_random=True`` construction (verify_explanations.py:5
 its draws are consumed before ``load_state_dict``), the new model's initialisation
 (complex.py:28-36: ``torch.rand`` tables scaled by ``init_scale``) and one
 ``torch.randperm`` per epoch (multiclass_nll_optimizer.py:102) come from the same
-torch CPU generator, in that order.  Supported: ComplEx with its
-MultiClassNLLOptimizer (Adagrad / Adam / SGD, N3); other models raise
+torch CPU generator, in that order (TransE: its xavier_normal_ tables and per epoch the
+numpy shuffle and torch.randint negatives of pairwise_ranking_optimizer.py:102-118).
+Supported: ComplEx with its MultiClassNLLOptimizer (Adagrad / Adam / SGD, N3) and
+TransE with its PairwiseRankingOptimizer (Adam, margin ranking, L2); ConvE raises
 ``NotImplementedError``.
 """
 from __future__ import annotations
@@ -21,7 +23,7 @@ import numpy as np
 import torch
 
 from .data import MANY_TO_ONE, ONE_TO_ONE, Dataset
-from .models import ComplEx
+from .models import ComplEx, TransE
 
 
 def set_seeds(seed: int = 42):
@@ -41,25 +43,67 @@ def _complex_init(dataset: Dataset, dimension: int, init_scale: float):
     return E.numpy(), R.numpy()
 
 
+def _transe_init(dataset: Dataset, dimension: int):
+    """TransE(dataset, hp, init_random=True) tables (transe.py:26-33): torch.rand draws,
+    then xavier_normal_ over each whole table."""
+    E = torch.rand(dataset.num_entities, int(dimension))
+    R = torch.rand(2 * dataset.num_relations, int(dimension))
+    torch.nn.init.xavier_normal_(E)
+    torch.nn.init.xavier_normal_(R)
+    return E.numpy(), R.numpy()
+
+
+def model_init(model_name: str, dataset: Dataset, model_params: dict):
+    """The tables of ``MODEL_REGISTRY[model_name](dataset, hp, init_random=True)``."""
+    if model_name == "ComplEx":
+        return _complex_init(dataset, model_params["dimension"], model_params["init_scale"])
+    if model_name == "TransE":
+        return _transe_init(dataset, model_params["dimension"])
+    raise NotImplementedError(f"device retraining supports ComplEx and TransE, not {model_name}")
+
+
+def _transe_epoch_rows(stack: np.ndarray, ratio: int, n_entities: int):
+    """PairwiseRankingOptimizer.epoch's draws and rows (pairwise_ranking_optimizer.py:102-118):
+    the in-place shuffle of the stack, randint(2) then randint(N) over ratio * n, and of
+    the repeated rows the first n, i.e. row i of the batch loop is stack[i // ratio]."""
+    np.random.shuffle(stack)
+    n = len(stack)
+    size = (n * ratio,)
+    head_or_tail = torch.randint(high=2, size=size).numpy()[:n]
+    ents = torch.randint(high=n_entities, size=size).numpy()[:n]
+    pos = stack[np.arange(n) // ratio]
+    neg = pos.copy()
+    mh = head_or_tail == 1
+    neg[mh, 0] = ents[mh]
+    neg[~mh, 2] = ents[~mh]
+    return pos.astype(np.int32), neg.astype(np.int32)
+
+
 def retrain(model_name: str, dataset: Dataset, model_params: dict, training: dict, device: int = 0,
             context_factory=None):
     """A fresh model (``init_random=True``) trained by its optimizer on
-    ``dataset.training_triples`` (``optimizer.train``, multiclass_nll_optimizer.py:57-99),
-    on the device.  Consumes the torch generator like the reference.
-    ``context_factory(model)``, if given, supplies the model's context (tests)."""
-    if model_name != "ComplEx":
-        raise NotImplementedError(f"device retraining supports ComplEx, not {model_name}")
-    E, R = _complex_init(dataset, model_params["dimension"], model_params["init_scale"])
-    model = ComplEx(dataset, E, R, init_scale=model_params["init_scale"], device=device)
+    ``dataset.training_triples`` (``optimizer.train``: multiclass_nll_optimizer.py:57-99,
+    pairwise_ranking_optimizer.py:55-100), on the device.  Consumes the torch / numpy
+    generators like the reference.  ``context_factory(model)``, if given, supplies the
+    model's context (tests)."""
+    E, R = model_init(model_name, dataset, model_params)
+    if model_name == "ComplEx":
+        model = ComplEx(dataset, E, R, init_scale=model_params["init_scale"], device=device)
+    else:
+        model = TransE(dataset, E, R, norm=model_params.get("norm", 2), device=device)
     if context_factory is not None:
         model._ctx = context_factory(model)
     hp = model.kp_hp(training)
     train = dataset.training_triples
-    triples = np.vstack([train, dataset.invert_triples(train)]).astype(np.int32)
+    stack = np.vstack([train, dataset.invert_triples(train)])
     ctx = model.ctx
     for epoch in range(int(training["epochs"])):
-        perm = torch.randperm(triples.shape[0]).numpy()
-        ctx.train_epoch(hp, triples, perm, epoch)
+        if model_name == "ComplEx":
+            perm = torch.randperm(stack.shape[0]).numpy()
+            ctx.train_epoch(hp, stack.astype(np.int32), perm, epoch)
+        else:
+            pos, neg = _transe_epoch_rows(stack, int(training["negative_triples_ratio"]), dataset.num_entities)
+            ctx.train_epoch(hp, pos, neg, epoch)
     E2, R2 = ctx.read_tables(2 * dataset.num_relations)
     model.entity_embeddings, model.relation_embeddings = E2, R2
     return model
@@ -85,11 +129,11 @@ def verify_explanations(explanations: list, dataset: Dataset, model, model_confi
     if mode not in ("necessary", "sufficient"):
         raise ValueError(mode)
     name = model_config["model"]
-    if name != "ComplEx":
-        raise NotImplementedError(f"device retraining supports ComplEx, not {name}")
+    if name not in ("ComplEx", "TransE"):
+        raise NotImplementedError(f"device retraining supports ComplEx and TransE, not {name}")
     set_seeds(42)
     # the original model's init_random=True construction (verify_explanations.py:59)
-    _complex_init(dataset, model_config["model_params"]["dimension"], model_config["model_params"]["init_scale"])
+    model_init(name, dataset, model_config["model_params"])
     preds = []
     if mode == "sufficient":
         convert_set, best = {}, {}

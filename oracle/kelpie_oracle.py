@@ -427,6 +427,48 @@ class ComplExTrainer:
             start += int(self.hp["batch_size"])
 
 
+class TransETrainer:
+    """PairwiseRankingOptimizer.epoch / step_on_batch (src/link_prediction/optimization/
+    pairwise_ranking_optimizer.py:102-157) for TransE (models/transe.py:67-75, L2
+    regularizers.py), numpy float32 over the whole tables, Adam.  ``epoch`` takes the
+    epoch's positive and corrupted rows in order."""
+
+    def __init__(self, E, R, hp: dict):
+        self.E = np.array(E, dtype=F32)
+        self.R = np.array(R, dtype=F32)
+        self.hp = hp
+        self.oE, self.oR = AdamState(self.E.size, hp["lr"]), AdamState(self.R.size, hp["lr"])
+
+    def _step(self, pos, neg):
+        E, R = self.E, self.R
+        B, d = len(pos), E.shape[1]
+        rows = [E[pos[:, 0]], R[pos[:, 1]], E[pos[:, 2]], E[neg[:, 0]], R[neg[:, 1]], E[neg[:, 2]]]
+        a = ((rows[0] + rows[1]) - rows[2]).astype(F32)
+        b = ((rows[3] + rows[4]) - rows[5]).astype(F32)
+        sp = np.sqrt((a * a).sum(1)).astype(F32)
+        sn = np.sqrt((b * b).sum(1)).astype(F32)
+        hinge = ((sp - sn) + F32(self.hp["margin"])) > 0
+        cp = np.where(hinge, F32(1.0 / B) / sp, F32(0))[:, None].astype(F32)
+        cn = np.where(hinge, -F32(1.0 / B) / sn, F32(0))[:, None].astype(F32)
+        wl = F32(self.hp.get("regularizer_weight", 0.0)) / (F32(3) * F32(B) * F32(d))
+        g = [cp * a + wl * rows[0], cp * a + wl * rows[1], -cp * a + wl * rows[2],
+             cn * b + wl * rows[3], cn * b + wl * rows[4], -cn * b + wl * rows[5]]
+        gE, gR = np.zeros_like(E), np.zeros_like(R)
+        keys = [(pos, 0, gE), (pos, 1, gR), (pos, 2, gE), (neg, 0, gE), (neg, 1, gR), (neg, 2, gE)]
+        for i in range(B):
+            for role, (src, col, G) in enumerate(keys):
+                G[src[i, col]] += g[role][i]
+        self.E = self.oE.step(E.reshape(-1), gE.reshape(-1)).reshape(E.shape)
+        self.R = self.oR.step(R.reshape(-1), gR.reshape(-1)).reshape(R.shape)
+
+    def epoch(self, pos, neg):
+        pos = np.asarray(pos, dtype=np.int64).reshape(-1, 3)
+        neg = np.asarray(neg, dtype=np.int64).reshape(-1, 3)
+        bs = int(self.hp["batch_size"])
+        for start in range(0, len(pos), bs):
+            self._step(pos[start:start + bs], neg[start:start + bs])
+
+
 # =============================================================================
 # post-training (one trainable kelpie row; SURVEY App. C gradients)
 # =============================================================================

@@ -163,11 +163,14 @@ class OracleBackedContext:
         return {"device_s": 0.0, "hot_s": 0.0, "hot_launches": 0}
 
     def train_epoch(self, hp, triples, perm, epoch):
-        """Stand-in for kp_train_epoch: the oracle's ComplExTrainer on this context's tables."""
+        """Stand-in for kp_train_epoch: the oracle's trainer on this context's tables."""
         if epoch == 0 or getattr(self, "_trainer", None) is None:
             hpd = self._hp(hp)
-            hpd["optimizer_name"] = {0: "Adagrad", 1: "Adam", 2: "SGD"}[hp.optimizer]
-            self._trainer = ko.ComplExTrainer(self.om.E, self.om.R, hpd)
+            if self.model.name == "TransE":
+                self._trainer = ko.TransETrainer(self.om.E, self.om.R, hpd)
+            else:
+                hpd["optimizer_name"] = {0: "Adagrad", 1: "Adam", 2: "SGD"}[hp.optimizer]
+                self._trainer = ko.ComplExTrainer(self.om.E, self.om.R, hpd)
         self._trainer.epoch(triples, perm)
         self.om.E, self.om.R = self._trainer.E, self._trainer.R
 

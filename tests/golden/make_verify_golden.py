@@ -1,12 +1,13 @@
 """Reference goldens for explanation verification (f3: verify_explanations.py and
 compute_metrics.py), development container only.
 
-On the complex_tiny graph and weights of make_golden.py (300 entities, 2,400 training
-triples), with three explained predictions per mode, the reference's own
+On the complex_tiny and transe_tiny graphs and weights of make_golden.py (300 entities,
+2,400 training triples), with three explained predictions per mode, the reference's own
 ``verify_explanations.main`` runs end to end (its set_seeds(42), the original model's
-init_random construction, the edited dataset, a fresh ComplEx trained by
-MultiClassNLLOptimizer.train, predict_triples before and after) for two training
-configurations (Adagrad + N3, Adam); its ``output_end_to_end.json`` is recorded.
+init_random construction, the edited dataset, a fresh model trained by its optimizer's
+train, predict_triples before and after) for the training configurations below
+(ComplEx: Adagrad + N3, Adam; TransE: Adam + L2); its ``output_end_to_end.json`` is
+recorded.
 A direct training run (set_seeds(42), ComplEx(init_random=True), optimizer.train on
 the unedited training set) records the trained tables, to pin the trainer itself.
 
@@ -30,13 +31,26 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 import ref_harness  # noqa: E402
 from make_golden import CASES, build_case  # noqa: E402
 
-TRAINING = {
-    "adagrad_n3": {"optimizer_name": "Adagrad", "batch_size": 100, "epochs": 3, "lr": 0.1, "decay1": 0.9,
-                   "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0.05},
-    "adam": {"optimizer_name": "Adam", "batch_size": 128, "epochs": 3, "lr": 0.01, "decay1": 0.9, "decay2": 0.999,
-             "regularizer_name": "N3", "regularizer_weight": 0.0},
+CASES_VERIFY = {
+    "complex_tiny": {
+        "model": "ComplEx",
+        "model_params": {"dimension": 8, "init_scale": 1e-3},
+        "training": {
+            "adagrad_n3": {"optimizer_name": "Adagrad", "batch_size": 100, "epochs": 3, "lr": 0.1, "decay1": 0.9,
+                           "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0.05},
+            "adam": {"optimizer_name": "Adam", "batch_size": 128, "epochs": 3, "lr": 0.01, "decay1": 0.9,
+                     "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0.0},
+        },
+    },
+    "transe_tiny": {
+        "model": "TransE",
+        "model_params": {"dimension": 16, "norm": 2},
+        "training": {
+            "adam_l2": {"batch_size": 512, "epochs": 3, "lr": 0.01, "margin": 5, "negative_triples_ratio": 5,
+                        "regularizer_weight": 1.0},
+        },
+    },
 }
-MODEL_PARAMS = {"dimension": 8, "init_scale": 1e-3}
 
 
 def explanations_for(dataset, g):
@@ -65,24 +79,17 @@ def digest(a):
     return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float32).tobytes()).hexdigest()
 
 
-def main():
-    src = ref_harness.load_reference()
-    name = "complex_tiny"
+def run_case(src, name, spec, ver, MODEL_REGISTRY):
     g, w, dataset, model = build_case(src, name, CASES[name])
-    import src.verify_explanations as ver
-    from src.link_prediction import MODEL_REGISTRY
-    # utils.set_seeds (utils/utils.py:15-21) without its torch.cuda state touch: the
-    # same three CPU seeds
-    ver.set_seeds = ref_harness.seed_all
-
-    out = {"case": name, "model_params": MODEL_PARAMS, "training": TRAINING, "runs": {}}
+    out = {"model": spec["model"], "model_params": spec["model_params"], "training": spec["training"], "runs": {}}
     with tempfile.TemporaryDirectory() as tmp:
         pt = os.path.join(tmp, "model.pt")
         torch.save(model.state_dict(), pt)
         ex_n, ex_s = explanations_for(dataset, g)
         out["explanations"] = {"necessary": ex_n, "sufficient": ex_s}
-        for tname, training in TRAINING.items():
-            cfg = {"model": "ComplEx", "model_path": pt, "model_params": MODEL_PARAMS, "training": training}
+        for tname, training in spec["training"].items():
+            cfg = {"model": spec["model"], "model_path": pt, "model_params": spec["model_params"],
+                   "training": training}
             cfg_path = os.path.join(tmp, f"{tname}.json")
             with open(cfg_path, "w") as f:
                 json.dump(cfg, f)
@@ -94,25 +101,36 @@ def main():
                 ver.main.callback(dataset=name, explanations_path=d, model_config=cfg_path, mode=mode)
                 with open(os.path.join(d, "output_end_to_end.json")) as f:
                     out["runs"][f"{tname}/{mode}"] = json.load(f)
-                print(tname, mode, json.dumps(out["runs"][f"{tname}/{mode}"])[:300], flush=True)
-        # the trainer alone on the unedited training set
-        from src.data import Dataset
-        direct = {}
-        for tname, training in TRAINING.items():
-            ref_harness.seed_all(42)
-            ds = Dataset(name)
-            cls = MODEL_REGISTRY["ComplEx"]["class"]
-            m = cls(dataset=ds, hp=cls.get_hyperparams_class()(**MODEL_PARAMS), init_random=True)
-            opt_cls = MODEL_REGISTRY["ComplEx"]["optimizer"]
-            opt = opt_cls(model=m, hp=opt_cls.get_hyperparams_class()(**training), verbose=False)
-            opt.train(training_triples=ds.training_triples)
-            E = m.entity_embeddings.detach().cpu().numpy()
-            R = m.relation_embeddings.detach().cpu().numpy()
-            direct[tname] = {"E_rows": E[:4].astype(np.float64).tolist(), "R_rows": R[:2].astype(np.float64).tolist(),
-                             "E_abs_sum": float(np.abs(E.astype(np.float64)).sum()),
-                             "R_abs_sum": float(np.abs(R.astype(np.float64)).sum()),
-                             "E_sha256": digest(E), "R_sha256": digest(R)}
-        out["direct"] = direct
+                print(name, tname, mode, json.dumps(out["runs"][f"{tname}/{mode}"])[:200], flush=True)
+    # the trainer alone on the unedited training set
+    from src.data import Dataset
+    direct = {}
+    for tname, training in spec["training"].items():
+        ref_harness.seed_all(42)
+        ds = Dataset(name)
+        cls = MODEL_REGISTRY[spec["model"]]["class"]
+        m = cls(dataset=ds, hp=cls.get_hyperparams_class()(**spec["model_params"]), init_random=True)
+        opt_cls = MODEL_REGISTRY[spec["model"]]["optimizer"]
+        opt = opt_cls(model=m, hp=opt_cls.get_hyperparams_class()(**training), verbose=False)
+        opt.train(training_triples=ds.training_triples)
+        E = m.entity_embeddings.detach().cpu().numpy()
+        R = m.relation_embeddings.detach().cpu().numpy()
+        direct[tname] = {"E_rows": E[:4].astype(np.float64).tolist(), "R_rows": R[:2].astype(np.float64).tolist(),
+                         "E_abs_sum": float(np.abs(E.astype(np.float64)).sum()),
+                         "R_abs_sum": float(np.abs(R.astype(np.float64)).sum()),
+                         "E_sha256": digest(E), "R_sha256": digest(R)}
+    out["direct"] = direct
+    return out
+
+
+def main():
+    src = ref_harness.load_reference()
+    import src.verify_explanations as ver
+    from src.link_prediction import MODEL_REGISTRY
+    # utils.set_seeds (utils/utils.py:15-21) without its torch.cuda state touch: the
+    # same three CPU seeds
+    ver.set_seeds = ref_harness.seed_all
+    out = {"cases": {name: run_case(src, name, spec, ver, MODEL_REGISTRY) for name, spec in CASES_VERIFY.items()}}
     with open(os.path.join(HERE, "verify_golden.json"), "w") as f:
         json.dump(out, f)
 
