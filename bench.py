@@ -389,7 +389,10 @@ def main():
         achieved = nbytes / hot_union / 1e9 if hot_union > 0 else None
         peak = 8000.0
         roof = {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                "frac": (achieved / peak) if achieved else None, "traffic": None, "kernel": "kp_te_posttrain"}
+                "frac": (achieved / peak) if achieved else None, "traffic": None, "kernel": "kp_te_posttrain",
+                "actual_limit": ("VALU issue on the CUs of the longest slots (R = 200-400 rows, one workgroup "
+                                 "per slot, ~1.9k SIMD cycles per stepped item, DESIGN.md section 6); the "
+                                 "frozen table (11.6 MB) is L2/MALL-resident, so HBM is not the limit")}
     else:
         # 4 * D flops per (query row, frozen entity): s = q.E_e and O += w(s) E_e
         D = wl["dim"] * (2 if wl["model"] == "ComplEx" else 1)

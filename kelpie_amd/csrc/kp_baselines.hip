@@ -16,9 +16,10 @@
 //     = y^T), relevance = z_p . ((1 - sig) y).  z = criage_first_step: the ComplEx
 //     query (complex.py:131) or the ConvE encoder output (conve.py:102-124).
 //     One workgroup per candidate eliminates its own D x D system in a device
-//     workspace (float64 VALU; D^3/3 multiply-adds, bound by the L2 traffic of
-//     the trailing updates).
+//     workspace, blocked by 32-column panels held in LDS (float64 VALU; D^3/3
+//     multiply-adds).
 #include <cmath>
+#include <utility>
 
 #include "kp_common.hpp"
 
@@ -130,31 +131,128 @@ __global__ __launch_bounds__(256) void kp_criage_zq(int n, const int2* __restric
 }
 
 // One workgroup per candidate: A = H_e + fl32(c * fl32(z_i z_j)), c = fl32(sig (1 - sig)),
-// Gaussian elimination with partial pivoting on [A | z_t], back substitution,
-// out = z_p . ((1 - sig) y).  items[i] = (z_pred row, z_triple row, entity slot, entity id).
-__global__ __launch_bounds__(256) void kp_criage_solve(int D, int dp, const int32_t* __restrict__ items,
-                                                       const float* __restrict__ Z, const float* __restrict__ E,
-                                                       const double* __restrict__ H, double* __restrict__ Aws,
-                                                       double* __restrict__ out, int32_t* __restrict__ status) {
-  __shared__ double lcol[512], prow[512], bsh[512];
-  __shared__ double rv[256];
-  __shared__ int ri[256];
+// with b = z_t as column Dp of the workspace (Dp = D rounded up to CR_NB, the system
+// bordered by an identity block, b by zeros; row stride ld = Dp + 1); right-looking blocked
+// Gaussian elimination with partial pivoting, out = z_p . ((1 - sig) y).  The border never
+// pivots into the first D columns (its entries there are 0, a tie with 0 means singular)
+// and its multipliers are 0, so the first D unknowns are those of the D x D system.
+//   row swaps exchange entries of a logical -> workspace row map in LDS, no data moves;
+//   per panel of CR_NB columns: the panel rows k0..Dp in registers, one row per thread,
+//   factorised there (pivot = first row of maximal |a| (idamax) by a DPP wave argmax and
+//   one barrier per column over the waves' best rows in LDS; multipliers; rank-1 update,
+//   whose first column is the next pivot search's input), then L to LDS;
+//   U12 = L11^-1 A12 over the trailing columns and b (one column per thread, its 32 loads
+//   issued together), then A22 -= L21 U12 (8 rows x 64 columns per wave item, loads first,
+//   L21 broadcast from LDS);
+//   back substitution by CR_NB-row blocks staged in LDS: the block's rows on one wave
+//   (shuffles), then every row above it updated by the block's y.
+// Every element sees the operations of the unblocked column-by-column elimination in the
+// same order (row swaps travel with the multipliers; subtractions in pivot order;
+// -ffp-contract=off), so the result equals it bit for bit; the blocking only removes the
+// per-column barriers and L2 round trips of the trailing matrix.
+// one DPP step of a wave argmax over (|a|, row): the larger value, the smaller row on ties
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void argmax_dpp(double& v, int& vi) {
+  const long long b = __double_as_longlong(v);
+  const int lo = (int)b, hi = (int)(b >> 32);
+  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xF, false);
+  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xF, false);
+  const int oi = __builtin_amdgcn_update_dpp(vi, vi, CTRL, ROW_MASK, 0xF, false);
+  const double ov = __longlong_as_double(((long long)ohi << 32) | (unsigned)olo);
+  if (ov > v || (ov == v && oi < vi)) {
+    v = ov;
+    vi = oi;
+  }
+}
+
+// wave argmax: quad xor 1 and 2, row rotations by 4 and 8, then row_bcast15 / row_bcast31
+// fold the four rows into lane 63, read back uniformly
+__device__ __forceinline__ void wave_argmax(double& v, int& vi) {
+  argmax_dpp<0xB1, 0xF>(v, vi);
+  argmax_dpp<0x4E, 0xF>(v, vi);
+  argmax_dpp<0x124, 0xF>(v, vi);
+  argmax_dpp<0x128, 0xF>(v, vi);
+  argmax_dpp<0x142, 0xA>(v, vi);
+  argmax_dpp<0x143, 0xC>(v, vi);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  v = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  vi = __builtin_amdgcn_readlane(vi, 63);
+}
+
+// f(std::integral_constant<int, 0>) ... f(std::integral_constant<int, N - 1>): a loop whose
+// index is a compile-time constant in every copy (register arrays stay in registers)
+template <class F, int... J>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+constexpr int CR_NB = 32;
+constexpr int CR_PS = CR_NB + 1;  // panel row stride (doubles): odd, row-per-lane access is conflict-free
+#ifndef KP_CR_T
+#define KP_CR_T 512
+#endif
+#ifndef KP_CR_ROWS
+#define KP_CR_ROWS 8
+#endif
+#ifndef KP_CR_SEG
+#define KP_CR_SEG 32
+#endif
+constexpr int CR_T = KP_CR_T;      // threads per workgroup (one panel row / one trailing column each)
+constexpr int CR_R = KP_CR_ROWS;   // rows per trailing-update chunk
+constexpr int CR_SEG = KP_CR_SEG;  // rows per trailing-update item
+// diagnostic: per-phase s_memtime totals of workgroup 0, printed at its end (KP_CR_STAMPS,
+// diagnostic builds only)
+#ifdef KP_CR_STAMPS
+#ifndef KP_DIAGNOSTIC_BUILD
+#error "KP_CR_STAMPS is a diagnostic define: build it with tools/build_variant.sh -DKP_DIAGNOSTIC_BUILD"
+#endif
+#define CR_ST(k)                                                 \
+  do {                                                           \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t_ - st_last;                                   \
+    st_last = t_;                                                \
+  } while (0)
+#else
+#define CR_ST(k) (void)0
+#endif
+static_assert(CR_T >= 512 && CR_T % 64 == 0 && CR_NB % CR_SEG == 0 && CR_SEG % CR_R == 0, "one thread per panel row (Dp <= 512)");
+
+__global__ __launch_bounds__(CR_T) void kp_criage_solve(int D, int dp, const int32_t* __restrict__ items,
+                                                        const float* __restrict__ Z, const float* __restrict__ E,
+                                                        const double* __restrict__ H, double* __restrict__ Aws,
+                                                        double* __restrict__ out, int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double crl[];  // panel [D][CR_PS]; later b, partial sums
+  __shared__ double wv[2][CR_T / 64];
+  __shared__ int wi[2][CR_T / 64];
+  __shared__ double wrow[2][CR_T / 64][32];  // each wave's best row (its panel columns), by column parity
+  __shared__ double jrow[2][32];             // row j, which the pivot row displaces
+  __shared__ int phys[512];  // logical row -> workspace row: row swaps move no data
+  __shared__ float red[4];
   __shared__ float sig_s;
-  __shared__ int bad;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef KP_CR_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
+  const int Dp = (D + CR_NB - 1) / CR_NB * CR_NB;
+  const int ld = Dp + 1;
   const int32_t* it = items + 4 * (size_t)blockIdx.x;
   const float* zp = Z + (size_t)it[0] * dp;
   const float* zt = Z + (size_t)it[1] * dp;
   const double* He = H + (size_t)it[2] * D * D;
   const float* ee = E + (size_t)it[3] * dp;
-  double* A = Aws + (size_t)blockIdx.x * D * D;
-  // sig = sigmoid(e . z_t) in float32
-  float part = 0.f;
-  for (int j = tid; j < D; j += 256) part += ee[j] * zt[j];
-  part = wsum(part);
-  __shared__ float red[4];
-  if ((tid & 63) == 0) red[tid >> 6] = part;
-  if (tid == 0) bad = 0;
+  double* A = Aws + (size_t)blockIdx.x * Dp * ld;
+  // sig = sigmoid(e . z_t) in float32: 256 partial sums, four waves, fixed combination order
+  if (tid < 256) {
+    float part = 0.f;
+    for (int j = tid; j < D; j += 256) part += ee[j] * zt[j];
+    part = wsum(part);
+    if (lane == 0) red[wave] = part;
+  }
   __syncthreads();
   if (tid == 0) {
     const float dot = (red[0] + red[1]) + (red[2] + red[3]);
@@ -163,90 +261,232 @@ __global__ __launch_bounds__(256) void kp_criage_solve(int D, int dp, const int3
   __syncthreads();
   const float sig = sig_s;
   const float c = sig * (1.0f - sig);
-  for (int i = tid >> 5; i < D; i += 8) {
-    const float zi = zt[i];
-    for (int j = tid & 31; j < D; j += 32) A[(size_t)i * D + j] = He[(size_t)i * D + j] + (double)(c * (zi * zt[j]));
-  }
-  for (int i = tid; i < D; i += 256) bsh[i] = (double)zt[i];
-  __syncthreads();
-  for (int k = 0; k < D; ++k) {
-    // pivot: first row of maximal |A[i][k]|, i >= k (idamax)
-    double best = -1.0;
-    int bi = D;
-    for (int i = k + tid; i < D; i += 256) {
-      const double v = fabs(A[(size_t)i * D + k]);
-      if (v > best) {
-        best = v;
-        bi = i;
-      }
+  for (int i = wave; i < Dp; i += CR_T / 64) {
+    if (i < D) {
+      const float zi = zt[i];
+      for (int j = lane; j < Dp; j += 64)
+        A[(size_t)i * ld + j] = j < D ? He[(size_t)i * D + j] + (double)(c * (zi * zt[j])) : 0.0;
+      if (lane == 0) A[(size_t)i * ld + Dp] = (double)zi;
+    } else {
+      for (int j = lane; j < ld; j += 64) A[(size_t)i * ld + j] = j == i ? 1.0 : 0.0;
     }
-    rv[tid] = best;
-    ri[tid] = bi;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (tid < s) {
-        const double a = rv[tid], b = rv[tid + s];
-        const int ia = ri[tid], ib = ri[tid + s];
-        if (b > a || (b == a && ib < ia)) {
-          rv[tid] = b;
-          ri[tid] = ib;
-        }
+  }
+  for (int i = tid; i < Dp; i += CR_T) phys[i] = i;
+  __syncthreads();
+  CR_ST(0);
+  bool singular = false;
+  constexpr int w = CR_NB;
+  for (int k0 = 0; k0 < Dp && !singular; k0 += CR_NB) {
+    const int m = Dp - k0;
+    // the panel: thread i holds logical row k0 + i in registers.  `me` is tid made opaque
+    // per panel, so the compiler does not hoist the 64 per-column row tests (tid == j,
+    // tid > j) out of the panel loop into spilled mask registers
+    int me = tid;
+    asm volatile("" : "+v"(me));
+    const bool own = me < m;
+    double P[CR_NB];
+    if (own) {
+      const double* src = A + (size_t)phys[k0 + tid] * ld + k0;
+#pragma unroll
+      for (int t = 0; t < w; ++t) P[t] = src[t];
+    }
+    CR_ST(1);
+    double v = own ? fabs(P[0]) : -1.0;
+    int vi = own ? me : 0x7fffffff;
+    static_for<CR_NB>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      // pivot: first row of maximal |a| (idamax); this column's candidates were
+      // computed by the previous column's update
+      // one barrier per column: each wave publishes its best (value, row) and that row's
+      // data, thread j its own row, in the buffer of this column's parity (a thread can
+      // only reach column j + 2's writes after every thread passed column j + 1's barrier)
+      constexpr int buf = j & 1;
+      wave_argmax(v, vi);
+      if (lane == 0) {
+        wv[buf][wave] = v;
+        wi[buf][wave] = vi;
+      }
+      if (me == vi) {
+#pragma unroll
+        for (int t = 0; t < w; ++t) wrow[buf][wave][t] = P[t];
+      }
+      if (me == j) {
+#pragma unroll
+        for (int t = 0; t < w; ++t) jrow[buf][t] = P[t];
       }
       __syncthreads();
-    }
-    const int piv = ri[0];
-    if (rv[0] == 0.0) {  // exactly singular: LAPACK's getrf reports it, numpy.linalg.inv raises
-      if (tid == 0) bad = 1;
-      break;
-    }
-    if (piv != k) {
-      for (int j = k + tid; j < D; j += 256) {
-        const double a = A[(size_t)k * D + j];
-        A[(size_t)k * D + j] = A[(size_t)piv * D + j];
-        A[(size_t)piv * D + j] = a;
+      CR_ST(2);
+      double best = wv[buf][0];
+      int p = wi[buf][0];
+#pragma unroll
+      for (int q = 1; q < CR_T / 64; ++q)
+        if (wv[buf][q] > best || (wv[buf][q] == best && wi[buf][q] < p)) {
+          best = wv[buf][q];
+          p = wi[buf][q];
+        }
+      // exactly singular: LAPACK's getrf reports it, numpy.linalg.inv raises (uniform; the
+      // remaining columns only pass their barriers)
+      singular = singular || best == 0.0;
+      if (singular) p = j;
+      const double* prow = wrow[buf][p >> 6];
+      if (p != j && me == 0) {
+        const int t = phys[k0 + j];
+        phys[k0 + j] = phys[k0 + p];
+        phys[k0 + p] = t;
       }
-      if (tid == 0) {
-        const double b = bsh[k];
-        bsh[k] = bsh[piv];
-        bsh[piv] = b;
+      CR_ST(3);
+      if (p != j && me == j) {
+#pragma unroll
+        for (int t = 0; t < w; ++t) P[t] = prow[t];
+      }
+      if (p != j && me == p) {
+#pragma unroll
+        for (int t = 0; t < w; ++t) P[t] = jrow[buf][t];
+      }
+      v = -1.0;
+      vi = 0x7fffffff;
+      if (!singular && own && me > j) {
+        const double l = P[j] / prow[j];
+        P[j] = l;
+        if constexpr (j + 1 < w) {
+          P[j + 1] -= l * prow[j + 1];
+          v = fabs(P[j + 1]);
+          vi = me;
+        }
+#pragma unroll
+        for (int t = j + 2; t < w; ++t) P[t] -= l * prow[t];
+      }
+      CR_ST(4);
+    });
+    if (singular) break;
+    // L11 / L21 to the LDS panel; U11 rows back to the workspace (the back substitution reads them)
+    if (own) {
+#pragma unroll
+      for (int t = 0; t < w; ++t) crl[tid * CR_PS + t] = P[t];
+    }
+    if (tid < w) {
+      double* dst = A + (size_t)phys[k0 + tid] * ld + k0;
+#pragma unroll
+      for (int t = 0; t < w; ++t) dst[t] = P[t];
+    }
+    __syncthreads();
+    // U12 = L11^-1 A12 over the trailing columns and b, one column per thread (nc <= 513)
+    const int c0 = k0 + w, nc = ld - c0;
+    if (tid < nc) {
+      double* Ac = A + c0 + tid;
+      double u[CR_NB];
+#pragma unroll
+      for (int j = 0; j < w; ++j) u[j] = Ac[(unsigned)(phys[k0 + j] * ld)];
+#pragma unroll
+      for (int j = 1; j < w; ++j) {
+#pragma unroll
+        for (int i = 0; i < j; ++i) u[j] -= crl[j * CR_PS + i] * u[i];
+        __builtin_amdgcn_sched_barrier(0);  // one row's L11 reads at a time (register pressure)
+      }
+      // the map re-read (memory clobber) rather than 32 offsets held across the solve
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < w; ++j) Ac[(unsigned)(phys[k0 + j] * ld)] = u[j];
+    }
+    __syncthreads();
+    CR_ST(5);
+    // A22 -= L21 U12: items of CR_SEG rows x 64 columns, one per wave at a time; U12's
+    // column loaded once per item, the rows in chunks of CR_R with the next chunk's loads
+    // issued before the current chunk's arithmetic
+    const int r0 = k0 + w, nr = Dp - r0;
+    if (nr > 0) {
+      const int rg = nr / CR_SEG, cg = (nc + 63) / 64;
+      for (int item = wave; item < rg * cg; item += CR_T / 64) {
+        const int ri = item / cg, ci = item - ri * cg;
+        const int col = c0 + ci * 64 + lane;
+        if (col < ld) {
+          double u[CR_NB];
+#pragma unroll
+          for (int t = 0; t < w; ++t) u[t] = A[(unsigned)(phys[k0 + t] * ld + col)];
+          const int rb = r0 + CR_SEG * ri;
+          double a[2][CR_R];
+          unsigned off[2][CR_R];
+#pragma unroll
+          for (int q = 0; q < CR_R; ++q) {
+            off[0][q] = (unsigned)(phys[rb + q] * ld + col);
+            a[0][q] = A[off[0][q]];
+          }
+          static_for<CR_SEG / CR_R>([&](auto cc) {
+            constexpr int ch = decltype(cc)::value, cur = ch & 1, nxt = cur ^ 1;
+            if constexpr (ch + 1 < CR_SEG / CR_R) {
+#pragma unroll
+              for (int q = 0; q < CR_R; ++q) {
+                off[nxt][q] = (unsigned)(phys[rb + (ch + 1) * CR_R + q] * ld + col);
+                a[nxt][q] = A[off[nxt][q]];
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < CR_R; ++q) {
+              const double* L = crl + (rb - k0 + ch * CR_R + q) * CR_PS;
+#pragma unroll
+              for (int t0 = 0; t0 < w; t0 += 8) {
+#pragma unroll
+                for (int t = t0; t < t0 + 8; ++t) a[cur][q] -= L[t] * u[t];
+                __builtin_amdgcn_sched_barrier(0);  // eight L21 reads in flight at a time (register pressure)
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < CR_R; ++q) A[off[cur][q]] = a[cur][q];
+          });
+        }
       }
     }
     __syncthreads();
-    const double pv = A[(size_t)k * D + k];
-    for (int i = k + 1 + tid; i < D; i += 256) {
-      lcol[i] = A[(size_t)i * D + k] / pv;
-      prow[i] = A[(size_t)k * D + i];
-    }
-    __syncthreads();
-    // trailing update: 8 row groups x 32 consecutive columns (coalesced rows, no index division)
-    for (int i = k + 1 + (tid >> 5); i < D; i += 8) {
-      const double li = lcol[i];
-      double* Ai = A + (size_t)i * D;
-      for (int j = k + 1 + (tid & 31); j < D; j += 32) Ai[j] -= li * prow[j];
-    }
-    for (int i = k + 1 + tid; i < D; i += 256) bsh[i] -= lcol[i] * bsh[k];
-    __syncthreads();
+    CR_ST(6);
   }
-  __syncthreads();
-  if (bad) {
+  if (singular) {
     if (tid == 0) {
       out[blockIdx.x] = NAN;
       status[blockIdx.x] = 1;
     }
     return;
   }
-  // back substitution, column-oriented: y_i = b_i / U_ii, then b_j -= U_ji y_i for j < i
-  for (int i = D - 1; i >= 0; --i) {
-    if (tid == 0) bsh[i] = bsh[i] / A[(size_t)i * D + i];
+  // back substitution: y_i = b_i / U_ii, then b_j -= U_ji y_i for j < i, i descending;
+  // U's columns [lo, hi) of rows [0, hi) staged in LDS per block
+  double* bsh = crl;
+  double* ub = crl + 768;
+  for (int i = tid; i < Dp; i += CR_T) bsh[i] = A[(size_t)phys[i] * ld + Dp];
+  for (int hi = Dp; hi > 0; hi -= CR_NB) {
+    const int lo = hi - CR_NB;
+    for (int r = tid >> 5; r < hi; r += CR_T / 32) ub[r * CR_PS + (tid & 31)] = A[(size_t)phys[r] * ld + lo + (tid & 31)];
     __syncthreads();
-    const double yi = bsh[i];
-    for (int j = tid; j < i; j += 256) bsh[j] -= A[(size_t)j * D + i] * yi;
+    if (wave == 0) {
+      const int row = lo + lane;
+      double b = lane < w ? bsh[row] : 0.0;
+      for (int i = hi - 1; i >= lo; --i) {
+        if (row == i) b = b / ub[row * CR_PS + (i - lo)];
+        const double yi = __shfl(b, i - lo, 64);
+        if (row < i) b -= ub[row * CR_PS + (i - lo)] * yi;
+      }
+      if (lane < w) bsh[row] = b;
+    }
+    __syncthreads();
+    for (int row = tid; row < lo; row += CR_T) {
+      const double* Ur = ub + row * CR_PS;
+      double b = bsh[row];
+      for (int i = hi - 1; i >= lo; --i) b -= Ur[i - lo] * bsh[i];
+      bsh[row] = b;
+    }
     __syncthreads();
   }
+  CR_ST(7);
+#ifdef KP_CR_STAMPS
+  if (blockIdx.x == 0 && tid == 0)
+    printf("[cr stamps] build %llu panel-load %llu pivot %llu swap %llu elim %llu u12 %llu trailing %llu backsub %llu\n",
+           st_acc[0], st_acc[1], st_acc[2], st_acc[3], st_acc[4], st_acc[5], st_acc[6], st_acc[7]);
+#endif
+  double* rv = crl + 512;
   const double om = (double)(1.0f - sig);
-  double acc = 0.0;
-  for (int j = tid; j < D; j += 256) acc += (double)zp[j] * (om * bsh[j]);
-  rv[tid] = acc;
+  if (tid < 256) {
+    double acc = 0.0;
+    for (int j = tid; j < D; j += 256) acc += (double)zp[j] * (om * bsh[j]);
+    rv[tid] = acc;
+  }
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (tid < s) rv[tid] += rv[tid + s];
@@ -347,15 +587,19 @@ void criage_relevance(kp_ctx* c, int n, const int32_t* items, int n_ents, const 
   hipLaunchKernelGGL(kp_criage_hessian, dim3((D * D + 255) / 256, n_ents), dim3(256), 0, c->stream, D, dOff, dX, dW,
                      dH);
   KP_HIP(hipGetLastError());
-  // candidates in chunks: one float64 D x D system per workgroup
-  const int chunk = std::max(1, std::min(n, (int)(((size_t)512 << 20) / ((size_t)D * D * sizeof(double)))));
-  double* dA = reinterpret_cast<double*>(ba.ensure(sizeof(double) * (size_t)chunk * D * D));
+  // candidates in chunks: one float64 D x (D + 1) system per workgroup
+  const int Dp = (D + CR_NB - 1) / CR_NB * CR_NB;
+  const size_t sys = (size_t)Dp * (Dp + 1);
+  const int chunk = std::max(1, std::min(n, (int)(((size_t)4 << 30) / (sys * sizeof(double)))));
+  double* dA = reinterpret_cast<double*>(ba.ensure(sizeof(double) * (size_t)chunk * sys));
+  const size_t lds = sizeof(double) * ((size_t)768 + (size_t)Dp * CR_PS);
   for (int i0 = 0; i0 < n; i0 += chunk) {
     const int m = std::min(chunk, n - i0);
     int32_t* dIt = upload(c, bit, it4.data() + 4 * (size_t)i0, (size_t)4 * m);
     double* dO = reinterpret_cast<double*>(bo.ensure(sizeof(double) * (size_t)m));
     int32_t* dS = reinterpret_cast<int32_t*>(bs.ensure(sizeof(int32_t) * (size_t)m));
-    hipLaunchKernelGGL(kp_criage_solve, dim3(m), dim3(256), 0, c->stream, D, c->dp, dIt, dZ, c->dE, dH, dA, dO, dS);
+    hipLaunchKernelGGL(kp_criage_solve, dim3(m), dim3(CR_T), lds, c->stream, D, c->dp, dIt, dZ, c->dE, dH, dA, dO,
+                       dS);
     KP_HIP(hipGetLastError());
     KP_HIP(hipMemcpyAsync(out + i0, dO, sizeof(double) * m, hipMemcpyDeviceToHost, c->stream));
     KP_HIP(hipMemcpyAsync(status + i0, dS, sizeof(int32_t) * m, hipMemcpyDeviceToHost, c->stream));

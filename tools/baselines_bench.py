@@ -33,6 +33,7 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--preds", type=int, default=8)
+    ap.add_argument("--dump", default=None, help="save the CRIAGE relevances (float64, .npy) here")
     a = ap.parse_args()
     import kelpie_amd.baselines as kb
     wl = bench.WORKLOADS["complex-fb15k237-necessary"]
@@ -51,9 +52,11 @@ def main():
         jobs = [(p, c) for p, c in jobs if c]
         n = sum(len(c) for _, c in jobs)
         t0 = time.perf_counter()
-        eng.compute_relevance_multi(jobs, "head")  # every prediction's candidates in one launch
+        res = eng.compute_relevance_multi(jobs, "head")  # every prediction's candidates in one launch
         dt = time.perf_counter() - t0
         out[name] = (n, dt)
+        if name == "criage" and a.dump:
+            np.save(a.dump, np.array([np.nan if v is None else float(v) for r in res for v in r], dtype=np.float64))
     # CPU oracle on a bounded sample (the first prediction's first candidates)
     from oracle import kelpie_oracle as ko
     om = ko.OracleModel("ComplEx", w, wl["dim"], {"init_scale": 1e-3})
