@@ -435,14 +435,40 @@ void bernoulli_words(TorchMt& mt, uint64_t n, double p, uint32_t* out, std::vect
 void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np,
                  std::vector<int32_t>& idx) {
   np.load(np_key, np_pos);
-  idx.resize(std::max(R, 1));
-  for (int i = 0; i < R; ++i) idx[i] = i;
+  idx.resize(2 * (size_t)std::max(R, 1));
+  int32_t* perm = idx.data();
+  int32_t* jv = perm + std::max(R, 1);  // jv[i] = the interval(i) draw of this epoch
+  for (int i = 0; i < R; ++i) perm[i] = i;
   for (int e = 0; e < epochs; ++e) {
-    for (int i = R - 1; i >= 1; --i) {  // for i in reversed(range(1, n)): j = interval(i)
-      const uint32_t j = np.interval((uint32_t)i);
-      std::swap(idx[i], idx[j]);
+    // for i in reversed(range(1, n)): j = random_interval(i) (masked rejection): one draw
+    // per iteration, branch-free; a rejected draw leaves i unchanged and its jv[i] is
+    // overwritten by the next one (the draws consumed are numpy's, in its order)
+    int i = R - 1;
+    while (i >= 1) {
+      if (np.pos >= kN) {
+        mt_twist(np.key);
+        np.temper_all();
+        np.pos = 0;
+      }
+      const int n = kN - np.pos;  // draws left in this block
+      const uint32_t* tb = np.tb + np.pos;
+      // the loop-carried chain is only compare -> subtract: the mask for i - 1 is derived
+      // from i and the current mask alongside (it halves when i - 1 drops below its top bit)
+      uint32_t ui = (uint32_t)i, mask = 0xFFFFFFFFu >> __builtin_clz(ui);
+      int k = 0;
+      for (; k < n && ui >= 1; ++k) {
+        const uint32_t v = tb[k] & mask;
+        jv[ui] = (int32_t)v;
+        const uint32_t m1 = (ui - 1 > (mask >> 1)) ? mask : (mask >> 1);
+        const bool acc = v <= ui;
+        mask = acc ? m1 : mask;
+        ui -= acc;
+      }
+      i = (int)ui;
+      np.pos += k;
     }
-    std::memcpy(out + (size_t)e * 3 * R, idx.data(), sizeof(int32_t) * R);
+    for (int t = R - 1; t >= 1; --t) std::swap(perm[t], perm[jv[t]]);
+    std::memcpy(out + (size_t)e * 3 * R, perm, sizeof(int32_t) * R);
   }
   np.store(np_key, np_pos);
 }
