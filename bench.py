@@ -54,7 +54,7 @@ CONVE_HP = {"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.
 WORKLOADS = {
     # BASELINE.json configs[2]: the north-star target (>= 50x, ComplEx on FB15k-237)
     "complex-fb15k237-sufficient": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="sufficient",
-                                        hp=COMPLEX_HP, candidates=20, convert=10, preds_per_step=1),
+                                        hp=COMPLEX_HP, candidates=20, convert=10, preds_per_step=1, depth=3),
     "complex-fb15k237-necessary": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="necessary",
                                        hp=COMPLEX_HP, candidates=20, preds_per_step=16),
     # BASELINE.json configs[1]
@@ -65,7 +65,7 @@ WORKLOADS = {
                                      hp=COMPLEX_DB100K_HP, candidates=20, preds_per_step=16),
     "complex-db100k-sufficient": dict(model="ComplEx", shape="DB100K", dim=200, mode="sufficient",
                                       hp=COMPLEX_DB100K_HP, candidates=20, convert=10, preds_per_step=1,
-                                      cpu_conversions=2),
+                                      cpu_conversions=2, depth=3),
     # BASELINE.json configs[4]
     "conve-yago310-necessary": dict(model="ConvE", shape="YAGO3-10", dim=200, mode="necessary", hp=CONVE_HP,
                                     candidates=20, preds_per_step=8, hidden_dropout=0.2),
@@ -348,16 +348,21 @@ def main():
     # Each step is one batch started from cleared per-prediction caches (the base
     # post-trainings are part of the work).  compute_relevance_pipeline schedules
     # step k+1's reference-order draws on the host while step k runs on the GPU.
+    # batches in flight (one device context each): 3 for the sufficient workloads, whose
+    # small batches leave the device idle during a batch's planning and download
+    # (default 588 -> 649 cand/s, profiles/r02v_depth.txt), 2 for the others (a third
+    # context costs the necessary workload 10 %)
+    depth = int(os.environ.get("KELPIE_PIPELINE_DEPTH", wl.get("depth", 2)))
     if args.warmup:
-        eng.compute_relevance_pipeline([items_of(jobs[i]) for i in range(args.warmup)])
-        # the pipeline's second device context (engine.compute_relevance_pipeline) runs
+        eng.compute_relevance_pipeline([items_of(jobs[i]) for i in range(args.warmup)], depth=depth)
+        # the pipeline's other device contexts (engine.compute_relevance_pipeline) run
         # the first warm-up batch too; no random draws are consumed
-        eng.warm_contexts(items_of(jobs[0]))
+        eng.warm_contexts(items_of(jobs[0]), depth=depth)
     kd.barrier()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    outs = eng.compute_relevance_pipeline([items_of(jobs[i]) for i in range(args.warmup, n_steps)])
+    outs = eng.compute_relevance_pipeline([items_of(jobs[i]) for i in range(args.warmup, n_steps)], depth=depth)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     kd.barrier()
@@ -454,6 +459,7 @@ def main():
                            "dim": wl["dim"], "mode": wl["mode"], "candidates_per_step": wl["candidates"] * per_step,
                            "predictions_per_step": per_step,
                            "conversion_entities": wl.get("convert"), "epochs": wl["hp"]["epochs"],
+                           "batches_in_flight": depth,
                            "parallelism": f"each batch's post-trainings sharded over {world} rank(s), "
                                           f"host schedule replicated, one all-gather per batch"},
                 "rank_delta_match_rate": (parity.get("fp32") or {}).get("match_rate"),
