@@ -161,3 +161,48 @@ def test_multi_equals_batch_cpu():
     multi = dp.compute_relevance_multi(jobs, "head")
     for (p, ts), m in zip(jobs, multi):
         assert m == dp.compute_relevance_batch(p, "head", ts)
+
+
+# ---------------------------------------------------------------------------- CRIAGE at production size
+def _criage_fullrank(dim, backend):
+    """A ComplEx model of dimension ``dim`` (D = 2 dim float64 systems: 400 pads to the
+    blocked solver's 416 with an identity border, 320 needs none) whose perspective
+    entity 0 has D + 60 tail triples, so H_0 has full rank; the engine's relevances
+    against the oracle's (numpy.linalg.inv, as the reference): float64 solves of systems
+    built in float32 (x = E_h * R_r, sigma(e . z)), whose dot products sum in another
+    order on the device, so the systems differ in their last float32 bits: relative 1e-5."""
+    rng = np.random.default_rng(dim)
+    ne, nr, D = 700, 6, 2 * dim
+    heads = rng.choice(np.arange(1, ne), size=D + 60, replace=False)
+    train = np.array([(int(h), int(rng.integers(nr)), 0) for h in heads] +
+                     [(int(rng.integers(1, ne)), int(rng.integers(nr)), int(rng.integers(1, ne))) for _ in range(400)])
+    test = np.array([(int(heads[0]), 0, 0)])
+    E = (0.3 * rng.standard_normal((ne, D))).astype(np.float32)
+    R = (0.3 * rng.standard_normal((2 * nr, D))).astype(np.float32)
+    ds = ka.Dataset(ne, nr, train, test[:0], test)
+    model = ka.ComplEx(ds, E, R, init_scale=1e-3)
+    if backend == "cpu":
+        from cpu_backend import OracleBackedContext
+        model._ctx = OracleBackedContext(model)
+    om = ko.OracleModel("ComplEx", {"entity_embeddings": E, "relation_embeddings": R}, dim, {"init_scale": 1e-3})
+    ods = ko.OracleDataset(ne, nr, train, test[:0], test)
+    pred = (int(heads[1]), 1, 0)
+    cands = [tuple(int(v) for v in t) for t in train[:12]]
+    got = kb.NecessaryCriageEngine(model, ds).compute_relevance_batch(pred, cands, "tail")
+    for t, v in zip(cands, got):
+        exp = float(ko.criage_relevance(om, ods, pred, t, "tail", "necessary"))
+        assert v is not None and abs(v - exp) <= 1e-5 * max(1e-3, abs(exp)), (dim, t, v, exp)
+
+
+import kelpie_amd as ka  # noqa: E402
+
+
+@pytest.mark.parametrize("dim", [200, 160])
+def test_criage_fullrank_host_protocol_cpu(dim):
+    _criage_fullrank(dim, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim", [200, 160])
+def test_criage_fullrank_gpu_vs_oracle(dim):
+    _criage_fullrank(dim, "gpu")
