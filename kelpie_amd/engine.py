@@ -38,6 +38,7 @@ class _Slot:
     pred: tuple
     filt: list
     result: dict = field(default=None)
+    rng_at: tuple = field(default=None)  # (arena, word offset) of rng in a deferred draw arena
 
 
 def _contiguous_draws(slots, total):
@@ -45,6 +46,22 @@ def _contiguous_draws(slots, total):
     in one buffer (the deferred arena of ReferenceRNG), else a concatenation."""
     if total == 0:
         return np.zeros(1, np.int32)
+    # fused TransE draws record where they lie (plain ints: no per-array address queries)
+    first = None
+    for s in slots:
+        if not s.rng.size:
+            continue
+        at = s.rng_at
+        if at is None:
+            break
+        if first is None:
+            first, arena, pos = at[1], at[0], at[1]
+        if at[0] is not arena or at[1] != pos:
+            break
+        pos += s.rng.size
+    else:
+        if first is not None and pos - first == total:
+            return arena[first:first + total]
     arrs = [s.rng for s in slots if s.rng.size]
     first = arrs[0]
     base = first.base
@@ -221,12 +238,17 @@ class PostTrainingEngine(RelevanceEngine):
         xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, [c["R_base"] for c in calls],
                                               [c["R_pt"] for c in calls], int(hp["epochs"]),
                                               int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1)
+        spans = self.rng.last_spans
         for i, c in enumerate(calls):
             db, dp = draws[i]
             if c["base"] is not None:
                 c["base"].x0, c["base"].rng = xb[i], db
+                if spans is not None:
+                    c["base"].rng_at = (spans[i][0], spans[i][1])
             if c["pt"] is not None:
                 c["pt"].x0, c["pt"].rng = xp[i], dp
+                if spans is not None:
+                    c["pt"].rng_at = (spans[i][0], spans[i][2])
 
     def _schedule_all(self, items, checkpoints):
         """_schedule_multi, with every queued TransE call's draws made before it returns or raises."""
