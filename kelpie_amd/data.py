@@ -256,6 +256,7 @@ class KelpieView:
             if b == k:
                 self.filter[p + R][a] += 1
         self.index = {t: i for i, t in enumerate(self.base_triples)}
+        self._filter_lists = {}  # rel -> filter_for(rel) without a delta (shared: callers copy or only read)
         self.base_arr = np.asarray(self.base_triples, dtype=np.int32).reshape(-1, 3)
         self.base_rows = self._rows(self.base_arr)
 
@@ -277,22 +278,32 @@ class KelpieView:
         return Dataset.replace_entity_in_triple(tuple(triple), self.original_entity, self.kelpie_entity)
 
     def filter_for(self, rel, delta=None):
-        """Filtered-out entities of key (kelpie, rel), after an optional multiset delta."""
-        c = Counter(self.filter.get(rel, {}))
-        if delta:
-            for e, n in delta.items():
-                c[e] += n
-        return [e for e, n in c.items() if n > 0]
+        """Filtered-out entities of key (kelpie, rel), after an optional multiset delta
+        (the multiset's insertion order: base entities first, then the delta's new ones)."""
+        base = self.filter.get(rel)
+        if not delta:
+            if base is None:
+                return []
+            cached = self._filter_lists.get(rel)
+            if cached is None:
+                cached = self._filter_lists[rel] = [e for e, n in base.items() if n > 0]
+            return cached
+        base = base or {}
+        out = [e for e, n in base.items() if n + delta.get(e, 0) > 0]
+        out += [e for e, n in delta.items() if e not in base and n > 0]
+        return out
 
     def _delta(self, conv, sign):
         k = self.kelpie_entity
         R = self.dataset.num_relations
-        d = defaultdict(Counter)
+        d = {}
         for a, p, b in conv:
             if a == k:
-                d[p][b] += sign
+                dp = d.setdefault(p, {})
+                dp[b] = dp.get(b, 0) + sign
             if b == k:
-                d[p + R][a] += sign
+                dp = d.setdefault(p + R, {})
+                dp[a] = dp.get(a, 0) + sign
         return d
 
     def removed(self, triples):
@@ -307,7 +318,7 @@ class KelpieView:
         kept = self.base_arr[keep]
         delta = self._delta(conv, -1)
         for rel, cnt in delta.items():
-            cur = self.filter.get(rel, Counter())
+            cur = self.filter.get(rel, {})
             for e, n in cnt.items():
                 if cur.get(e, 0) + n < 0:
                     raise ValueError("list.remove(x): x not in list")
