@@ -13,6 +13,7 @@ would.
 from __future__ import annotations
 
 import math
+import os
 import random
 import time
 from collections import OrderedDict
@@ -38,43 +39,15 @@ class _Slot:
     pred: tuple
     filt: list
     result: dict = field(default=None)
-    rng_at: tuple = field(default=None)  # (arena, word offset) of rng in a deferred draw arena
 
 
 def _contiguous_draws(slots, total):
-    """The slots' draws as one int32 array: a view when they already lie back to back
-    in one buffer (the deferred arena of ReferenceRNG), else a concatenation."""
+    """The slots' draws as one fresh int32 array.  Handing the library a view of the
+    deferred draw arena instead (no copy) measured slower end to end: its upload from
+    the arena's pages, first touched by the RNG worker threads, took 10-20 ms per TransE
+    batch against 3 ms after this copy (profiles/r02zd_transe_draws_upload.txt)."""
     if total == 0:
         return np.zeros(1, np.int32)
-    # fused TransE draws record where they lie (plain ints: no per-array address queries)
-    first = None
-    for s in slots:
-        if not s.rng.size:
-            continue
-        at = s.rng_at
-        if at is None:
-            break
-        if first is None:
-            first, arena, pos = at[1], at[0], at[1]
-        if at[0] is not arena or at[1] != pos:
-            break
-        pos += s.rng.size
-    else:
-        if first is not None and pos - first == total:
-            return arena[first:first + total]
-    arrs = [s.rng for s in slots if s.rng.size]
-    first = arrs[0]
-    base = first.base
-    if base is not None and all(a.dtype == np.int32 and a.base is base and a.flags.c_contiguous for a in arrs):
-        addr = first.__array_interface__["data"][0]
-        end = addr
-        for a in arrs:
-            if a.__array_interface__["data"][0] != end:
-                break
-            end += 4 * a.size
-        else:
-            off = (addr - base.__array_interface__["data"][0]) // 4
-            return base.reshape(-1)[off:off + total]
     return np.concatenate([s.rng.reshape(-1) for s in slots]).astype(np.int32, copy=False)
 
 
@@ -238,17 +211,12 @@ class PostTrainingEngine(RelevanceEngine):
         xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, [c["R_base"] for c in calls],
                                               [c["R_pt"] for c in calls], int(hp["epochs"]),
                                               int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1)
-        spans = self.rng.last_spans
         for i, c in enumerate(calls):
             db, dp = draws[i]
             if c["base"] is not None:
                 c["base"].x0, c["base"].rng = xb[i], db
-                if spans is not None:
-                    c["base"].rng_at = (spans[i][0], spans[i][1])
             if c["pt"] is not None:
                 c["pt"].x0, c["pt"].rng = xp[i], dp
-                if spans is not None:
-                    c["pt"].rng_at = (spans[i][0], spans[i][2])
 
     def _schedule_all(self, items, checkpoints):
         """_schedule_multi, with every queued TransE call's draws made before it returns or raises."""

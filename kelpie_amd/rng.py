@@ -75,7 +75,6 @@ class ReferenceRNG:
     """Draws from the process-global torch / numpy generators (reference order)."""
 
     _defer_depth = 0
-    last_spans = None  # transe_calls: per call (arena, base draws' offset, post-training draws' offset)
 
     @contextlib.contextmanager
     def deferred(self):
@@ -183,15 +182,9 @@ class ReferenceRNG:
             sync()
         _set_state(st)
         draws, off, empty = [], 0, np.zeros(0, np.int32)
-        # where each call's draws lie in the deferred arena (engine._contiguous_draws)
-        at = (self._arena, self._arena_pos - total) if (self._defer_depth and total) else None
-        spans = [] if at is not None else None
         for a, b in sizes:
             draws.append((out[off:off + a] if a else empty, out[off + a:off + a + b] if b else empty))
-            if spans is not None:
-                spans.append((at[0], at[1] + off, at[1] + off + a))
             off += a + b
-        self.last_spans = spans
         return xb, xp, draws
 
     def conve_masks(self, n_rows_per_step, dim: int, p_drop: float) -> np.ndarray:
