@@ -119,6 +119,17 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
       for (int d = 0; d < DP; ++d) err_o = std::max(err_o, std::fabs(gO[d] - O[d]) / onorm);
     }
   }
+  // FNV-1a over the output bits: variants meant to be bitwise identical print the same hash
+  unsigned long long bits = 1469598103934665603ull;
+  auto fnv = [&](const std::vector<float>& v) {
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(v.data());
+    for (size_t i = 0; i < v.size() * 4; ++i) bits = (bits ^ p[i]) * 1099511628211ull;
+  };
+  if (MODE != ATT_BCE_O) {
+    fnv(hm);
+    fnv(hl);
+  }
+  fnv(hO);
   const double flops = (MODE == ATT_SOFTMAX ? 2.0 : 4.0) * DP * (double)nq * n_ent;
 #ifdef KP_ATTN3_STAMPS
   {
@@ -134,9 +145,9 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
   }
 #endif
   printf("{\"DB\": %d, \"mode\": %d, \"n_ent\": %d, \"nq\": %d, \"parts\": %d, \"ranges\": %d, \"n_wg\": %d, "
-         "\"ms\": %.5f, \"tflops\": %.2f, \"frac_bf16x6\": %.4f, \"err_l\": %.3e, \"err_o\": %.3e}\n",
+         "\"ms\": %.5f, \"tflops\": %.2f, \"frac_bf16x6\": %.4f, \"err_l\": %.3e, \"err_o\": %.3e, \"bits\": \"%016llx\"}\n",
          DB, MODE, n_ent, nq, parts, plan.wk.ranges, plan.n_wg, ms, flops / ms / 1e9, flops / ms / 1e9 / 419.43,
-         err_l, err_o);
+         err_l, err_o, bits);
   return 0;
 }
 
