@@ -76,6 +76,12 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     // the fp32-MFMA kernel of kp_attn.hpp
     c->attn_mode = 1;
     if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "f32") == 0 ? 0 : 1;
+    // ConvE FC GEMMs in the step loop (bit 0 forward, bit 1 backward on kp_gemm3_abt):
+    // KP_FC=f32 | fwd | bwd | both; with the fp32 attention always fp32
+    c->fc_mode = 0;
+    if (const char* a = std::getenv("KP_FC"))
+      c->fc_mode = std::strcmp(a, "f32") == 0 ? 0 : std::strcmp(a, "fwd") == 0 ? 1 : std::strcmp(a, "bwd") == 0 ? 2 : 3;
+    if (c->attn_mode == 0) c->fc_mode = 0;
     if (const char* a = std::getenv("KP_ATTN_PART"))
       c->attn_part = std::strcmp(a, "streamk") == 0 ? 1 : std::strcmp(a, "ranges") == 0 ? 2 : 0;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -112,6 +118,10 @@ int kp_ctx_destroy(kp_ctx* c) {
     if (p) (void)hipFree(p);
   for (auto& b : c->ws) b.release();
   c->e3.release();
+  c->e3ts.release();
+  c->e3pre.release();
+  c->fc3.release();
+  c->fct3.release();
   train_state_free(c);
   for (auto e : c->evpool) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);

@@ -95,11 +95,14 @@ struct kp_ctx {
   bool time_hot = true;
   // attention contraction: 0 = fp32 MFMA (kp_attn.hpp), 1 = bf16x3 MFMA (kp_attn3.hpp)
   int attn_mode = 0;
+  int fc_mode = 0;  // ConvE step-loop FC GEMMs on kp_gemm3_abt (bf16x3): bit 0 forward, bit 1 backward
   int attn_part = 0;  // kp_attn3 partition: 0 chosen per launch, 1 stream-K, 2 XCD-grouped ranges (KP_ATTN_PART)
   DevBuf e3;               // kp_attn3's split image of dE, built on first use
   bool e3_ready = false;
   DevBuf e3ts, e3pre;      // kp_attn3's fp64 tile sums / prefix sums of dE over tiles
   bool e3pre_ready = false;
+  DevBuf fc3, fct3;        // ConvE: three-piece bf16 images of the FC weight and its transpose (kp_gemm3.hip)
+  bool fc3_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
   std::vector<hipEvent_t> evpool;
@@ -185,6 +188,15 @@ void train_state_free(kp_ctx* c);
 // out[z][m][n] = act(sum_{k in split z} A[m][k] B[n][k] + (z == 0 ? bias[n] : 0)), fp32 MFMA
 void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
                      int ldo, const float* bias, int act, int ksplit);
+// the same on bf16 MFMA with three-piece operands (kp_gemm3.hip): B3 is a split image
+// ([3][rows][ld] bf16, split3_rows), A one too or fp32 (a_f32: split while staged);
+// K and the leading dims multiples of 8
+void launch_gemm3_abt(kp_ctx* c, const void* A, bool a_f32, int lda, int M, const uint16_t* B3, int ldb, int N,
+                      int K, float* out, int ldo, const float* bias, int act, int ksplit);
+// X [rows][ld] fp32 -> [3][rows][ld] bf16 pieces (columns [0, cols); the rest left as is)
+void split3_rows(kp_ctx* c, const float* X, int rows, int cols, int ld, uint16_t* out);
+// ConvE: the FC weight's [dim][hidden] and its transpose's [hidden][dim] split images (built once)
+const uint16_t* conve_fc3(kp_ctx* c, bool transposed);
 enum { RANK_TRIPLE_RESULTS = 0, RANK_PREDICT_TAILS = 1, RANK_SORT_POSITION = 2 };
 void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
                        const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
