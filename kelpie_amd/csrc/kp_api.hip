@@ -77,7 +77,8 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     c->attn_mode = 1;
     if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "f32") == 0 ? 0 : 1;
     // ConvE FC GEMMs in the step loop (bit 0 forward, bit 1 backward on kp_gemm3_abt):
-    // KP_FC=f32 | fwd | bwd | both; with the fp32 attention always fp32
+    // KP_FC=f32 | fwd | bwd | both; fp32 by default (the bf16x3 forms measured slower end to
+    // end) and always with the fp32 attention
     c->fc_mode = 0;
     if (const char* a = std::getenv("KP_FC"))
       c->fc_mode = std::strcmp(a, "f32") == 0 ? 0 : std::strcmp(a, "fwd") == 0 ? 1 : std::strcmp(a, "bwd") == 0 ? 2 : 3;
