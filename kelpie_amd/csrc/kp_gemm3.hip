@@ -28,12 +28,13 @@ constexpr int G3_BK = 32;
 constexpr int G3_RS = 48;                // LDS row stride in bf16 (96 B)
 constexpr int G3_PS = 64 * G3_RS;        // one piece of one operand tile (bf16)
 constexpr int G3_STAGE = 2 * 3 * G3_PS;  // A and B pieces of one stage
-constexpr size_t G3_LDS = 2u * G3_STAGE * sizeof(__bf16);  // 73,728 B
 
 // A_F32: A arrives as fp32 [M][lda] and each workgroup splits its own A tiles while staging
 // them (the ConvE forward, whose 9728-wide activations four column tiles read: a split
 // image would cost more HBM traffic than the redundant split costs VALU)
-template <bool A_F32>
+// NST: LDS stages (2: 73,728 B, two workgroups per CU; 1: 36,864 B, four, with a second
+// barrier per k tile)
+template <bool A_F32, int NST>
 __global__ __launch_bounds__(256) void kp_gemm3_abt(const void* __restrict__ Av, int lda, int M,
                                                     const __bf16* __restrict__ B3, int ldb, int N, int k_begin,
                                                     int k_end, float* __restrict__ out, int ldo,
@@ -103,12 +104,16 @@ __global__ __launch_bounds__(256) void kp_gemm3_abt(const void* __restrict__ Av,
 
   if (kb < ke) {
     gload(kb);
-    lstore(0);
+    if (NST == 2) lstore(0);
   }
-  __syncthreads();
+  if (NST == 2) __syncthreads();
   int st = 0;
   for (int k0 = kb; k0 < ke; k0 += G3_BK) {
     const bool more = k0 + G3_BK < ke;
+    if (NST == 1) {
+      lstore(0);
+      __syncthreads();
+    }
     if (more) gload(k0 + G3_BK);
     const __bf16* sa = g3s + st * G3_STAGE;
     const __bf16* sb = sa + 3 * G3_PS;
@@ -123,9 +128,9 @@ __global__ __launch_bounds__(256) void kp_gemm3_abt(const void* __restrict__ Av,
       for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(sb + p * G3_PS + (16 * n + c) * G3_RS + 8 * g);
       acc[n] = kpattn::mfma3(a, b, acc[n]);
     }
-    if (more) lstore(st ^ 1);
+    if (NST == 2 && more) lstore(st ^ 1);
     __syncthreads();
-    st ^= 1;
+    if (NST == 2) st ^= 1;
   }
   // C block n: lane (g, c) holds rows 16 w + 4 g + r, column 16 n + c
 #pragma unroll
@@ -176,12 +181,17 @@ void launch_gemm3_abt(kp_ctx* c, const void* A, bool a_f32, int lda, int M, cons
   KP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && K <= lda && K <= ldb,
              "gemm3: K and leading dims must be multiples of 8, K within them");
   dim3 grid((N + 63) / 64, (M + 63) / 64, std::max(1, ksplit));
-  if (a_f32)
-    hipLaunchKernelGGL(kp_gemm3_abt<true>, grid, dim3(256), G3_LDS, c->stream, A, lda, M,
-                       reinterpret_cast<const __bf16*>(B3), ldb, N, 0, K, out, ldo, bias, act);
-  else
-    hipLaunchKernelGGL(kp_gemm3_abt<false>, grid, dim3(256), G3_LDS, c->stream, A, lda, M,
-                       reinterpret_cast<const __bf16*>(B3), ldb, N, 0, K, out, ldo, bias, act);
+  static const bool one_stage = std::getenv("KP_FC_STAGES") && std::atoi(std::getenv("KP_FC_STAGES")) == 1;
+  const __bf16* b3 = reinterpret_cast<const __bf16*>(B3);
+  const size_t lds = (one_stage ? 1 : 2) * G3_STAGE * sizeof(__bf16);
+#define KP_G3(AF, NS) \
+  hipLaunchKernelGGL((kp_gemm3_abt<AF, NS>), grid, dim3(256), lds, c->stream, A, lda, M, b3, ldb, N, 0, K, out, ldo, bias, act)
+  if (a_f32) {
+    if (one_stage) KP_G3(true, 1); else KP_G3(true, 2);
+  } else {
+    if (one_stage) KP_G3(false, 1); else KP_G3(false, 2);
+  }
+#undef KP_G3
   KP_HIP(hipGetLastError());
 }
 
