@@ -47,3 +47,19 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean resources stamps diag
+
+# host sanitizer builds of the library's host C++ (kp_rng.cpp worker pool / arenas,
+# kp_graph.cpp) linked into tests/native/host_san_driver.cpp; run by
+# tests/test_host_sanitizers.py (CPU suite), or by hand: make asan tsan
+SAN_SRC := kelpie_amd/csrc/kp_rng.cpp kelpie_amd/csrc/kp_graph.cpp tests/native/host_san_driver.cpp
+SAN_FLAGS := -O1 -g -std=c++17 -fno-omit-frame-pointer -mavx2 -mfma -ffp-contract=off -pthread -Iinclude
+asan: build/san/host_asan
+tsan: build/san/host_tsan
+build/san/host_asan: $(SAN_SRC) include/kelpie_hip.h
+	@mkdir -p build/san
+	$(CXX) $(SAN_FLAGS) -fsanitize=address,undefined -fno-sanitize-recover=undefined $(SAN_SRC) -o $@
+build/san/host_tsan: $(SAN_SRC) include/kelpie_hip.h
+	@mkdir -p build/san
+	$(CXX) $(SAN_FLAGS) -fsanitize=thread $(SAN_SRC) -o $@
+
+.PHONY: asan tsan

@@ -80,16 +80,16 @@ def committed_traffic(workload, kernel):
     import json
     import re
     here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_{workload}_pmc.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f).get("fetch_bytes_per_launch", {})
     m = re.match(r"(kp_attn3?)<(\d+),(\w+)>", kernel)
     want = f"{m.group(1)}<{m.group(2)}, {ATT_MODES[m.group(3)]}>" if m else kernel
-    for name, v in d.items():
-        if want in name:
-            return v["hbm_bytes"], os.path.relpath(files[-1], here)
+    # newest first; a kernel-trace-only summary (no FETCH_SIZE pass) carries no bytes, so
+    # fall through to the newest file that does
+    for path in sorted(glob.glob(os.path.join(here, "profiles", f"r*_{workload}_pmc.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f).get("fetch_bytes_per_launch") or {}
+        for name, v in d.items():
+            if want in name and v.get("hbm_bytes"):
+                return v["hbm_bytes"], os.path.relpath(path, here)
     return None, None
 
 

@@ -866,8 +866,13 @@ inline AttnPlan attn_plan_ctx(const kp_ctx* c, int nq, int n_ent, int slots) {
 template <int DB, int MODE>
 void launch_attn3(kp_ctx* c, int n_ent, const float* Q, int nq, const AttnPlan& plan, float* m, float* l, float* O,
                   const float* qscale, float ylo) {
-  const uint8_t* E3 = split3_image<DB>(c);
   KP_REQUIRE(n_ent == c->n_ent, "attn3: key count differs from the table's (tile prefix sums)");
+  // the buffer descriptor's record count and the per-piece soffset are 32-bit: the split
+  // image (ROW_B per entity, whole tiles, 1 KiB slack) must stay below 2^31 bytes
+  // (D = 400: ~890k entities; out-of-range buffer loads would return zeros silently)
+  KP_REQUIRE((long long)(n_ent + 31) / 32 * 32 * split3_row_bytes(16 * DB) + 1024 < (1LL << 31),
+             "attn3: table too large for the 32-bit buffer descriptor of the split image");
+  const uint8_t* E3 = split3_image<DB>(c);
   const double* pre = tile_prefix<DB>(c);
   hipLaunchKernelGGL((kp_attn3<DB, MODE>), dim3(plan.n_wg), dim3(256), attn3_lds_bytes(DB), c->stream, E3, n_ent, Q,
                      nq, plan.wk, m, l, O, qscale, ylo, pre);

@@ -34,6 +34,7 @@
 #include <functional>
 #include <mutex>
 #include <new>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -473,6 +474,9 @@ void bernoulli_words(TorchMt& mt, uint64_t n, double p, uint32_t* out, std::vect
 
 void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np,
                  std::vector<int32_t>& idx) {
+  // validated here, on the thread that owns the live numpy state while draws are queued
+  // (the enqueueing thread must not read it: the sequential worker may be writing it)
+  if (*np_pos < 0 || *np_pos > kN) throw std::invalid_argument("numpy MT19937 pos out of range");
   np.load(np_key, np_pos);
   idx.resize(2 * (size_t)std::max(R, 1));
   int32_t* perm = idx.data();
@@ -562,9 +566,9 @@ class DrawQueue {
   int wait() {
     std::unique_lock<std::mutex> lk(mu_);
     cv_done_.wait(lk, [this] { return pending_ == 0; });
-    const bool f = failed_;
-    failed_ = false;
-    return f ? KP_ENOMEM : KP_OK;
+    const int rc = fail_rc_;
+    fail_rc_ = KP_OK;
+    return rc;
   }
 
  private:
@@ -599,14 +603,16 @@ class DrawQueue {
         t = std::move(q.front());
         q.pop_front();
       }
-      bool ok = true;
+      int rc = KP_OK;
       try {
         t(sc);
+      } catch (const std::invalid_argument&) {
+        rc = KP_EINVAL;
       } catch (...) {
-        ok = false;
+        rc = KP_ENOMEM;
       }
       std::lock_guard<std::mutex> lk(mu_);
-      if (!ok) failed_ = true;
+      if (rc != KP_OK && fail_rc_ == KP_OK) fail_rc_ = rc;
       if (--pending_ == 0) cv_done_.notify_all();
     }
   }
@@ -614,7 +620,7 @@ class DrawQueue {
   std::condition_variable cv_work_, cv_done_;
   std::deque<Task> seq_, fills_;
   int64_t pending_ = 0;
-  bool failed_ = false;
+  int fail_rc_ = KP_OK;  // first failure of a queued task since the last wait()
   pid_t pid_ = 0;
 };
 
@@ -682,7 +688,6 @@ int kp_rng_transe_enqueue(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* n
   if (!ts || tlen < 24 + kN * 8 || !np_key || !np_pos || R < 0 || epochs < 0 || ratio < 1 || n_entities < 1 ||
       n_entities >= (1LL << 32) || (R > 0 && epochs > 0 && !out))
     return KP_EINVAL;
-  if (*np_pos < 0 || *np_pos > kN) return KP_EINVAL;
   if (R == 0 || epochs == 0) return KP_OK;  // np.random.shuffle of an empty array draws nothing
   try {
     TorchMt mt;
@@ -690,6 +695,8 @@ int kp_rng_transe_enqueue(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* n
     const int rc = te_enqueue(mt, np_key, np_pos, R, epochs, ratio, (uint32_t)n_entities, out);
     if (rc != KP_OK) return rc;
     mt.store(ts);
+  } catch (const std::invalid_argument&) {
+    return KP_EINVAL;
   } catch (...) {
     return KP_ENOMEM;
   }
@@ -704,7 +711,6 @@ int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_
       (n > 0 && (!R_base || !R_pt || !x_base || !x_pt)) || epochs < 0 || ratio < 1 || n_entities < 1 ||
       n_entities >= (1LL << 32))
     return KP_EINVAL;
-  if (*np_pos < 0 || *np_pos > kN) return KP_EINVAL;
   int64_t words = 0;
   for (int32_t i = 0; i < n; ++i) {
     if (R_base[i] < -1 || R_pt[i] < -1) return KP_EINVAL;
@@ -732,6 +738,8 @@ int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_
       }
     }
     mt.store(ts);
+  } catch (const std::invalid_argument&) {
+    return KP_EINVAL;
   } catch (...) {
     return KP_ENOMEM;
   }

@@ -128,6 +128,13 @@ __global__ void kp_tr_rowgrads(const float* __restrict__ E, const float* __restr
     gt[(size_t)b * dp + i] = ta;
     gt[(size_t)b * dp + i + half] = tb;
   }
+  // the row padding [2 half, dp): kp_tr_scatter sums all dp columns into the table
+  // gradient, and the buffers are not cleared between calls
+  for (int i = 2 * half + threadIdx.x; i < dp; i += blockDim.x) {
+    gl[(size_t)b * dp + i] = 0.f;
+    gr[(size_t)b * dp + i] = 0.f;
+    gt[(size_t)b * dp + i] = 0.f;
+  }
 }
 
 // G[key] += the key's row gradients in batch order (items: 4 row + role; role 0 = lhs,
