@@ -258,11 +258,14 @@ int kp_rng_transe_enqueue(uint8_t* torch_state, size_t torch_len, uint32_t* np_k
  * -> x_pt[i], and its epoch draws if R_pt[i] >= 0 (R = -1: the call schedules no such
  * post-training).  The epoch draws (as kp_rng_transe_epochs, deferred as
  * kp_rng_transe_enqueue: complete after kp_rng_wait) go to `out` back to back in that
- * order.  d >= 16; x_base / x_pt are [n][d]. */
+ * order.  want (NULL = all): per call, bit 0 = the base post-training's draws are
+ * wanted, bit 1 = the post-trained one's; an unwanted post-training (one that another
+ * rank runs, kelpie_amd/distributed.py) only advances both generators and takes no
+ * space in `out`.  d >= 16; x_base / x_pt are [n][d]. */
 int kp_rng_transe_calls(uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos, int32_t cap,
                         int32_t D, int32_t d, float xavier_std, int32_t n, const int32_t* R_base,
-                        const int32_t* R_pt, int32_t epochs, int32_t ratio, int64_t n_entities, float* x_base,
-                        float* x_pt, int32_t* out);
+                        const int32_t* R_pt, const uint8_t* want, int32_t epochs, int32_t ratio,
+                        int64_t n_entities, float* x_base, float* x_pt, int32_t* out);
 
 /* Block until every slot queued by kp_rng_transe_enqueue is written. */
 int kp_rng_wait(void);

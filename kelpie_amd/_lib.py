@@ -89,8 +89,8 @@ def lib():
         L.kp_read_tables.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_rng_normal.argtypes = [C.c_void_p, C.c_size_t, C.c_int64, C.c_float, C.c_float, C.c_int32, C.c_void_p]
         L.kp_rng_transe_calls.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
-                                          C.c_int32, C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
-                                          C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+                                          C.c_int32, C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_rng_conve_masks.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_int32, C.c_double,
                                          C.c_void_p]
         L.kp_rng_conve_masks_enqueue.argtypes = L.kp_rng_conve_masks.argtypes
@@ -179,17 +179,20 @@ def rng_normal(state: np.ndarray, n: int, mean: float, std: float, cap: int | No
 
 def transe_calls(state: np.ndarray, np_key: int, np_pos: int, cap: int, D: int, d: int, std: float,
                  R_base: np.ndarray, R_pt: np.ndarray, epochs: int, ratio: int, n_entities: int,
-                 out: np.ndarray | None):
+                 out: np.ndarray | None, want: np.ndarray | None = None):
     """kp_rng_transe_calls for len(R_base) calls: returns (x_base [n][d], x_pt [n][d]); the
-    epoch draws land in ``out`` back to back (complete after :func:`rng_wait`)."""
+    epoch draws land in ``out`` back to back (complete after :func:`rng_wait`).  ``want``
+    (uint8 per call, bit 0 base / bit 1 pt; None = all): unwanted post-trainings only
+    advance the generators."""
     n = len(R_base)
     rb = np.ascontiguousarray(R_base, dtype=np.int32)
     rp = np.ascontiguousarray(R_pt, dtype=np.int32)
+    w = None if want is None else np.ascontiguousarray(want, dtype=np.uint8)
     xb = np.empty((n, d), np.float32)
     xp = np.empty((n, d), np.float32)
     check(lib().kp_rng_transe_calls(_ptr(state), state.size, C.c_void_p(np_key), C.c_void_p(np_pos), int(cap),
-                                    int(D), int(d), float(std), n, _ptr(rb), _ptr(rp), int(epochs), int(ratio),
-                                    int(n_entities), _ptr(xb), _ptr(xp), _ptr(out)))
+                                    int(D), int(d), float(std), n, _ptr(rb), _ptr(rp), _ptr(w), int(epochs),
+                                    int(ratio), int(n_entities), _ptr(xb), _ptr(xp), _ptr(out)))
     return xb, xp
 
 

@@ -511,7 +511,7 @@ void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, i
       np.pos += k;
     }
     for (int t = R - 1; t >= 1; --t) std::swap(perm[t], perm[jv[t]]);
-    std::memcpy(out + (size_t)e * 3 * R, perm, sizeof(int32_t) * R);
+    if (out) std::memcpy(out + (size_t)e * 3 * R, perm, sizeof(int32_t) * R);  // null: advance only
   }
   np.store(np_key, np_pos);
 }
@@ -558,8 +558,10 @@ class DrawQueue {
       seq_.push_back(std::move(seq));
       ++pending_;
     }
-    fills_.push_back(std::move(fill));
-    ++pending_;
+    if (fill) {
+      fills_.push_back(std::move(fill));
+      ++pending_;
+    }
     cv_work_.notify_all();
     return true;
   }
@@ -625,24 +627,28 @@ class DrawQueue {
 };
 
 // Queue one slot's TransE epoch draws (see the deferred protocol above) from the torch
-// generator `mt`, which is advanced past the slot's randints.
+// generator `mt`, which is advanced past the slot's randints.  out == nullptr: a slot
+// another rank post-trains -- only the generators advance (the numpy shuffles still run:
+// their consumption is data-dependent), nothing is written.
 int te_enqueue(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t ratio, uint32_t nent,
                int32_t* out) {
   if (R == 0 || epochs == 0) return KP_OK;  // np.random.shuffle of an empty array draws nothing
   const TorchMt snap = mt;
   mt.skip((uint64_t)epochs * 2u * (uint64_t)ratio * (uint64_t)R);
   Task seq = [=](Scratch& sc) { te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx); };
-  Task fill = [=](Scratch& sc) {
-    TorchMt m = snap;
-    te_randints(m, R, epochs, ratio, nent, out, sc.draw);
-  };
+  Task fill;
+  if (out)
+    fill = [=](Scratch& sc) {
+      TorchMt m = snap;
+      te_randints(m, R, epochs, ratio, nent, out, sc.draw);
+    };
   if (!DrawQueue::get().enqueue(seq, fill)) {
     // no worker threads: finish every queued task first (numpy order), then this one
     const int rc = DrawQueue::get().wait();
     if (rc != KP_OK) return rc;
     Scratch sc;
     seq(sc);
-    fill(sc);
+    if (fill) fill(sc);
   }
   return KP_OK;
 }
@@ -705,8 +711,8 @@ int kp_rng_transe_enqueue(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* n
 
 int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t cap, int32_t D,
                         int32_t d, float xavier_std, int32_t n, const int32_t* R_base, const int32_t* R_pt,
-                        int32_t epochs, int32_t ratio, int64_t n_entities, float* x_base, float* x_pt,
-                        int32_t* out) {
+                        const uint8_t* want, int32_t epochs, int32_t ratio, int64_t n_entities, float* x_base,
+                        float* x_pt, int32_t* out) {
   if (!ts || tlen < 24 + kN * 8 || !np_key || !np_pos || (cap != 0 && cap != 1) || D < 0 || d < 16 || n < 0 ||
       (n > 0 && (!R_base || !R_pt || !x_base || !x_pt)) || epochs < 0 || ratio < 1 || n_entities < 1 ||
       n_entities >= (1LL << 32))
@@ -714,7 +720,8 @@ int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_
   int64_t words = 0;
   for (int32_t i = 0; i < n; ++i) {
     if (R_base[i] < -1 || R_pt[i] < -1) return KP_EINVAL;
-    words += (int64_t)epochs * 3 * (std::max(R_base[i], 0) + std::max(R_pt[i], 0));
+    const int w = want ? want[i] : 3;
+    words += (int64_t)epochs * 3 * ((w & 1 ? std::max(R_base[i], 0) : 0) + (w & 2 ? std::max(R_pt[i], 0) : 0));
   }
   if (words > 0 && !out) return KP_EINVAL;
   try {
@@ -724,17 +731,18 @@ int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_
     int32_t* o = out;
     for (int32_t i = 0; i < n; ++i) {
       mt.skip((uint64_t)D);  // torch.rand(1, D): one output per element, values unused
+      const int w = want ? want[i] : 3;  // bit 0: base draws wanted here, bit 1: the pt draws
       normal_draw(mt, d, 0.0f, xavier_std, cap, x_base + (size_t)i * d);  // base KelpieTransE's xavier_normal_
       if (R_base[i] >= 0) {
-        const int rc = te_enqueue(mt, np_key, np_pos, R_base[i], epochs, ratio, nent, o);
+        const int rc = te_enqueue(mt, np_key, np_pos, R_base[i], epochs, ratio, nent, (w & 1) ? o : nullptr);
         if (rc != KP_OK) return rc;
-        o += (size_t)epochs * 3 * R_base[i];
+        if (w & 1) o += (size_t)epochs * 3 * R_base[i];
       }
       normal_draw(mt, d, 0.0f, xavier_std, cap, x_pt + (size_t)i * d);  // the post-trained one's
       if (R_pt[i] >= 0) {
-        const int rc = te_enqueue(mt, np_key, np_pos, R_pt[i], epochs, ratio, nent, o);
+        const int rc = te_enqueue(mt, np_key, np_pos, R_pt[i], epochs, ratio, nent, (w & 2) ? o : nullptr);
         if (rc != KP_OK) return rc;
-        o += (size_t)epochs * 3 * R_pt[i];
+        if (w & 2) o += (size_t)epochs * 3 * R_pt[i];
       }
     }
     mt.store(ts);

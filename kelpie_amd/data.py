@@ -306,29 +306,35 @@ class KelpieView:
                 dp[a] = dp.get(a, 0) + sign
         return d
 
-    def removed(self, triples):
-        """Rows and filter delta after ``remove_training_triples`` (kelpie_dataset.py:130-158)."""
+    def removed(self, triples, rows=True):
+        """Rows and filter delta after ``remove_training_triples`` (kelpie_dataset.py:130-158).
+        ``rows=False``: the row COUNT instead of the rows (same checks and errors), for
+        a slot another rank post-trains (kelpie_amd.distributed)."""
         for s, _, o in triples:
             assert self.original_entity == s or self.original_entity == o
         conv = [Dataset.replace_entity_in_triple(tuple(t), self.original_entity, self.kelpie_entity)
                 for t in triples]
         idx = [self.index[x] for x in conv]  # KeyError for a foreign triple, like the reference
-        keep = np.ones(len(self.base_triples), dtype=bool)
-        keep[idx] = False
-        kept = self.base_arr[keep]
         delta = self._delta(conv, -1)
         for rel, cnt in delta.items():
             cur = self.filter.get(rel, {})
             for e, n in cnt.items():
                 if cur.get(e, 0) + n < 0:
                     raise ValueError("list.remove(x): x not in list")
-        return self._rows(kept), delta
+        if not rows:
+            return 2 * (len(self.base_triples) - len(set(idx))), delta
+        keep = np.ones(len(self.base_triples), dtype=bool)
+        keep[idx] = False
+        return self._rows(self.base_arr[keep]), delta
 
-    def added(self, triples):
-        """Rows and filter delta after ``add_training_triples`` (kelpie_dataset.py:92-128)."""
+    def added(self, triples, rows=True):
+        """Rows and filter delta after ``add_training_triples`` (kelpie_dataset.py:92-128)
+        (``rows=False``: the row count, as :meth:`removed`)."""
         for s, _, o in triples:
             assert self.original_entity == s or self.original_entity == o
         conv = [Dataset.replace_entity_in_triple(tuple(t), self.original_entity, self.kelpie_entity)
                 for t in triples]
+        if not rows:
+            return 2 * (len(self.base_triples) + len(conv)), self._delta(conv, +1)
         rows = np.concatenate([self.base_arr, np.asarray(conv, dtype=np.int32).reshape(-1, 3)])
         return self._rows(rows), self._delta(conv, +1)

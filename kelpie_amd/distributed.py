@@ -9,14 +9,20 @@ draws, engine.py:125, stochastic_builder.py:161-165).  A rank that starts a late
 prediction from a fresh seed returns different results than the sequential run.
 
 ``SlotSharding`` keeps the results identical to the 1-rank (and reference) run: every
-rank schedules every engine batch -- the same host-side draws in the same order, so
-every generator stays in lockstep -- and post-trains only its share of the batch's
-slots on its GPU (longest-processing-time assignment by row count, the same on every
-rank); one all-gather of fixed-size (slot, score, rank) records per batch (RCCL over
-xGMI with the ``nccl`` backend, ``gloo`` on CPU) gives every rank every result, so
-the builder's accept / early-exit / ``random.random()`` replay runs identically on all
-ranks.  ``select_entities_to_convert`` shards its conversion test by entity range and
-all-gathers the keep mask.
+rank walks every engine batch's draws in the same order -- so every generator stays in
+lockstep -- but only the slots it *claims* are scheduled in full (kelpie init, edited
+rows, rank filter, draw values) and post-trained on its GPU; for the other slots it
+only advances the generators (the torch ones by one deferred discard per run of such
+slots, the numpy one by simulating the TransE shuffles, whose consumption is
+data-dependent).  Claims are made while scheduling, in slot order, by the same
+greedy rule on every rank: a slot goes to the rank with the least claimed row count so
+far (ties to the lowest rank).  One all-gather of fixed-size (slot, score, rank)
+records per batch (RCCL over xGMI with the ``nccl`` backend, ``gloo`` on CPU) gives
+every rank every result, so the builder's accept / early-exit / ``random.random()``
+replay runs identically on all ranks; each rank's record set carries a status row, so
+a rank whose device work failed makes every rank raise instead of leaving the others
+blocked in the gather.  ``select_entities_to_convert`` shards its conversion test by
+entity range and all-gathers the keep mask.
 """
 from __future__ import annotations
 
@@ -106,36 +112,41 @@ class SlotSharding:
         self.world = dist.get_world_size() if world is None and init else (world or 1)
         self.device = device
         self.gathers = 0
+        self.loads = [0] * self.world
 
-    def owners(self, costs):
-        """Owner rank of every slot: longest processing time first, ties to the lowest
-        index / rank, so every rank computes the same assignment."""
-        order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
-        loads = [0] * self.world
-        own = [0] * len(costs)
-        for i in order:
-            r = min(range(self.world), key=lambda k: (loads[k], k))
-            own[i] = r
-            loads[r] += costs[i]
-        return own
+    def begin_batch(self):
+        """Start claiming the slots of a new engine batch."""
+        self.loads = [0] * self.world
 
-    def mine(self, costs):
-        own = self.owners(costs)
-        return [i for i, r in enumerate(own) if r == self.rank]
+    def claim(self, cost) -> bool:
+        """Assign the next slot of the batch (in scheduling order) to the rank with the
+        least claimed cost so far, ties to the lowest rank; True if that is this rank.
+        Every rank makes the same calls in the same order, so all agree."""
+        r = min(range(self.world), key=lambda k: (self.loads[k], k))
+        self.loads[r] += int(cost)
+        return r == self.rank
 
-    def gather_slots(self, idx, score, rank, n):
-        """Every rank's (slot index, score, rank) records -> full [n] score / rank arrays."""
-        recs = np.zeros((len(idx), 3), np.float64)
+    def gather_slots(self, idx, score, rank, n, failed=False):
+        """Every rank's (slot index, score, rank) records -> full [n] score / rank arrays.
+        Each rank adds a status record (index -1, its failure flag); if any rank failed,
+        every rank raises after the gather."""
+        recs = np.zeros((len(idx) + 1, 3), np.float64)
         if len(idx):
-            recs[:, 0] = idx
-            recs[:, 1] = np.asarray(score, np.float64)
-            recs[:, 2] = np.asarray(rank, np.float64)
+            recs[:-1, 0] = idx
+            recs[:-1, 1] = np.asarray(score, np.float64)
+            recs[:-1, 2] = np.asarray(rank, np.float64)
+        recs[-1] = (-1.0, 1.0 if failed else 0.0, float(self.rank))
         allr = self._gather(recs, 3)
+        bad = [int(rk) for i, st, rk in allr if i < 0 and st != 0]
+        if bad:
+            raise RuntimeError(f"slot sharding: the device work of rank(s) {bad} failed")
         out_s = np.zeros(n, np.float32)
         out_r = np.zeros(n, np.int64)
         seen = np.zeros(n, np.int32)
         for i, sc, rk in allr:
             i = int(i)
+            if i < 0:
+                continue
             out_s[i], out_r[i] = sc, int(rk)
             seen[i] += 1
         if not np.all(seen == 1):

@@ -39,6 +39,9 @@ class _Slot:
     pred: tuple
     filt: list
     result: dict = field(default=None)
+    # False: another rank post-trains this slot (kelpie_amd.distributed); only the
+    # generators were advanced past its draws, and x0 / rows / rng / filt may be None
+    own: bool = True
 
 
 def _contiguous_draws(slots, total):
@@ -151,6 +154,15 @@ class PostTrainingEngine(RelevanceEngine):
         draws = self.model.posttrain_draws(rows, self.hp, self.rng)
         return _Slot(x0=x0, rows=rows, rng=draws, pred=tuple(int(v) for v in kelpie_pred), filt=list(filt))
 
+    def _sharded(self):
+        sh = self.sharding
+        return sh is not None and sh.world > 1
+
+    def _skip_slot(self, kp, rows=None, n_rows=0):
+        """A slot another rank post-trains: advance the generators past its draws only."""
+        self.model.posttrain_skip(rows, n_rows, self.hp, self.rng)
+        return _Slot(x0=None, rows=None, rng=None, pred=tuple(int(v) for v in kp), filt=None, own=False)
+
     def _schedule(self, pred, triples, mode, slots, pending_base):
         """Consume the draws of one reference compute_relevance call (post_training_engine.py:46-62)
         and append its slots.  Returns (pt_slot, base_key)."""
@@ -158,6 +170,8 @@ class PostTrainingEngine(RelevanceEngine):
         view = self._get_kelpie_dataset(pred[0])
         if getattr(self.model, "fused_call_draws", False):
             return self._schedule_fused(pred, view, triples, mode, slots, pending_base)
+        if self._sharded():
+            return self._schedule_sharded(pred, view, triples, mode, slots, pending_base)
         init = self.rng.rand_init(self.model.dimension)
         x_base = self.model.kelpie_init(init, self.rng)  # base KelpieModel is built every call (A-Q6)
         kp = view.as_kelpie_triple(pred)
@@ -170,6 +184,47 @@ class PostTrainingEngine(RelevanceEngine):
         slots.append(self._slot(x_pt, rows, kp, filt))
         return len(slots) - 1, pred
 
+    def _schedule_sharded(self, pred, view, triples, mode, slots, pending_base):
+        """_schedule when the batch is sharded over ranks (kelpie_amd.distributed): every
+        rank walks the same draws in the same order, but only the slots this rank claims
+        get their kelpie init, rows, filter and draw values; for the others the
+        generators are only advanced (one deferred torch discard for a run of them), so a
+        rank's host work is its share of the slots plus the generator walk."""
+        m, rng, sh = self.model, self.rng, self.sharding
+        kp = view.as_kelpie_triple(pred)
+        need_base = pred not in self.base_pt_results and pred not in pending_base
+        own_base = need_base and sh.claim(max(1, len(view.base_rows)))
+        edit = view.removed if mode == "necessary" else view.added
+        try:
+            n_pt, _ = edit(triples, rows=False)  # the reference raises after the draws below
+            err = None
+        except Exception as e:  # noqa: BLE001 -- re-raised at the reference's point
+            err, n_pt = e, 0
+        own_pt = err is None and sh.claim(max(1, n_pt))
+        if own_base or own_pt:
+            init = rng.rand_init(m.dimension)
+        else:
+            init = None
+            rng.skip_rand_init(m.dimension)
+        # the base KelpieModel is built every call (A-Q6), then (uncached) post-trained
+        x_base = m.kelpie_init(init, rng) if own_base else m.kelpie_skip(rng)
+        if need_base:
+            pending_base[pred] = len(slots)
+            if own_base:
+                slots.append(self._slot(x_base, view.base_rows, kp, view.filter_for(kp[1])))
+            else:
+                slots.append(self._skip_slot(kp, view.base_rows, len(view.base_rows)))
+        x_pt = m.kelpie_init(init, rng) if own_pt else m.kelpie_skip(rng)
+        if err is not None:
+            raise err
+        if own_pt or m.skip_needs_rows:
+            rows, delta = edit(triples)
+        if own_pt:
+            slots.append(self._slot(x_pt, rows, kp, view.filter_for(kp[1], delta.get(kp[1]))))
+        else:
+            slots.append(self._skip_slot(kp, rows if m.skip_needs_rows else None, n_pt))
+        return len(slots) - 1, pred
+
     def _schedule_fused(self, pred, view, triples, mode, slots, pending_base):
         """_schedule for TransE: the call's slots are appended now and its draws are
         queued; :meth:`_flush_fused` makes every queued call's draws in one library call
@@ -178,22 +233,34 @@ class PostTrainingEngine(RelevanceEngine):
         the post-trained model's epochs) are consumed, then the error propagates."""
         kp = view.as_kelpie_triple(pred)
         need_base = pred not in self.base_pt_results and pred not in pending_base
+        sharded = self._sharded()
+        own_base = need_base and (not sharded or self.sharding.claim(max(1, len(view.base_rows))))
+        edit = view.removed if mode == "necessary" else view.added
         err = None
         try:
-            rows, delta = view.removed(triples) if mode == "necessary" else view.added(triples)
+            if sharded:
+                # another rank's slot needs only the row count (kelpie_amd.distributed)
+                n_pt, delta = edit(triples, rows=False)
+                own_pt = self.sharding.claim(max(1, n_pt))
+                rows = edit(triples)[0] if own_pt else None
+            else:
+                rows, delta = edit(triples)
+                n_pt, own_pt = len(rows), True
         except Exception as e:  # noqa: BLE001 -- re-raised below, after the reference's draws
-            err, rows = e, None
-        call = {"R_base": len(view.base_rows) if need_base else -1, "R_pt": -1 if err else len(rows),
-                "base": None, "pt": None}
+            err, rows, own_pt = e, None, False
+        call = {"R_base": len(view.base_rows) if need_base else -1, "R_pt": -1 if err else n_pt,
+                "want": (1 if own_base else 0) | (2 if own_pt else 0), "base": None, "pt": None}
         if need_base:
             pending_base[pred] = len(slots)
-            call["base"] = _Slot(x0=None, rows=view.base_rows, rng=None, pred=kp, filt=list(view.filter_for(kp[1])))
+            call["base"] = _Slot(x0=None, rows=view.base_rows, rng=None, pred=kp,
+                                 filt=list(view.filter_for(kp[1])) if own_base else None, own=own_base)
             slots.append(call["base"])
         self._fused.append(call)
         if err is not None:
             self._flush_fused()
             raise err
-        call["pt"] = _Slot(x0=None, rows=rows, rng=None, pred=kp, filt=list(view.filter_for(kp[1], delta.get(kp[1]))))
+        call["pt"] = _Slot(x0=None, rows=rows, rng=None, pred=kp,
+                           filt=list(view.filter_for(kp[1], delta.get(kp[1]))) if own_pt else None, own=own_pt)
         slots.append(call["pt"])
         if len(self._fused) >= self._FUSED_FLUSH:
             # hand the draws to the library's workers early: their numpy shuffles then run
@@ -208,9 +275,11 @@ class PostTrainingEngine(RelevanceEngine):
         if not calls:
             return
         m, hp = self.model, self.hp
+        want = [c["want"] for c in calls] if self._sharded() else None
         xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, [c["R_base"] for c in calls],
                                               [c["R_pt"] for c in calls], int(hp["epochs"]),
-                                              int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1)
+                                              int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1,
+                                              want=want)
         for i, c in enumerate(calls):
             db, dp = draws[i]
             if c["base"] is not None:
@@ -220,6 +289,8 @@ class PostTrainingEngine(RelevanceEngine):
 
     def _schedule_all(self, items, checkpoints):
         """_schedule_multi, with every queued TransE call's draws made before it returns or raises."""
+        if self._sharded():
+            self.sharding.begin_batch()
         try:
             return self._schedule_multi(items, checkpoints)
         finally:
@@ -230,16 +301,19 @@ class PostTrainingEngine(RelevanceEngine):
         rank's share runs; ``_collect`` then gathers every rank's results."""
         if not slots:
             return {}
-        sh = self.sharding
-        if sh is not None and sh.world > 1:
-            mine = sh.mine([max(1, len(s.rows)) for s in slots])
-            if not mine:
-                stats = {"slots": 0, "rows": 0, "pack_s": 0.0, "lib_s": 0.0, "_local": (mine, [], [], len(slots))}
-                self.last_batch_stats = stats
-                return stats
-            sub = [slots[i] for i in mine]
-            stats = self._run_slots(sub, ctx, fill=False)
-            stats["_local"] = (mine, stats.pop("_score"), stats.pop("_rank"), len(slots))
+        if self._sharded():
+            # the slots this rank claimed while scheduling; a failure is reported to the
+            # other ranks through the gather (_collect) instead of leaving them waiting in it
+            mine = [i for i, s in enumerate(slots) if s.own]
+            stats = {"slots": 0, "rows": 0, "pack_s": 0.0, "lib_s": 0.0}
+            score, rank, err = [], [], None
+            if mine:
+                try:
+                    stats = self._run_slots([slots[i] for i in mine], ctx, fill=False)
+                    score, rank = stats.pop("_score"), stats.pop("_rank")
+                except Exception as e:  # noqa: BLE001 -- raised on every rank by _collect
+                    err, mine = e, []
+            stats["_local"] = (mine, score, rank, len(slots), err)
             self.last_batch_stats = stats
             return stats
         return self._run_slots(slots, ctx, fill=True)
@@ -249,9 +323,14 @@ class PostTrainingEngine(RelevanceEngine):
         local = stats.pop("_local", None) if stats else None
         if local is None:
             return
-        mine, score, rank, n = local
+        mine, score, rank, n, err = local
         t0 = time.perf_counter()
-        all_s, all_r = self.sharding.gather_slots(mine, score, rank, n)
+        try:
+            all_s, all_r = self.sharding.gather_slots(mine, score, rank, n, failed=err is not None)
+        except Exception:
+            if err is not None:
+                raise err
+            raise
         for i, s in enumerate(slots):
             s.result = {"target_score": float(all_s[i]), "target_rank": int(all_r[i])}
         stats["gather_s"] = time.perf_counter() - t0

@@ -99,6 +99,18 @@ class FrozenModel:
         """Random draws of one post-training over ``rows`` (kelpie rows + inverses)."""
         raise NotImplementedError
 
+    # Slots another rank post-trains (kelpie_amd.distributed): consume the same draws
+    # without producing what only the post-training needs.  The defaults make the draws
+    # and drop them; models override with a bare generator advance where they can.
+    skip_needs_rows = True  # posttrain_skip needs the edited rows, not only their count
+
+    def kelpie_skip(self, rng: ReferenceRNG):
+        """The draws of a KelpieModel construction (kelpie_init) whose row is not needed."""
+        self.kelpie_init(np.zeros(self.dimension, np.float32), rng)
+
+    def posttrain_skip(self, rows, n_rows: int, hp: dict, rng: ReferenceRNG):
+        self.posttrain_draws(rows, hp, rng)
+
 
 class ComplEx(FrozenModel):
     """ComplEx (complex.py:17-142): rows [Re | Im], maximizer."""
@@ -127,6 +139,14 @@ class ComplEx(FrozenModel):
 
     def posttrain_draws(self, rows, hp, rng):
         return rng.complex_epochs(len(rows), int(hp["epochs"]), int(hp["batch_size"]))
+
+    skip_needs_rows = False
+
+    def kelpie_skip(self, rng):
+        pass  # KelpieComplEx draws nothing at construction
+
+    def posttrain_skip(self, rows, n_rows, hp, rng):
+        rng.complex_epochs(int(n_rows), int(hp["epochs"]), int(hp["batch_size"]), want=False)
 
 
 class TransE(FrozenModel):
@@ -222,6 +242,14 @@ class ConvE(FrozenModel):
     def posttrain_draws(self, rows, hp, rng):
         steps = self.er_vocab_sizes(rows, int(hp["batch_size"]), int(hp["epochs"]))
         return rng.conve_masks(steps, self.dimension, self.hidden_dropout_rate)
+
+    def kelpie_skip(self, rng):
+        rng.conve_construction(self.hidden_layer_size, self.dimension)
+
+    def posttrain_skip(self, rows, n_rows, hp, rng):
+        if self.hidden_dropout_rate > 0.0:
+            steps = self.er_vocab_sizes(rows, int(hp["batch_size"]), int(hp["epochs"]))
+            rng.discard(2 * self.dimension * int(sum(steps)))  # bernoulli_: one random64 per element
 
 
 MODEL_REGISTRY = {"ComplEx": ComplEx, "TransE": TransE, "ConvE": ConvE}

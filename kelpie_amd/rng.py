@@ -62,13 +62,30 @@ _outstanding = False
 _inflight = []
 
 
+# torch-generator outputs owed by draws whose values nobody needs (the slots another
+# rank post-trains, kelpie_amd.distributed): accumulated and applied as ONE discard
+# before the next real torch draw or state read
+_skip = 0
+
+
+def _flush_skip():
+    global _skip
+    if _skip:
+        n, _skip = _skip, 0
+        st = _get_state()
+        _lib.mt19937_discard(st, n)
+        _set_state(st)
+
+
 def sync():
-    """Wait for every queued TransE draw (the numpy global state is then current)."""
+    """Wait for every queued TransE draw (the numpy global state is then current) and
+    apply any pending torch-generator advance."""
     global _outstanding
     if _outstanding:
         _outstanding = False
         _lib.rng_wait()
     _inflight.clear()
+    _flush_skip()
 
 
 class ReferenceRNG:
@@ -109,27 +126,36 @@ class ReferenceRNG:
 
     # ---------------------------------------------------------------- model construction
     def rand_init(self, D: int) -> np.ndarray:
+        _flush_skip()
         return torch.rand(1, D).numpy()[0]  # float32 already
+
+    def skip_rand_init(self, D: int):
+        """Consume torch.rand(1, D) without its values (one output per float32 element)."""
+        self.discard(D)
 
     def xavier_row(self, d: int) -> np.ndarray:
         # xavier_normal_ on a (1, d) parameter: normal_(0, sqrt(2 / (d + 1)))
+        _flush_skip()
         return torch.empty(1, d).normal_(0.0, math.sqrt(2.0 / float(d + 1))).numpy()[0]  # float32 already
 
     def discard(self, n: int):
-        if n <= 0:
-            return
-        st = _get_state()
-        _lib.mt19937_discard(st, n)
-        _set_state(st)
+        """Advance the torch generator by n outputs (deferred to the next real draw)."""
+        global _skip
+        if n > 0:
+            _skip += int(n)
+        if not self._defer_depth:
+            _flush_skip()  # outside a deferred block nobody else flushes it
 
     def conve_construction(self, hidden: int, dim: int):
         self.discard(32 * 9 + 32 + hidden * dim + dim)
 
     # ---------------------------------------------------------------- per-optimizer draws
-    def complex_epochs(self, R: int, epochs: int, batch_size: int) -> np.ndarray:
-        """Per-epoch ``torch.randperm(R)``; values are only needed when an epoch
-        has more than one minibatch."""
-        if R > batch_size:
+    def complex_epochs(self, R: int, epochs: int, batch_size: int, want: bool = True) -> np.ndarray:
+        """Per-epoch ``torch.randperm(R)`` (R - 1 outputs each); values are only needed
+        when an epoch has more than one minibatch (and ``want``: the slot is post-trained
+        here)."""
+        if R > batch_size and want:
+            _flush_skip()
             return np.concatenate([torch.randperm(R).numpy().astype(np.int32) for _ in range(epochs)]) \
                 if epochs else np.zeros(0, np.int32)
         self.discard(epochs * max(R - 1, 0))
@@ -144,6 +170,7 @@ class ReferenceRNG:
         if epochs <= 0:
             return np.zeros(0, np.int32)
         global _outstanding
+        _flush_skip()
         st = _get_state()
         # numpy's global MT19937 is advanced in place through its C state struct
         # (BitGenerator.ctypes.state_address -> {uint32 key[624]; int pos}):
@@ -159,24 +186,29 @@ class ReferenceRNG:
         _set_state(st)
         return out
 
-    def transe_calls(self, D: int, d: int, R_base, R_pt, epochs: int, ratio: int, n_entities: int):
+    def transe_calls(self, D: int, d: int, R_base, R_pt, epochs: int, ratio: int, n_entities: int, want=None):
         """Every draw of n TransE compute_relevance calls in one library call
         (kp_rng_transe_calls).  Per call: ``torch.rand(1, D)``, the base row's
         ``xavier_normal_``, the base post-training's epoch draws (``R_base[i]`` >= 0),
         the post-trained row's ``xavier_normal_`` and its epoch draws (``R_pt[i]`` >= 0).
         Returns ``(x_base [n][d], x_pt [n][d], [(draws_base, draws_pt)] * n)``; the draws
-        are complete on leaving :meth:`deferred` (or at once outside it)."""
+        are complete on leaving :meth:`deferred` (or at once outside it).  ``want[i]``
+        (bit 0 base, bit 1 pt; default all): an unwanted post-training's draws are not
+        made, only the generators advance past them (its entry is an empty array)."""
         global _outstanding
+        _flush_skip()
         st = _get_state()
         addr = _np_mt_state_address()
         if not self._defer_depth:
             sync()
-        sizes = [(epochs * 3 * max(rb, 0), epochs * 3 * max(rp, 0)) for rb, rp in zip(R_base, R_pt)]
+        w = [3] * len(R_base) if want is None else list(want)
+        sizes = [(epochs * 3 * max(rb, 0) if wi & 1 else 0, epochs * 3 * max(rp, 0) if wi & 2 else 0)
+                 for rb, rp, wi in zip(R_base, R_pt, w)]
         total = sum(a + b for a, b in sizes)
         out = (self._take(total) if self._defer_depth else np.empty(total, np.int32)) if total else None
         xb, xp = _lib.transe_calls(st, addr, addr + 4 * 624, _lib.normal_cap(), D, d,
                                    float(np.float32(math.sqrt(2.0 / float(d + 1)))), R_base, R_pt, epochs, ratio,
-                                   n_entities, out)
+                                   n_entities, out, None if want is None else np.array(w, np.uint8))
         _outstanding = True
         if not self._defer_depth:
             sync()
@@ -192,6 +224,7 @@ class ReferenceRNG:
         if p_drop <= 0.0 or len(n_rows_per_step) == 0:
             return np.zeros(0, np.int32)
         global _outstanding
+        _flush_skip()
         st = _get_state()
         if self._defer_depth:
             words = _lib.conve_masks_enqueue(st, n_rows_per_step, dim, 1.0 - p_drop,

@@ -113,12 +113,26 @@ int main(int argc, char** argv) {
   for (int i = 0; i < n_calls; ++i) tot += (size_t)4 * 3 * ((rb[i] > 0 ? rb[i] : 0) + (rp[i] > 0 ? rp[i] : 0));
   std::vector<int32_t> calls(tot + 1);
   std::vector<float> xb((size_t)n_calls * 32), xp((size_t)n_calls * 32);
-  ok(kp_rng_transe_calls(ts.data(), ts.size(), key.data(), &pos, 1, 32, 32, 0.2425f, n_calls, rb.data(), rp.data(), 4,
-                         5, 14542, xb.data(), xp.data(), calls.data()),
+  ok(kp_rng_transe_calls(ts.data(), ts.size(), key.data(), &pos, 1, 32, 32, 0.2425f, n_calls, rb.data(), rp.data(),
+                         nullptr, 4, 5, 14542, xb.data(), xp.data(), calls.data()),
      "transe_calls");
   ok(kp_rng_wait(), "wait");
   calls.resize(tot);
   put(calls);
+  put(xb);
+  put(xp);
+  // the same shape with some post-trainings unwanted (another rank's): advance only
+  std::vector<uint8_t> want = {1, 2, 0, 3, 0, 2};
+  size_t tot2 = 0;
+  for (int i = 0; i < n_calls; ++i)
+    tot2 += (size_t)4 * 3 * ((want[i] & 1 && rb[i] > 0 ? rb[i] : 0) + (want[i] & 2 && rp[i] > 0 ? rp[i] : 0));
+  std::vector<int32_t> calls2(tot2 + 1);
+  ok(kp_rng_transe_calls(ts.data(), ts.size(), key.data(), &pos, 1, 32, 32, 0.2425f, n_calls, rb.data(), rp.data(),
+                         want.data(), 4, 5, 14542, xb.data(), xp.data(), calls2.data()),
+     "transe_calls(want)");
+  ok(kp_rng_wait(), "wait");
+  calls2.resize(tot2);
+  put(calls2);
   put(xb);
   put(xp);
   std::vector<uint32_t> masks(mask_words);
@@ -133,10 +147,7 @@ int main(int argc, char** argv) {
   const int64_t n_tri = (int64_t)(tri.size() / 12);
   std::vector<int32_t> t3(n_tri * 3);
   std::memcpy(t3.data(), tri.data(), tri.size());
-  int32_t n_ent = 0;
-  for (int32_t v : t3) n_ent = v + 1 > n_ent ? v + 1 : n_ent;
-  // relation ids share the array: entities are columns 0 and 2 only
-  n_ent = 0;
+  int32_t n_ent = 0;  // entities are columns 0 and 2 (column 1 holds relation ids)
   for (int64_t i = 0; i < n_tri; ++i) {
     n_ent = t3[3 * i] + 1 > n_ent ? t3[3 * i] + 1 : n_ent;
     n_ent = t3[3 * i + 2] + 1 > n_ent ? t3[3 * i + 2] + 1 : n_ent;

@@ -102,6 +102,13 @@ def _engine_run(name, sharding, backend="cpu"):
             res = explain_preds(pipe, ds, preds, prefilter_k=len(b["candidates"]))
         out["builder"] = [(r["rule_to_relevance"], r["#relevances"]) for r in res]
     out["gathers"] = sharding.gathers if sharding is not None else 0
+    if sharding is not None:
+        # the last batch: this rank scheduled in full only the slots it claimed
+        eng.set_cache()
+        with eng.rng.deferred():
+            slots, _, _ = eng._schedule_all(items[:1], None)
+        own = [s for s in slots if s.own]
+        assert 0 < len(own) < len(slots) and all(s.filt is None and (s.rng is None or s.rng.size == 0) for s in slots if not s.own)
     return out
 
 
@@ -184,3 +191,55 @@ def test_engine_sharding_world2_gpu():
             got, exp = dict(res[name]), dict(single[name])
             got.pop("gathers"), exp.pop("gathers")
             assert got == exp, (rank, name)
+
+
+def _failing_worker(rank, world, port, q):
+    """Rank 1's device work fails in the second batch: both ranks must raise (rank 1 its
+    own error, rank 0 the gathered failure) instead of rank 0 waiting in the gather."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from engine_cases import build_product
+    from golden_io import seed_all
+    import kelpie_amd as ka
+    from kelpie_amd import distributed as kd
+    from kelpie_amd._lib import KelpieHipError
+    kd.init_from_env(backend="gloo")
+    try:
+        rec, ds, model = build_product("complex_tiny", "cpu")
+        seed_all(rec["seed"])
+        eng = ka.NecessaryPostTrainingEngine(model, ds, rec["hp"])
+        eng.sharding = kd.SlotSharding(device="cpu")
+        block = rec["necessary"][0]
+        rules = [[tuple(t) for t in c["rule"]] for c in block["calls"]]
+        eng.compute_relevance_batch(tuple(block["pred"]), rules)
+        if rank == 1:
+            def boom(*a, **k):
+                raise KelpieHipError("injected device failure")
+            model.ctx.posttrain_rank = boom
+        eng.set_cache()
+        try:
+            eng.compute_relevance_batch(tuple(block["pred"]), rules)
+            q.put((rank, "no error"))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, type(e).__name__ + ": " + str(e)))
+    finally:
+        import torch.distributed as dist
+        dist.barrier()  # both ranks have read the gather before the connection closes
+        dist.destroy_process_group()
+
+
+def test_engine_sharding_failure_raises_on_every_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert out[1].startswith("KelpieHipError: injected device failure"), out
+    assert out[0].startswith("RuntimeError: slot sharding: the device work of rank(s) [1] failed"), out

@@ -78,6 +78,12 @@ def _expected(ts, key, pos, tri, n_ent, off, cls):
     xb, xp = _lib.transe_calls(st, ka, pa, 1, 32, 32, float(np.float32(0.2425)), rb, rp, 4, 5, 14542, calls)
     _lib.rng_wait()
     out += [calls[:tot].tobytes(), xb.tobytes(), xp.tobytes()]
+    want = np.array([1, 2, 0, 3, 0, 2], np.uint8)
+    tot2 = int(sum(4 * 3 * ((max(a, 0) if w & 1 else 0) + (max(b, 0) if w & 2 else 0)) for a, b, w in zip(rb, rp, want)))
+    calls2 = np.zeros(tot2 + 1, np.int32)
+    xb, xp = _lib.transe_calls(st, ka, pa, 1, 32, 32, float(np.float32(0.2425)), rb, rp, 4, 5, 14542, calls2, want)
+    _lib.rng_wait()
+    out += [calls2[:tot2].tobytes(), xb.tobytes(), xp.tobytes()]
     out.append(_lib.conve_masks(st, rows, 200, 0.8).tobytes())
     out += [st.tobytes(), key.tobytes(), posa.tobytes()]
     g = _lib.Graph(n_ent, tri)

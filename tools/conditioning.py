@@ -161,9 +161,13 @@ def main():
     ap.add_argument("--variants", nargs="+", default=["fp32", "fp32_perm", "fp64"])
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--fixture-only", action="store_true", help="rewrite the fixture from the profiles record")
+    ap.add_argument("--pred-index", type=int, default=None,
+                    help="a further sample: prediction k of bench.pick_preds (fixture <workload>__p<k>.json)")
+    ap.add_argument("--candidates", type=int, default=3, help="candidates of that prediction (with --pred-index)")
     args = ap.parse_args()
+    name = args.workload if args.pred_index is None else f"{args.workload}__p{args.pred_index}"
     if args.fixture_only:
-        with open(os.path.join(ROOT, "profiles", f"conditioning_{args.workload}.json")) as f:
+        with open(os.path.join(ROOT, "profiles", f"conditioning_{name}.json")) as f:
             write_fixture(json.load(f))
         return
     torch.set_num_threads(args.threads)
@@ -172,7 +176,29 @@ def main():
     nf_path = os.path.join(ROOT, "profiles", f"noise_floor_{args.workload}.json")
     g = synth.make_graph(wl["shape"], seed=0)
     w0 = synth.make_weights(wl["model"], g.num_entities, g.num_relations, wl["dim"], seed=0)
-    if os.path.exists(nf_path):
+    if args.pred_index is not None:
+        # a further sample of the bench's own predictions: pick_preds' k-th prediction and
+        # its first candidates (bench.candidates_of), conversion entities as the reference
+        # selects them (engine.py:22-126, seeds 42)
+        from kelpie_amd import Dataset
+        ds = Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test, name=wl["shape"])
+        pk = bench.pick_preds(ds, args.pred_index + 1, seed=1234)[args.pred_index]
+        nf = {"pred": list(pk), "candidates": [list(c) for c in bench.candidates_of(ds, pk, wl["candidates"])
+                                                [:args.candidates]], "entities_to_convert": None, "runs": {}}
+        if wl["mode"] == "sufficient":
+            from src.relevance_engines import SufficientPostTrainingEngine
+            dataset, model = noise_floor.reference_model(src, wl, g, w0)
+            # the synthetic DB100K shape has entities with no training triple, which the
+            # reference's degree lookup (engine.py:73, a plain dict) raises on; real datasets
+            # index every entity from the training file.  Degree 0 there means "skip", as the
+            # engine's own `< 1` test does (kelpie_amd/engine.py uses .get(e, 0)).
+            import collections
+            dataset.entity_to_degree = collections.defaultdict(int, dataset.entity_to_degree)
+            ref_harness.seed_all(42)
+            se = SufficientPostTrainingEngine(model, dataset, wl["hp"])
+            se.select_entities_to_convert(tuple(pk), wl["convert"], 200)
+            nf["entities_to_convert"] = [int(e) for e in se.entities_to_convert]
+    elif os.path.exists(nf_path):
         with open(nf_path) as f:
             nf = json.load(f)  # the sample (pred, candidates, conversion entities) and its GPU run
     else:
@@ -193,8 +219,8 @@ def main():
     cands = [tuple(c) for c in nf["candidates"]]
     ents = nf.get("entities_to_convert")
     D = wl["dim"] * (2 if wl["model"] == "ComplEx" else 1)
-    out_path = os.path.join(ROOT, "profiles", f"conditioning_{args.workload}.json")
-    out = {"workload": args.workload, "pred": list(pred), "candidates": [list(c) for c in cands],
+    out_path = os.path.join(ROOT, "profiles", f"conditioning_{name}.json")
+    out = {"workload": args.workload, "name": name, "pred": list(pred), "candidates": [list(c) for c in cands],
            "entities_to_convert": ents, "threads": args.threads, "runs": {}}
     if os.path.exists(out_path):
         with open(out_path) as f:
@@ -245,7 +271,7 @@ def write_fixture(rec):
                             "seconds": run.get("seconds"), "cand_seconds": run.get("cand_seconds")}
     d = os.path.join(ROOT, "tests", "golden", "fullsize")
     os.makedirs(d, exist_ok=True)
-    with open(os.path.join(d, rec["workload"] + ".json"), "w") as f:
+    with open(os.path.join(d, rec.get("name", rec["workload"]) + ".json"), "w") as f:
         json.dump(fx, f, indent=1)
 
 
