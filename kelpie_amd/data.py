@@ -335,6 +335,6 @@ class KelpieView:
         conv = [Dataset.replace_entity_in_triple(tuple(t), self.original_entity, self.kelpie_entity)
                 for t in triples]
         if not rows:
-            return 2 * (len(self.base_triples) + len(conv)), self._delta(conv, +1)
+            return 2 * (len(self.base_triples) + len(conv)), None  # additions cannot fail
         rows = np.concatenate([self.base_arr, np.asarray(conv, dtype=np.int32).reshape(-1, 3)])
         return self._rows(rows), self._delta(conv, +1)

@@ -122,8 +122,9 @@ class SlotSharding:
         """Assign the next slot of the batch (in scheduling order) to the rank with the
         least claimed cost so far, ties to the lowest rank; True if that is this rank.
         Every rank makes the same calls in the same order, so all agree."""
-        r = min(range(self.world), key=lambda k: (self.loads[k], k))
-        self.loads[r] += int(cost)
+        loads = self.loads
+        r = loads.index(min(loads))  # the first (lowest) rank among the least loaded
+        loads[r] += int(cost)
         return r == self.rank
 
     def gather_slots(self, idx, score, rank, n, failed=False):

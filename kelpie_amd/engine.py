@@ -240,9 +240,9 @@ class PostTrainingEngine(RelevanceEngine):
         try:
             if sharded:
                 # another rank's slot needs only the row count (kelpie_amd.distributed)
-                n_pt, delta = edit(triples, rows=False)
+                n_pt, _ = edit(triples, rows=False)
                 own_pt = self.sharding.claim(max(1, n_pt))
-                rows = edit(triples)[0] if own_pt else None
+                rows, delta = edit(triples) if own_pt else (None, None)
             else:
                 rows, delta = edit(triples)
                 n_pt, own_pt = len(rows), True
