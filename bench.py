@@ -19,12 +19,12 @@ reference's random init, the ComplEx DBpedia50 explanation hp (Adagrad 0.043,
 (pipeline.py:36-39, degree cap 200).
 
 For N > 1 the driver launches one rank per GPU with torchrun.  A step then holds
-N times the predictions (weak scaling: the per-GPU work is fixed); every rank
-schedules every batch -- the reference's one global random stream, drawn in the same
-order on every rank -- and post-trains its share of the batch's slots, with one
-all-gather of the (slot, score, rank) records per batch
-(kelpie_amd.distributed.SlotSharding), so the results equal the 1-rank run.  Rank 0
-prints ONE JSON line.
+N times the predictions (weak scaling: the per-GPU work is fixed); every rank walks
+every batch's draws -- the reference's one global random stream, in the same order on
+every rank -- but schedules in full and post-trains only the slots it claims (for the
+others it only advances the generators), with one all-gather of the (slot, score,
+rank) records per batch (kelpie_amd.distributed.SlotSharding), so the results equal
+the 1-rank run.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -54,7 +54,16 @@ CONVE_HP = {"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.
 WORKLOADS = {
     # BASELINE.json configs[2]: the north-star target (>= 50x, ComplEx on FB15k-237)
     "complex-fb15k237-sufficient": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="sufficient",
-                                        hp=COMPLEX_HP, candidates=20, convert=10, preds_per_step=1, depth=3),
+                                        hp=COMPLEX_HP, candidates=20, convert=10, preds_per_step=1, depth=3,
+                                        cpu_conversions=2),
+    # the same with "many conversion entities" (K = 10 / 50 / 100; engine.py:125
+    # samples min(K, convertible) of them)
+    "complex-fb15k237-sufficient-k50": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="sufficient",
+                                            hp=COMPLEX_HP, candidates=20, convert=50, preds_per_step=1, depth=3,
+                                            cpu_conversions=2),
+    "complex-fb15k237-sufficient-k100": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="sufficient",
+                                             hp=COMPLEX_HP, candidates=20, convert=100, preds_per_step=1, depth=3,
+                                             cpu_conversions=2),
     "complex-fb15k237-necessary": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="necessary",
                                        hp=COMPLEX_HP, candidates=20, preds_per_step=16),
     # BASELINE.json configs[1]
@@ -230,6 +239,9 @@ def cpu_baseline(wl, ds, weights, pred, cands, ents=None, fixture=None):
     steady = times[1:]
     out = {"value": (frac * len(steady) / sum(steady)) if steady else None, "unit": "candidates/s",
            "cores": int(threads), "kind": "port", **_cores(),
+           # the box gives one GPU's job a fixed CPU share (OMP_NUM_THREADS / MAX_JOBS are set
+           # to it and are not to be raised): the oracle's BLAS runs on all of that share
+           "cpu_share_of_this_gpu": int(os.environ.get("OMP_NUM_THREADS", threads)),
            "first_candidate_s": times[0] / frac, "steady_candidates": len(steady),
            "steady_s_per_candidate": (sum(steady) / len(steady) / frac) if steady else None,
            "sample": f"1 prediction of the workload: its first candidate (with the prediction's base post-training) "
@@ -436,7 +448,7 @@ def main():
         pred, cands_s, ents, parity = parity_sample(eng, wl, fixture, (pred, cands, ents))
         log(f"[rank 0] parity sample vs reference: {json.dumps(parity)}")
         if not args.no_cpu_baseline:
-            n_cpu = 3 if wl["mode"] == "sufficient" else 5
+            n_cpu = 5  # the first candidate (with the prediction's base post-trainings) + 4 steady
             cpu_cands = (cands_s + [c for c in candidates_of(ds, pred, wl["candidates"]) if c not in cands_s])[:n_cpu]
             try:
                 cpu = cpu_baseline(wl, ds, weights, pred, cpu_cands, ents, fixture)
@@ -456,12 +468,17 @@ def main():
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
                 "config": {"workload": args.workload, "model": wl["model"], "graph": wl["shape"] + " (synthetic)",
-                           "dim": wl["dim"], "mode": wl["mode"], "candidates_per_step": wl["candidates"] * per_step,
+                           "dim": wl["dim"], "mode": wl["mode"],
+                           # units actually evaluated per timed step (a prediction has at most
+                           # `candidates` singleton candidates; low-degree subjects have fewer)
+                           "candidates_per_step": total_units / max(args.steps, 1),
+                           "candidates_cap_per_prediction": wl["candidates"],
                            "predictions_per_step": per_step,
                            "conversion_entities": wl.get("convert"), "epochs": wl["hp"]["epochs"],
                            "batches_in_flight": depth,
                            "parallelism": f"each batch's post-trainings sharded over {world} rank(s), "
-                                          f"host schedule replicated, one all-gather per batch"},
+                                          f"each rank schedules only its claimed slots (generators walked for "
+                                          f"the rest), one all-gather per batch"},
                 "rank_delta_match_rate": (parity.get("fp32") or {}).get("match_rate"),
                 "rank_delta_max_abs_diff": (parity.get("fp32") or {}).get("max_abs_diff"),
                 "rank_delta_vs": "the reference (fp32, CPU) on the fixture tests/golden/fullsize/<workload>.json",

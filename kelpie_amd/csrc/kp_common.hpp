@@ -101,6 +101,8 @@ struct kp_ctx {
   bool e3_ready = false;
   DevBuf e3ts, e3pre;      // kp_attn3's fp64 tile sums / prefix sums of dE over tiles
   bool e3pre_ready = false;
+  DevBuf eT;               // dE transposed [dp][round_up(n_ent, 256)] fp32 (fp64 rank scoring), on first use
+  bool eT_ready = false;
   DevBuf fc3, fct3;        // ConvE: three-piece bf16 images of the FC weight and its transpose (kp_gemm3.hip)
   bool fc3_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
@@ -198,6 +200,14 @@ void split3_rows(kp_ctx* c, const float* X, int rows, int cols, int ld, uint16_t
 // ConvE: the FC weight's [dim][hidden] and its transpose's [hidden][dim] split images (built once)
 const uint16_t* conve_fc3(kp_ctx* c, bool transposed);
 enum { RANK_TRIPLE_RESULTS = 0, RANK_PREDICT_TAILS = 1, RANK_SORT_POSITION = 2 };
+// get_triple_results of a maximizer in fp64 (kp_rank.hip): q64 [n][dp] the ranking queries,
+// t64 [n] their target scores (q . E_o, or the kelpie column when o is the kelpie),
+// kcol64 [n] the kelpie column scores q . x; rank = #{e not filtered : score_e >= target}
+// over the frozen entities (scores q . E_e summed in fp64, sequentially over d) plus the
+// kelpie column.  The target itself counts unless filtered.
+void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* d_t64, const double* d_kcol64,
+                     const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt, float* d_target,
+                     int64_t* d_rank);
 void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
                        const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
                        int minimizer, float* d_target, int64_t* d_rank,

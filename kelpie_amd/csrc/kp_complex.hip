@@ -265,23 +265,43 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
   }
 }
 
-// ranking queries: q_s = x_s o R[p_s]; kelpie column score q_s . x_s
+// fp64 ranking queries (launch_rank_f64): q_s = x_s o R[p_s] from exact fp64 products of
+// the fp32 operands; the target score q_s . E_o and the kelpie column q_s . x_s as one
+// sequential fp64 FMA chain over d (the order kp_rank_f64_count scores every entity in)
+__device__ __forceinline__ double cx_q64(const float* __restrict__ lhs, const float* __restrict__ rel, int d,
+                                         int half) {
+  if (d < half) return (double)lhs[d] * (double)rel[d] - (double)lhs[d + half] * (double)rel[d + half];
+  if (d < 2 * half) {
+    const int i = d - half;
+    return (double)lhs[i] * (double)rel[d] + (double)lhs[d] * (double)rel[i];
+  }
+  return 0.0;
+}
+
 template <int DP>
-__global__ void kp_cx_rankq(const float* __restrict__ X, const float* __restrict__ R, int half,
-                            const int32_t* __restrict__ pred, int n_slots, float* __restrict__ Q,
-                            float* __restrict__ scores, int ld, int kcol) {
+__global__ void kp_cx_rankq64(const float* __restrict__ X, const float* __restrict__ R, const float* __restrict__ E,
+                              int n_ent, int half, const int32_t* __restrict__ pred, int n_slots,
+                              double* __restrict__ Q, double* __restrict__ t64, double* __restrict__ kcol64) {
   const int s = blockIdx.x;
   if (s >= n_slots) return;
   const float* x = X + (size_t)s * DP;
   const float* rel = R + (size_t)pred[3 * s + 1] * DP;
-  float z = 0.f;
-  for (int d = threadIdx.x; d < DP; d += 64) {
-    float q = cx_q(x, rel, d, half);
-    Q[(size_t)s * DP + d] = q;
-    z += q * x[d];
+  double* q = Q + (size_t)s * DP;
+  for (int d = threadIdx.x; d < DP; d += blockDim.x) q[d] = cx_q64(x, rel, d, half);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int o = pred[3 * s + 2];
+    double z = 0.0, t = 0.0;
+    for (int d = 0; d < DP; ++d) z = __fma_rn(q[d], (double)x[d], z);
+    if (o < n_ent) {
+      const float* eo = E + (size_t)o * DP;
+      for (int d = 0; d < DP; ++d) t = __fma_rn(q[d], (double)eo[d], t);
+    } else {
+      t = z;  // the kelpie entity is its own object
+    }
+    kcol64[s] = z;
+    t64[s] = t;
   }
-  z = wave_sum(z);
-  if (threadIdx.x == 0) scores[(size_t)s * ld + kcol] = z;
 }
 
 __global__ void kp_cx_scoreq(const float* __restrict__ E, const float* __restrict__ R, int dp, int half,
@@ -364,10 +384,10 @@ void launch_update(kp_ctx* c, int n_act, const int4* act, const CxPlan* plans, c
 }
 
 template <int DB>
-void launch_rankq(kp_ctx* c, const float* X, const int32_t* pred, int n, float* Q, float* scores, int ld) {
+void launch_rankq64(kp_ctx* c, const float* X, const int32_t* pred, int n, double* Q, double* t64, double* kcol64) {
   if (n <= 0) return;
-  hipLaunchKernelGGL((kp_cx_rankq<16 * DB>), dim3(n), dim3(64), 0, c->stream, X, c->dR, c->dim / 2, pred, n, Q,
-                     scores, ld, c->n_ent);
+  hipLaunchKernelGGL((kp_cx_rankq64<16 * DB>), dim3(n), dim3(64), 0, c->stream, X, c->dR, c->dE, c->n_ent,
+                     c->dim / 2, pred, n, Q, t64, kcol64);
   KP_HIP(hipGetLastError());
 }
 
@@ -685,10 +705,10 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   }
   KP_HIP(hipEventRecord(h1, c->stream));
 
-  // ---- ranking: scores of (kelpie, p, .) over E plus the kelpie column
-  const int ld = round_up(c->n_ent + 1, 4);
-  float* dScores = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)ns * ld));
-  float* dQr = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * (size_t)ns * DP));
+  // ---- ranking: scores of (kelpie, p, .) over E plus the kelpie column, in fp64
+  // (launch_rank_f64: at the reference init the target's neighbours are ~1e-5 relative away)
+  double* dQ64 = reinterpret_cast<double*>(c->ws[29].ensure(sizeof(double) * (size_t)ns * DP));
+  double* dT64 = reinterpret_cast<double*>(c->ws[30].ensure(sizeof(double) * 2 * (size_t)ns));
   int32_t* dPred = upload(c, c->ws[18], bt->pred, (size_t)ns * 3);
   std::vector<int32_t> po(ns);
   for (int s = 0; s < ns; ++s) po[s] = bt->pred[3 * s + 2];
@@ -697,9 +717,8 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   int32_t* dF = upload(c, c->ws[21], bt->filt, (size_t)bt->filt_off[ns]);
   float* dTarget = reinterpret_cast<float*>(c->ws[22].ensure(sizeof(float) * (size_t)ns));
   int64_t* dRank = reinterpret_cast<int64_t*>(c->ws[23].ensure(sizeof(int64_t) * (size_t)ns));
-  CX_DISPATCH(DBV, launch_rankq<DB>(c, dX, dPred, ns, dQr, dScores, ld));
-  launch_score_gemm(c, dQr, ns, dScores, ld, 0);
-  launch_rank_count(c, ns, dScores, ld, c->n_ent + 1, dPo, dFo, dF, 0, dTarget, dRank);
+  CX_DISPATCH(DBV, launch_rankq64<DB>(c, dX, dPred, ns, dQ64, dT64, dT64 + ns));
+  launch_rank_f64(c, ns, dQ64, dT64, dT64 + ns, dPo, dFo, dF, dTarget, dRank);
   KP_HIP(hipEventRecord(c->ev1, c->stream));
 
   if (bt->out_x) {

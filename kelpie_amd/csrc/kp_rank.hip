@@ -165,6 +165,128 @@ void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, in
   KP_HIP(hipGetLastError());
 }
 
+// ----------------------------------------------------------------------------
+// fp64 filtered rank of a maximizer (ComplEx get_triple_results, post_training_engine.py:
+// 101-125).  At the reference's random init the post-trained target sits among dense
+// near-ties (scores ~1e-6, nearest neighbour ~1e-11 away), and an fp32 dot product over
+// 400 terms with cancellation is off by ~1e-5 relative: enough to move the rank.  The
+// reference's fp64 run is the exact version of the same computation, so the device
+// scores in fp64 (exact products of the fp32 operands, one fp64 FMA chain over d per
+// entity, the same order for the target) and compares in fp64.  No score matrix is
+// written: each thread scores one entity for RQ slots and counts against their targets.
+// ----------------------------------------------------------------------------
+constexpr int RQ = 16;  // slots per workgroup row of the grid
+
+// E^T [dp][ldt] (fp32, zero columns past n_ent), once per context
+__global__ void kp_transpose_table(const float* __restrict__ E, int n_ent, int dp, float* __restrict__ ET, int ldt) {
+  __shared__ float tile[32][33];
+  const int e0 = blockIdx.x * 32, d0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int e = e0 + i, d = d0 + tx;
+    tile[i][tx] = (e < n_ent && d < dp) ? E[(size_t)e * dp + d] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int d = d0 + i, e = e0 + tx;
+    if (d < dp && e < ldt) ET[(size_t)d * ldt + e] = tile[tx][i];
+  }
+}
+
+// per slot: the filter bitmap over the n_ent + 1 columns (kelpie last)
+__global__ __launch_bounds__(256) void kp_rank_filter_bits(int n_slots, int nwords, const int32_t* __restrict__ filt_off,
+                                                           const int32_t* __restrict__ filt, int n_cols,
+                                                           uint32_t* __restrict__ bits) {
+  const int s = blockIdx.x;
+  uint32_t* b = bits + (size_t)s * nwords;
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) b[i] = 0u;
+  __syncthreads();
+  for (int i = filt_off[s] + threadIdx.x; i < filt_off[s + 1]; i += blockDim.x) {
+    const int e = filt[i];
+    if (e >= 0 && e < n_cols) atomicOr(&b[e >> 5], 1u << (e & 31));
+  }
+}
+
+// kelpie column and target: one thread per slot (counts the kelpie column, writes the
+// fp32 target score)
+__global__ void kp_rank_f64_kelpie(int n_slots, int n_ent, int nwords, const uint32_t* __restrict__ bits,
+                                   const double* __restrict__ t64, const double* __restrict__ kcol64,
+                                   float* __restrict__ target_out, unsigned long long* __restrict__ rank) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slots) return;
+  const bool filtered = (bits[(size_t)s * nwords + (n_ent >> 5)] >> (n_ent & 31)) & 1u;
+  rank[s] = (!filtered && kcol64[s] >= t64[s]) ? 1ull : 0ull;
+  target_out[s] = (float)t64[s];
+}
+
+__global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent, int dp, const double* __restrict__ Q,
+                                                         const double* __restrict__ t64,
+                                                         const int32_t* __restrict__ pred_o, const float* __restrict__ ET,
+                                                         int ldt, int nwords, const uint32_t* __restrict__ bits,
+                                                         unsigned long long* __restrict__ rank) {
+  __shared__ int part[4][RQ];
+  const int s0 = blockIdx.y * RQ;
+  const int e = blockIdx.x * 256 + threadIdx.x;  // < ldt: ET is zero-padded
+  const int ns = min(RQ, n_slots - s0);
+  double acc[RQ];
+#pragma unroll
+  for (int j = 0; j < RQ; ++j) acc[j] = 0.0;
+  // the slot rows are wave-uniform: scalar loads, one fp64 FMA chain over d per (slot, entity)
+  const double* q = Q + (size_t)s0 * dp;
+  for (int d = 0; d < dp; ++d) {
+    const double v = (double)ET[(size_t)d * ldt + e];
+#pragma unroll
+    for (int j = 0; j < RQ; ++j)
+      if (j < ns) acc[j] = __fma_rn(q[(size_t)j * dp + d], v, acc[j]);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < RQ; ++j) {
+    int hit = 0;
+    if (j < ns && e < n_ent) {
+      const int s = s0 + j;
+      const bool filtered = (bits[(size_t)s * nwords + (e >> 5)] >> (e & 31)) & 1u;
+      // the target counts itself (unless filtered) whatever the rounding of its own score
+      hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s]);
+    }
+    for (int o = 32; o > 0; o >>= 1) hit += __shfl_xor(hit, o, 64);
+    if (lane == 0) part[w][j] = hit;
+  }
+  __syncthreads();
+  if (threadIdx.x < ns) {
+    const int j = threadIdx.x;
+    const int tot = part[0][j] + part[1][j] + part[2][j] + part[3][j];
+    if (tot) atomicAdd(&rank[s0 + j], (unsigned long long)tot);
+  }
+}
+
+void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* d_t64, const double* d_kcol64,
+                     const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt, float* d_target,
+                     int64_t* d_rank) {
+  if (n_slots <= 0) return;
+  const int ldt = (c->n_ent + 255) / 256 * 256;
+  if (!c->eT_ready) {
+    float* ET = reinterpret_cast<float*>(c->eT.ensure(sizeof(float) * (size_t)c->dp * ldt));
+    hipLaunchKernelGGL(kp_transpose_table, dim3(ldt / 32, (c->dp + 31) / 32), dim3(256), 0, c->stream, c->dE,
+                       c->n_ent, c->dp, ET, ldt);
+    KP_HIP(hipGetLastError());
+    c->eT_ready = true;
+  }
+  const int n_cols = c->n_ent + 1;
+  const int nwords = (n_cols + 31) / 32;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(c->ws[28].ensure(sizeof(uint32_t) * (size_t)n_slots * nwords));
+  unsigned long long* rank = reinterpret_cast<unsigned long long*>(d_rank);
+  hipLaunchKernelGGL(kp_rank_filter_bits, dim3(n_slots), dim3(256), 0, c->stream, n_slots, nwords, d_filt_off, d_filt,
+                     n_cols, bits);
+  KP_HIP(hipGetLastError());
+  hipLaunchKernelGGL(kp_rank_f64_kelpie, dim3((n_slots + 63) / 64), dim3(64), 0, c->stream, n_slots, c->n_ent, nwords,
+                     bits, d_t64, d_kcol64, d_target, rank);
+  KP_HIP(hipGetLastError());
+  hipLaunchKernelGGL(kp_rank_f64_count, dim3(ldt / 256, (n_slots + RQ - 1) / RQ), dim3(256), 0, c->stream, n_slots,
+                     c->n_ent, c->dp, d_q64, d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
+  KP_HIP(hipGetLastError());
+}
+
 void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
                      int ldo, const float* bias, int act, int ksplit) {
   if (M <= 0 || N <= 0) return;

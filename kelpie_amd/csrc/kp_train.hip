@@ -413,6 +413,7 @@ void complex_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* tripl
   // the tables changed: the attention image and its prefix sums are stale
   c->e3_ready = false;
   c->e3pre_ready = false;
+  c->eT_ready = false;
 }
 
 // One PairwiseRankingOptimizer epoch (TransE) on the context's own tables: positive
@@ -530,4 +531,5 @@ void transe_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* pos, c
   KP_HIP(hipStreamSynchronize(c->stream));
   c->e3_ready = false;
   c->e3pre_ready = false;
+  c->eT_ready = false;
 }
