@@ -101,6 +101,8 @@ struct kp_ctx {
   bool e3_ready = false;
   DevBuf e3ts, e3pre;      // kp_attn3's fp64 tile sums / prefix sums of dE over tiles
   bool e3pre_ready = false;
+  DevBuf e4;               // kp_attn4's blocked split image of dE, built on first use
+  bool e4_ready = false;
   DevBuf eT;               // dE transposed [dp][round_up(n_ent, 256)] fp32 (fp64 rank scoring), on first use
   bool eT_ready = false;
   DevBuf fc3, fct3;        // ConvE: three-piece bf16 images of the FC weight and its transpose (kp_gemm3.hip)

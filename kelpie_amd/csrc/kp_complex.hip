@@ -111,52 +111,57 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
     float z = 0.f;
     for (int d = lane; d < 2 * half; d += 64) z += cx_q(x, rel, d, half) * x[d];
     z = wave_sum(z);
+    // The softmax normalisation in fp64 with correctly rounded exp / log.  <E> below is
+    // ~5e-4 per coordinate at the reference init and the row contributions cancel to a
+    // gradient up to ~100x smaller on the coordinates Adagrad has not saturated, so a
+    // one-sided ulp error of a fast exp / log here (every row, every step, the same
+    // sign) became a one-sided drift of those coordinates of the kelpie row (measured
+    // ~-4e-6 against the fp64 reference, tools/headline_probe.py).
     float mm = kNegInf;
     for (int sp = 0; sp < n_split; ++sp) mm = fmaxf(mm, att_m[(size_t)sp * nq + item]);
-    float ll = 0.f;
+    double ll = 0.0;
     for (int sp = 0; sp < n_split; ++sp) {
       const float ms = att_m[(size_t)sp * nq + item];
-      ll += (ms == kNegInf) ? 0.f : att_l[(size_t)sp * nq + item] * __expf(ms - mm);
+      ll += (ms == kNegInf) ? 0.0 : (double)att_l[(size_t)sp * nq + item] * exp((double)ms - (double)mm);
     }
-    const float lse_f = mm + __logf(ll);
-    const float hi = fmaxf(lse_f, z), lo = fminf(lse_f, z);
-    const float lse = hi + log1pf(__expf(lo - hi));
-    const float pk = __expf(z - lse);
+    const double lse_f = (double)mm + log(ll);
+    const double hi = fmax(lse_f, (double)z), lo = fmin(lse_f, (double)z);
+    const double lse = hi + log1p(exp(lo - hi));
+    const double pk = exp((double)z - lse);
     // merge the partials split by split: each split's loads for all of this lane's
     // dimensions are in flight together, with few live registers (occupancy)
     constexpr int NI = (DP / 2 + 63) / 64;
-    float ore_k[NI], oim_k[NI];
+    double ore_k[NI], oim_k[NI];
 #pragma unroll
-    for (int k = 0; k < NI; ++k) ore_k[k] = oim_k[k] = 0.f;
+    for (int k = 0; k < NI; ++k) ore_k[k] = oim_k[k] = 0.0;
     for (int sp = 0; sp < n_split; ++sp) {
       const float ms = att_m[(size_t)sp * nq + item];
-      const float wv = (ms == kNegInf) ? 0.f : __expf(ms - lse);
+      const double wv = (ms == kNegInf) ? 0.0 : exp((double)ms - lse);
       const float* Op = att_O + ((size_t)sp * nq + item) * DP;
 #pragma unroll
       for (int k = 0; k < NI; ++k) {
         const int i = lane + 64 * k;
         if (i < half) {
-          ore_k[k] += wv * Op[i];
-          oim_k[k] += wv * Op[i + half];
+          ore_k[k] += wv * (double)Op[i];
+          oim_k[k] += wv * (double)Op[i + half];
         }
       }
     }
-    const float fc = (float)Q.c, fck = (float)Q.ck;
-    const float cf = fc * pk - fck;
+    const double fc = (double)Q.c, fck = (double)Q.ck;
+    const double cf = fc * pk - fck;
     const float* ts = Tsum + (size_t)sq.z * DP;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
       const int i = lane + 64 * k;
       if (i >= half) continue;
-      const float a = x[i], b = x[i + half];
-      const float cc = rel[i], ee = rel[i + half];
-      const float ore = ore_k[k], oim = oim_k[k];
-      const float ere = ore + pk * a, eim = oim + pk * b;
-      const float dre = fc * ere - ts[i] - fck * a;
-      const float dim_ = fc * eim - ts[i + half] - fck * b;
-      const float qre = a * cc - b * ee, qim = a * ee + b * cc;
-      out[i] = dre * cc + dim_ * ee + cf * qre;
-      out[i + half] = -dre * ee + dim_ * cc + cf * qim;
+      const double a = x[i], b = x[i + half];
+      const double cc = rel[i], ee = rel[i + half];
+      const double ere = ore_k[k] + pk * a, eim = oim_k[k] + pk * b;
+      const double dre = fc * ere - (double)ts[i] - fck * a;
+      const double dim_ = fc * eim - (double)ts[i + half] - fck * b;
+      const double qre = a * cc - b * ee, qim = a * ee + b * cc;
+      out[i] = (float)(dre * cc + dim_ * ee + cf * qre);
+      out[i + half] = (float)(-dre * ee + dim_ * cc + cf * qim);
     }
   } else {
     const int4 st = stept[item - nq];  // slot, pair, count
@@ -165,11 +170,11 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
     float z = 0.f;
     for (int d = lane; d < 2 * half; d += 64) z += qp[d] * x[d];
     z = wave_sum(z);
-    const float lf = lsef[st.y];
-    const float hi = fmaxf(lf, z), lo = fminf(lf, z);
-    const float lse = hi + log1pf(__expf(lo - hi));
-    const float coef = (float)st.z * (__expf(z - lse) - 1.0f);
-    for (int d = lane; d < 2 * half; d += 64) out[d] = coef * qp[d];
+    const double lf = lsef[st.y];
+    const double hi = fmax(lf, (double)z), lo = fmin(lf, (double)z);
+    const double lse = hi + log1p(exp(lo - hi));
+    const double coef = (double)st.z * (exp((double)z - lse) - 1.0);
+    for (int d = lane; d < 2 * half; d += 64) out[d] = (float)(coef * (double)qp[d]);
   }
 }
 

@@ -13,6 +13,10 @@
 #include <random>
 
 #include "kp_attn3.hpp"  // -I selects the source tree under test (tools/attn_micro.sh)
+#if __has_include("kp_attn4.hpp")
+#include "kp_attn4.hpp"
+#define KP_MICRO_HAS_ATTN4 1
+#endif
 
 using namespace kpattn;
 
@@ -52,7 +56,20 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
   KP_HIP(hipMalloc(&dl, (size_t)parts * nq * 4));
   KP_HIP(hipMalloc(&dO, (size_t)parts * nq * DP * 4));
   const float ylo = 0.05f;
-  auto launch = [&]() { launch_attn3<DB, MODE>(&c, n_ent, dQ, nq, plan, dm, dl, dO, dqs, ylo); };
+  // KP_MICRO_ATTN4=1: the pipelined kernel (kp_attn4.hpp) where it exists
+  const bool use4 = std::getenv("KP_MICRO_ATTN4") && std::atoi(std::getenv("KP_MICRO_ATTN4")) == 1;
+  auto launch = [&]() {
+#ifdef KP_MICRO_HAS_ATTN4
+    if constexpr (attn4_supported(DB) && MODE == ATT_SOFTMAX_O) {
+      if (use4) {
+        launch_attn4<DB>(&c, n_ent, dQ, nq, plan, dm, dl, dO);
+        return;
+      }
+    }
+#endif
+    (void)use4;
+    launch_attn3<DB, MODE>(&c, n_ent, dQ, nq, plan, dm, dl, dO, dqs, ylo);
+  };
   launch();
   KP_HIP(hipStreamSynchronize(c.stream));
   hipEvent_t e0, e1;

@@ -28,7 +28,13 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "gpurun_out")
 
 
-def ref_side(workload, variant, threads):
+def _fixture(name):
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "fullsize", name + ".json")) as f:
+        return json.load(f)
+
+
+def ref_side(workload, variant, threads, name):
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import bench
@@ -38,7 +44,7 @@ def ref_side(workload, variant, threads):
     from kelpie_amd import synth
     torch.set_num_threads(threads)
     wl = bench.WORKLOADS[workload]
-    fx = bench.load_fixture(workload)
+    fx = _fixture(name)
     src = ref_harness.load_reference()
     g = synth.make_graph(wl["shape"], seed=0)
     w0 = synth.make_weights(wl["model"], g.num_entities, g.num_relations, wl["dim"], seed=0)
@@ -65,18 +71,18 @@ def ref_side(workload, variant, threads):
         rels, log = noise_floor.run_reference(src, wl, dataset, model, tuple(fx["pred"]),
                                               [tuple(c) for c in fx["candidates"]], fx.get("entities_to_convert"))
     os.makedirs(OUT, exist_ok=True)
-    np.savez_compressed(os.path.join(OUT, f"probe_{workload}_{variant}.npz"), rows=np.array(rows),
+    np.savez_compressed(os.path.join(OUT, f"probe_{name}_{variant}.npz"), rows=np.array(rows),
                         scores=np.array(scores), rank=np.array([m[0] for m in meta]),
                         score=np.array([m[1] for m in meta]))
     print(variant, rels, noise_floor.deltas_of(log))
 
 
-def gpu_side(workload, tag):
+def gpu_side(workload, tag, name):
     import bench
     from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine
     from kelpie_amd import engine as keng
     wl = bench.WORKLOADS[workload]
-    fx = bench.load_fixture(workload)
+    fx = _fixture(name)
     ds, model, _ = bench.build(wl, 0, 0)
     cls = SufficientPostTrainingEngine if wl["mode"] == "sufficient" else NecessaryPostTrainingEngine
     eng = cls(model, ds, wl["hp"])
@@ -95,18 +101,13 @@ def gpu_side(workload, tag):
     r = np.concatenate([c[1] for c in captured])
     x = np.concatenate([c[2] for c in captured])
     os.makedirs(OUT, exist_ok=True)
-    np.savez_compressed(os.path.join(OUT, f"probe_{workload}_gpu{tag}.npz"), rows=x, score=s, rank=r)
+    np.savez_compressed(os.path.join(OUT, f"probe_{name}_gpu{tag}.npz"), rows=x, score=s, rank=r)
     print(json.dumps(par))
-
-
-def slot_order(fx, n_conv):
-    """Map GPU slot order to reference call order.  The engine schedules, per candidate and
-    conversion entity, [base (first time only), pt]; the reference logs the same order."""
-    return None  # identical by construction (post_training_engine.py:46-62 call order)
 
 
 def compare(workload, tags):
     ref = {v: np.load(os.path.join(OUT, f"probe_{workload}_{v}.npz")) for v in ("fp32", "fp64")}
+    # (workload here is the fixture name)
     e64 = ref["fp64"]
     print(f"{'i':>3} {'rank64':>7} {'r32':>6} " + " ".join(f"{'r' + t:>6}" for t in tags) +
           "  xerr32   " + " ".join(f"xerr{t:<6}" for t in tags) + "  serr32    " +
@@ -142,13 +143,17 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--tag", default="")
     ap.add_argument("--tags", nargs="+", default=[""])
+    ap.add_argument("--fixture", default=None, help="tests/golden/fullsize/<name>.json (default: the workload's)")
     a = ap.parse_args()
+    name = a.fixture or a.workload
+    if a.fixture:
+        a.workload = _fixture(name)["workload"]
     if a.side == "ref":
-        ref_side(a.workload, a.variant, a.threads)
+        ref_side(a.workload, a.variant, a.threads, name)
     elif a.side == "gpu":
-        gpu_side(a.workload, a.tag)
+        gpu_side(a.workload, a.tag, name)
     else:
-        compare(a.workload, a.tags)
+        compare(name, a.tags)
 
 
 if __name__ == "__main__":
