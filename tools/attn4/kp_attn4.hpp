@@ -1,5 +1,9 @@
 // kp_attn4.hpp -- the ComplEx step attention (kp_attn3<DB, ATT_SOFTMAX_O>'s contract) as a
-// cross-tile software pipeline.
+// cross-tile software pipeline.  EXPERIMENT, not part of the library: built only into the
+// micro-benchmark (tools/attn_micro.hip with -Itools/attn4).  Correct (the micro's fp64
+// check and output hash equal kp_attn3's on every shape) but no faster: 0.351-0.353 vs
+// 0.353-0.358 ms (FB15k-237 shape), 1.300-1.303 vs 1.311-1.341 ms (DB100K shape), best
+// variant KP_A4_SAHEAD=2 (profiles/r03k_attn4_micro.jsonl).
 //
 // kp_attn3 runs each 32-entity key tile as a dependent chain per wave: S = E . Q^T on
 // the MFMA pipe, then the softmax weights and their three-piece split on the VALU, then
@@ -42,6 +46,9 @@
 
 namespace kpattn {
 
+#if (defined(KP_A4_NODMA) || defined(KP_A4_NOSM) || defined(KP_A4_NOREAD)) && !defined(KP_DIAGNOSTIC_BUILD)
+#error "kp_attn4 timing-only diagnostics (wrong results) need KP_DIAGNOSTIC_BUILD"
+#endif
 #ifndef KP_A4_DMA_PER_GROUP
 #define KP_A4_DMA_PER_GROUP 2  // LDS-DMA pieces per wave issued with each MFMA group
 #endif
@@ -109,6 +116,14 @@ __device__ __forceinline__ bf16x4 rdt(uint32_t lo, uint32_t hi) {
 
 // The group stream of one steady iteration.  Position p in [0, NPOS): H1 = [0, 3 SH1),
 // H2 = [3 SH1, NPOS).  kind 0 = O block, 1 = S step; idx = block / step.
+#ifndef KP_A4_SAHEAD
+#define KP_A4_SAHEAD 1  // groups ahead that an S step's operands are read (1: one S operand slot)
+#endif
+#ifndef KP_A4_OAHEAD
+#define KP_A4_OAHEAD 2  // groups ahead that an O block's operands are read
+#endif
+static_assert(KP_A4_SAHEAD >= 1 && KP_A4_SAHEAD <= 2 && KP_A4_OAHEAD >= 2 && KP_A4_OAHEAD <= 3, "read-ahead");
+
 template <int DB>
 struct Attn4Plan {
   static constexpr int DP = 16 * DB;
@@ -137,12 +152,44 @@ struct Attn4Plan {
   }
   // first position of the weights' O blocks (H2's tail)
   static constexpr int SM0 = NH1 + 2 + 2 * NS2 - 1;
+  // Read schedule.  Group q (q >= NPOS: the next iteration's group q - NPOS, always an O
+  // block) has its 6 operand reads issued during position issue(q) = q - ahead(kind).
+  static constexpr int kind_x(int q) { return q < NPOS ? kind(q) : 0; }
+  static constexpr int ahead(int q) { return kind_x(q) == 1 ? KP_A4_SAHEAD : KP_A4_OAHEAD; }
+  static constexpr int issue(int q) { return q - ahead(q); }
+  // groups whose reads are issued during position p, in order (at most 2)
+  static constexpr int MAXA = KP_A4_OAHEAD > KP_A4_SAHEAD ? KP_A4_OAHEAD : KP_A4_SAHEAD;
+  static constexpr int n_issued(int p) {
+    int n = 0;
+    for (int q = p + 1; q <= p + MAXA; ++q)
+      if (issue(q) == p) ++n;
+    return n;
+  }
+  static constexpr int issued(int p, int i) {
+    int n = 0;
+    for (int q = p + 1; q <= p + MAXA; ++q)
+      if (issue(q) == p) {
+        if (n == i) return q;
+        ++n;
+      }
+    return -1;
+  }
+  // lgkmcnt before group p's MFMAs: reads issued before position p that come after p's
+  // own in issue order (those of later groups)
+  static constexpr int wait(int p) {
+    int n = 0;
+    for (int r = p + 1; r <= p + MAXA; ++r)
+      if (issue(r) < p && (issue(r) > issue(p) || (issue(r) == issue(p) && r > p))) n += 6;
+    return n;
+  }
+  static_assert(NPOS >= 4, "plan");
 };
 
 // O-operand slot of block m (see kp_attn4's operand slots)
 template <int DB>
 __host__ __device__ constexpr int attn4_oslot(int m) {
-  return (m == DB - 1 && DB % 3 == 1) ? 3 : m % 3;
+  constexpr int R = KP_A4_OAHEAD + 1;  // ring: the block in use plus OAHEAD in flight
+  return (m == DB - 1 && DB % R == 1) ? R : m % R;
 }
 
 template <int DB>
@@ -162,7 +209,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
   constexpr int K1 = (P1 + 3) / 4, K2 = (P2 + 3) / 4;  // per wave, at most
   extern __shared__ __attribute__((aligned(16))) uint8_t lds4[];  // [2][TILE_B]
   constexpr auto oslot = [](int m) constexpr { return attn4_oslot<DB>(m); };
-  static_assert(DB % 3 != 2, "kp_attn4: the O-operand ring needs DB % 3 != 2");
+  static_assert(DB % (KP_A4_OAHEAD + 1) <= 1, "kp_attn4: the O-operand ring needs DB % (OAHEAD + 1) <= 1");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -170,6 +217,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
   const int g = lane >> 4, c = lane & 15;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds4;
   int kt_base = 0, key_begin = 0, key_end = 0;
+#ifdef KP_ATTN3_STAMPS
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
+#endif
 
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(E4), (short)0, (int)((n_ent + 31) / 32 * TILE_B + 1024), 0x00020000);
@@ -262,16 +312,17 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
     // operand slots: S reads by step parity, O reads by oslot(block) -- a ring of three
     // (reads run two groups ahead) plus a fourth for the last block when DB % 3 == 1, so
     // the ring continues into the next tile's blocks 0 and 1 (read during blocks DB-2, DB-1)
-    bf16x8 sa[2][2][3];  // [slot][sub-tile][piece]
+    constexpr int NSS = KP_A4_SAHEAD;  // S operand slots
+    bf16x8 sa[NSS][2][3];  // [slot][sub-tile][piece]
     bf16x4 ta[2][3];     // tail step
-    bf16x4 ol[4][3], oh[4][3];
+    bf16x4 ol[KP_A4_OAHEAD + 2][3], oh[KP_A4_OAHEAD + 2][3];
     // reads of S step J (6) from the buffer at bases (lo, hi)
     auto read_s = [&](auto J, uint32_t lo, uint32_t hi, uint32_t tlo, uint32_t thi) {
       constexpr int j = decltype(J)::value;
       if constexpr (j < NK) {
         static_for<0, 6>([&](auto K) {
           constexpr int k = decltype(K)::value, u = k & 1, p = k >> 1;
-          sa[j & 1][u][p] = rd8<(2 * j * 3 + p) * 1024 + u * 512>(lo, hi);
+          sa[j % NSS][u][p] = rd8<(2 * j * 3 + p) * 1024 + u * 512>(lo, hi);
         });
       } else {
         static_for<0, 6>([&](auto K) {
@@ -284,7 +335,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
     auto read_s1 = [&](auto J, auto K, uint32_t lo, uint32_t hi, uint32_t tlo, uint32_t thi) {
       constexpr int j = decltype(J)::value, k = decltype(K)::value, u = k & 1, p = k >> 1;
       if constexpr (j < NK)
-        sa[j & 1][u][p] = rd8<(2 * j * 3 + p) * 1024 + u * 512>(lo, hi);
+        sa[j % NSS][u][p] = rd8<(2 * j * 3 + p) * 1024 + u * 512>(lo, hi);
       else
         ta[u][p] = rd4<(2 * NK * 3 + p) * 1024 + u * 512>(tlo, thi);
     };
@@ -303,7 +354,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
       static_for<0, 12>([&](auto K) {
         constexpr int k = decltype(K)::value, u = k & 1, pr = k >> 1;
         if constexpr (j < NK)
-          sc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[j & 1][u][kPA[pr]], qb[j < NK ? j : 0][kPB[pr]], sc[u],
+          sc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[j % NSS][u][kPA[pr]], qb[j < NK ? j : 0][kPB[pr]], sc[u],
                                                           0, 0, 0);
         else
           sc[u] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, ta[u][kPA[pr]]),
@@ -333,10 +384,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
     float lt = 0.f;
     auto weight1 = [&](int k0, auto JJ) {
       constexpr int jj = decltype(JJ)::value, u = jj >> 2, r = jj & 3;
+      // branch-free (selects, no exec-masked region inside the MFMA stream)
       const bool ok = k0 + 16 * u + 4 * g + r < key_end;
-      const float v = ok ? sc[u][r] : kNegInf;
-      m_seen = fmaxf(m_seen, v);
-      const float pw = ok ? __fsub_rn(__expf(v - m_ref), csh) : 0.f;
+      const float s = sc[u][r];
+      m_seen = fmaxf(m_seen, ok ? s : kNegInf);
+      const float e = __expf((ok ? s : m_ref) - m_ref);
+      const float pw = ok ? __fsub_rn(e, csh) : 0.f;
       lt += pw;
       __bf16 h, mm, l;
       split3(pw, h, mm, l);
@@ -361,18 +414,31 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
         // S(0), one step of reads ahead
         const uint32_t lo = sbase(0), hi = lo + 32768, tlo = tbase(0), thi = tlo + 32768;
         sc[0] = sc[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        read_s(std::integral_constant<int, 0>{}, lo, hi, tlo, thi);
-        static_for<0, NS>([&](auto J) {
-          constexpr int j = decltype(J)::value;
-          if constexpr (j + 1 < NS) {
-            read_s(std::integral_constant<int, j + 1>{}, lo, hi, tlo, thi);
-            lgkm_wait<6>();
-          } else {
+        if constexpr (NSS >= 2) {
+          read_s(std::integral_constant<int, 0>{}, lo, hi, tlo, thi);
+          static_for<0, NS>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if constexpr (j + 1 < NS) {
+              read_s(std::integral_constant<int, j + 1>{}, lo, hi, tlo, thi);
+              lgkm_wait<6>();
+            } else {
+              lgkm_wait<0>();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_s(J, [](auto) {});
+          });
+        } else {
+          // one S slot: step j + 1's reads ride in step j's MFMA gaps (after its operands
+          // are in registers: the A pieces are copied into the MFMA operands first)
+          read_s(std::integral_constant<int, 0>{}, lo, hi, tlo, thi);
+          static_for<0, NS>([&](auto J) {
+            constexpr int j = decltype(J)::value;
             lgkm_wait<0>();
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          mfma_s(J, [](auto) {});
-        });
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_s(J, [](auto) {});
+            if constexpr (j + 1 < NS) read_s(std::integral_constant<int, j + 1>{}, lo, hi, tlo, thi);
+          });
+        }
         // weights of tile 0: the reference max (pass 0) and the centring shift
         if (pass == 0) {
           float tmax = kNegInf;
@@ -398,14 +464,20 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
         l_run += lt;
 #pragma unroll
         for (int p = 0; p < 3; ++p) pb[p] = pbn[p];
-        // the first two groups' reads (O blocks 0 and 1 of tile 0)
+        // the first OAHEAD groups' reads (O blocks of tile 0)
         const uint32_t olo = obase(0), ohi = olo + 32768;
-        static_for<0, 6>([&](auto K) { read_o1(std::integral_constant<int, 0>{}, K, olo, ohi); });
-        static_for<0, 6>([&](auto K) { read_o1(std::integral_constant<int, 1>{}, K, olo, ohi); });
+        static_for<0, KP_A4_OAHEAD>([&](auto M) {
+          static_for<0, 6>([&](auto K) { read_o1(M, K, olo, ohi); });
+        });
       }
 
       // ---- steady iterations: O(t) with S(t+1)
+#ifdef KP_ATTN3_STAMPS
+      // diagnostic build: [H1 groups, mid barrier, H2 groups, end barrier, iterations]
+      unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0;
+#endif
       for (int t = 0; t + 1 < ntiles; ++t) {
+        KP3_STAMP(st0);
         const int bo = t & 1, bs = bo ^ 1;
         const uint32_t olo = obase(bo), ohi = olo + 32768;
         const uint32_t slo = sbase(bs), shi = slo + 32768, tlo = tbase(bs), thi = tlo + 32768;
@@ -423,60 +495,93 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
           if constexpr (p == NH1) {
             // mid barrier: this half's DMA (tile t+1, blocks [OH1, DB)) has landed everywhere,
             // and every wave is past O(t) blocks [0, OH1)
+            KP3_STAMP(st1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            KP3_STAMP(st2);
           }
-          lgkm_wait<6>();
+          lgkm_wait<PL::wait(p)>();
           __builtin_amdgcn_sched_barrier(0);
           // DMA pieces of this position: KP_A4_DMA_PER_GROUP per group from the start of each
           // half, so the last piece has most of the half to land before the barrier that
           // waits for it (spread evenly over the half, the last pieces' fetch latency was
           // exposed at the barriers)
+#ifdef KP_A4_NODMA
+          if constexpr (false) {
+#else
           if constexpr (p < NH1) {
+#endif
 #pragma unroll
             for (int k = 0; k < K1; ++k)
               if (k / KP_A4_DMA_PER_GROUP == p) dma_h1(t + 1, k);
-          } else {
+          } else if constexpr (p >= NH1
+#ifdef KP_A4_NODMA
+                               && false
+#endif
+          ) {
 #pragma unroll
             for (int k = 0; k < K2; ++k)
               if (k / KP_A4_DMA_PER_GROUP == p - NH1) dma_h2(t + 2, k);
           }
           __builtin_amdgcn_sched_barrier(0);
-          // reads of position p + 2 (the next iteration's first two O blocks at the end)
-          auto rd_next = [&](auto K) {
-            constexpr int k = decltype(K)::value;
-            if constexpr (p + 2 < NPOS) {
-              constexpr int kn = PL::kind(p + 2), in = PL::idx(p + 2);
-              if constexpr (kn == 1)
-                read_s1(std::integral_constant<int, in>{}, K, slo, shi, tlo, thi);
-              else
-                read_o1(std::integral_constant<int, in>{}, K, olo, ohi);
-            } else {
-              read_o1(std::integral_constant<int, p + 2 - NPOS>{}, K, nlo, nhi);
+          // read r (0 .. 6 n_issued - 1) of the groups whose operands are read during p (the
+          // next iteration's first O blocks at the end of the stream)
+          constexpr int NR = 6 * PL::n_issued(p);
+          auto rd_next = [&](auto R) {
+            constexpr int r = decltype(R)::value;
+#ifdef KP_A4_NOREAD
+            return;
+#endif
+            if constexpr (r < NR) {
+              constexpr int q = PL::issued(p, r / 6);
+              constexpr auto K = std::integral_constant<int, r % 6>{};
+              if constexpr (q < NPOS) {
+                constexpr int kn = PL::kind(q), in = PL::idx(q);
+                if constexpr (kn == 1)
+                  read_s1(std::integral_constant<int, in>{}, K, slo, shi, tlo, thi);
+                else
+                  read_o1(std::integral_constant<int, in>{}, K, olo, ohi);
+              } else {
+                read_o1(std::integral_constant<int, q - NPOS>{}, K, nlo, nhi);
+              }
             }
-            (void)k;
           };
           if constexpr (kind == 1) {
-            mfma_s(std::integral_constant<int, ix>{}, [&](auto K) {
-              constexpr int k = decltype(K)::value;
-              if constexpr (k % 2 == 0) rd_next(std::integral_constant<int, k / 2>{});
-            });
+            // 12 MFMAs: one read after each of the first NR
+            mfma_s(std::integral_constant<int, ix>{}, [&](auto K) { rd_next(K); });
           } else {
+            // 6 MFMAs: NR / 6 reads after each
             mfma_o(std::integral_constant<int, ix>{}, [&](auto K) {
               constexpr int k = decltype(K)::value;
-              rd_next(K);
+              if constexpr (NR > 6) {
+                rd_next(std::integral_constant<int, 2 * k>{});
+                rd_next(std::integral_constant<int, 2 * k + 1>{});
+              } else {
+                rd_next(K);
+              }
               // the weights of tile t+1 in the issue gaps of the last O blocks
               if constexpr (p >= PL::SM0) {
                 constexpr int slot = (p - PL::SM0) * 6 + k;  // 0 .. 6 OSM - 1
+#ifndef KP_A4_NOSM
                 if constexpr (slot % 3 == 1 && slot / 3 < 8) weight1(k1, std::integral_constant<int, slot / 3>{});
+#endif
               }
             });
           }
         });
         l_run += lt;
+        KP3_STAMP(st3);
         // end barrier: tile t+2's first part has landed; every wave is done with buffer bo
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        KP3_STAMP(st4);
+#ifdef KP_ATTN3_STAMPS
+        st_acc[0] += st1 - st0;
+        st_acc[1] += st2 - st1;
+        st_acc[2] += st3 - st2;
+        st_acc[3] += st4 - st3;
+        st_acc[4] += 1;
+#endif
 #pragma unroll
         for (int p = 0; p < 3; ++p) pb[p] = pbn[p];
       }
@@ -487,13 +592,13 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
         const uint32_t olo = obase(bo), ohi = olo + 32768;
         static_for<0, DB>([&](auto M) {
           constexpr int m = decltype(M)::value;
-          if constexpr (m + 1 < DB)
-            lgkm_wait<6>();
-          else
-            lgkm_wait<0>();
+          // in flight: blocks m .. min(m + OAHEAD - 1, DB - 1)
+          constexpr int later = (m + KP_A4_OAHEAD - 1 < DB ? KP_A4_OAHEAD - 1 : DB - 1 - m);
+          lgkm_wait<6 * later>();
           __builtin_amdgcn_sched_barrier(0);
           mfma_o(M, [&](auto K) {
-            if constexpr (m + 2 < DB) read_o1(std::integral_constant<int, m + 2>{}, K, olo, ohi);
+            if constexpr (m + KP_A4_OAHEAD < DB)
+              read_o1(std::integral_constant<int, m + KP_A4_OAHEAD>{}, K, olo, ohi);
           });
         });
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -545,8 +650,13 @@ __global__ __launch_bounds__(256, 1) void kp_attn4(const uint8_t* __restrict__ E
       }
     }
   }
+#ifdef KP_ATTN3_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_attn3_stamps[i], st_acc[i]);
+#endif
 }
 
+// (diagnostic stamps flushed at the end of kp_attn4, see below)
 // Host: the blocked split image of c->dE, built once per context.
 template <int DB>
 const uint8_t* split3_blocked_image(kp_ctx* c) {
