@@ -323,6 +323,45 @@ int kp_graph_set_classes(kp_graph* g, const int64_t* cls_off, const int32_t* cls
  * +inf when there is no path. */
 int kp_graph_dijkstra_pairs(const kp_graph* g, int32_t n, const int32_t* src, const int32_t* dst, double* out);
 
+/* ---- slot assembly of a post-training batch, host C++ ----
+ * Replaces the per-call KelpieDataset work of the reference
+ * (src/data/kelpie_dataset.py:13-158: the deep-copied kelpie dataset, its
+ * remove_training_triples / add_training_triples edits and the to_filter lists
+ * get_triple_results reads, post_training_engine.py:101-125) for a whole batch of
+ * calls: one view per subject, one library call per run of calls, rows and filters
+ * packed straight into kp_batch's arrays (csrc/kp_sched.cpp).
+ *
+ * kp_view_create: base[n][3] = the subject's training triples with the original entity
+ * replaced by `kelpie` (the caller's order: Dataset.entity_to_training_triples),
+ * extra[m][3] = its validation and test triples (they only enter the filters);
+ * n_rel = |R| (inverse relation = p + n_rel). */
+typedef struct kp_view kp_view;
+typedef struct kp_sched_batch kp_sched_batch;
+int kp_view_create(int32_t kelpie, int32_t n_rel, int32_t original, const int32_t* base, int32_t n,
+                   const int32_t* extra, int32_t m, kp_view** out);
+void kp_view_destroy(kp_view* v);
+int kp_sched_batch_create(kp_sched_batch** out);
+void kp_sched_batch_destroy(kp_sched_batch* b);
+
+/* n calls: call c ranks (kelpie, rel[c], ·) after editing views[c] with the candidate
+ * triples cands[cand_off[c] .. cand_off[c+1]) (original ids); flags[c]: bit 0 the call
+ * needs its base post-training, bit 1 this process runs that base slot, bit 2 it runs the
+ * edited (pt) slot, bit 3 sufficient mode (an addition; else a removal).  Per call and
+ * slot (base, pt): slot_idx[2c + j] (-1: not run here), n_rows[2c + j] (rows incl.
+ * inverses), n_filt[2c + j] (filter length).  The edits are checked in the reference's
+ * order; at the first failing call fail = {call, code, triple}: code 1 a triple without
+ * the entity (AssertionError), 2 not a kelpie training triple (KeyError), 3 a removal the
+ * filter multiset cannot take (list.remove ValueError); that call's base slot is added,
+ * nothing after it.  Otherwise fail[0] = -1.  The views must outlive the batch. */
+int kp_sched_add_calls(kp_sched_batch* b, int32_t n, kp_view* const* views, const int32_t* rel, const uint8_t* flags,
+                       const int32_t* cand_off, const int32_t* cands, int32_t* slot_idx, int32_t* n_rows,
+                       int32_t* n_filt, int32_t* fail);
+
+/* Rows (kelpie rows then their inverses, the optimizers' order) and rank filters of the
+ * batch slots idx[0 .. n), back to back, into rows[rows_cap] / filt[filt_cap] (int32). */
+int kp_sched_pack(const kp_sched_batch* b, int32_t n, const int32_t* idx, int32_t* rows, int64_t rows_cap,
+                  int32_t* filt, int64_t filt_cap);
+
 /* Library version string. */
 const char* kp_version(void);
 

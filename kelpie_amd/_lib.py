@@ -22,7 +22,8 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_rng_conve_masks_enqueue", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
            "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals", "kp_rng_normal",
-           "kp_rng_transe_calls", "kp_train_epoch", "kp_read_tables"]
+           "kp_rng_transe_calls", "kp_train_epoch", "kp_read_tables", "kp_view_create", "kp_view_destroy",
+           "kp_sched_batch_create", "kp_sched_batch_destroy", "kp_sched_add_calls", "kp_sched_pack"]
 
 
 class ModelDesc(C.Structure):
@@ -98,6 +99,17 @@ def lib():
                                      C.POINTER(C.c_int64), C.POINTER(C.c_double)]
         L.kp_hot_intervals.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(C.c_int64)]
         L.kp_version.restype = C.c_char_p
+        L.kp_view_create.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                                     C.POINTER(C.c_void_p)]
+        L.kp_view_destroy.argtypes = [C.c_void_p]
+        L.kp_view_destroy.restype = None
+        L.kp_sched_batch_create.argtypes = [C.POINTER(C.c_void_p)]
+        L.kp_sched_batch_destroy.argtypes = [C.c_void_p]
+        L.kp_sched_batch_destroy.restype = None
+        L.kp_sched_add_calls.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.kp_sched_pack.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                    C.c_int64]
         _LIB = L
     return _LIB
 
@@ -394,3 +406,67 @@ class Graph:
         out = np.empty(len(s), np.float64)
         self._check(self._lib.kp_graph_dijkstra_pairs(self._h, len(s), _ptr(s), _ptr(d), _ptr(out)))
         return out
+
+
+class NativeView:
+    """A kelpie view in the library's host scheduler (kp_view_create, csrc/kp_sched.cpp):
+    the kelpie entity's training triples ``base`` [n][3] (original entity already replaced,
+    in the Python view's order) and its validation / test triples ``extra`` (filters only)."""
+
+    def __init__(self, kelpie: int, n_rel: int, original: int, base: np.ndarray, extra: np.ndarray):
+        b = np.ascontiguousarray(base, dtype=np.int32).reshape(-1, 3)
+        e = np.ascontiguousarray(extra, dtype=np.int32).reshape(-1, 3)
+        h = C.c_void_p()
+        self._lib = lib()
+        check(self._lib.kp_view_create(int(kelpie), int(n_rel), int(original), _ptr(b), len(b), _ptr(e), len(e),
+                                       C.byref(h)))
+        self.h = h.value
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self._lib.kp_view_destroy(C.c_void_p(h))
+            self.h = None
+
+
+class SchedBatch:
+    """One engine batch's natively assembled slots (kp_sched_*): ``add_calls`` edits the
+    views and builds the rank filters of a run of calls, ``pack`` writes the rows and
+    filters of any of its slots into the kp_posttrain_rank arrays."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        self._lib = lib()
+        check(self._lib.kp_sched_batch_create(C.byref(h)))
+        self.h = h.value
+        self.views = []  # the NativeViews its slots point into (kept alive with the batch)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self._lib.kp_sched_batch_destroy(C.c_void_p(h))
+            self.h = None
+
+    def add_calls(self, views, rels, flags, cand_off, cands):
+        """Per call (flags: bit 0 base needed, 1 base owned, 2 pt owned, 3 sufficient):
+        returns (slot index [n][2], rows [n][2], filter lengths [n][2], fail (call, code,
+        triple)); code 1 assertion, 2 KeyError, 3 ValueError; -1 entries: no slot."""
+        n = len(views)
+        v = np.array(views, dtype=np.uint64)
+        r = np.ascontiguousarray(rels, dtype=np.int32)
+        f = np.ascontiguousarray(flags, dtype=np.uint8)
+        co = np.ascontiguousarray(cand_off, dtype=np.int32)
+        ct = np.ascontiguousarray(cands, dtype=np.int32).reshape(-1, 3) if len(cands) else np.zeros((1, 3), np.int32)
+        idx = np.empty((n, 2), np.int32)
+        rows = np.empty((n, 2), np.int32)
+        nf = np.empty((n, 2), np.int32)
+        fail = np.empty(3, np.int32)
+        check(self._lib.kp_sched_add_calls(C.c_void_p(self.h), n, _ptr(v), _ptr(r), _ptr(f), _ptr(co), _ptr(ct),
+                                           _ptr(idx), _ptr(rows), _ptr(nf), _ptr(fail)))
+        return idx, rows, nf, (int(fail[0]), int(fail[1]), int(fail[2]))
+
+    def pack(self, idx, rows: np.ndarray, filt: np.ndarray):
+        i = np.ascontiguousarray(idx, dtype=np.int32)
+        assert rows.dtype == np.int32 and rows.flags.c_contiguous and filt.dtype == np.int32
+        check(self._lib.kp_sched_pack(C.c_void_p(self.h), len(i), _ptr(i), _ptr(rows), rows.size, _ptr(filt),
+                                      filt.size))

@@ -83,6 +83,10 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     if (const char* a = std::getenv("KP_FC"))
       c->fc_mode = std::strcmp(a, "f32") == 0 ? 0 : std::strcmp(a, "fwd") == 0 ? 1 : std::strcmp(a, "bwd") == 0 ? 2 : 3;
     if (c->attn_mode == 0) c->fc_mode = 0;
+    // ConvE d = 200: fused conv + FC forward and FC^T + transposed-conv backward
+    // (kp_cv_fused.hpp) by default; KP_CV_FUSED=0 selects the separate kernels (A/B)
+    c->cv_fused = 1;
+    if (const char* a = std::getenv("KP_CV_FUSED")) c->cv_fused = std::atoi(a) != 0;
     if (const char* a = std::getenv("KP_ATTN_PART"))
       c->attn_part = std::strcmp(a, "streamk") == 0 ? 1 : std::strcmp(a, "ranges") == 0 ? 2 : 0;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -123,6 +127,10 @@ int kp_ctx_destroy(kp_ctx* c) {
   c->e3pre.release();
   c->fc3.release();
   c->fct3.release();
+  c->e4.release();
+  c->eT.release();
+  c->cvf_fw3.release();
+  c->cvf_bw3.release();
   train_state_free(c);
   for (auto e : c->evpool) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);

@@ -107,6 +107,9 @@ struct kp_ctx {
   bool eT_ready = false;
   DevBuf fc3, fct3;        // ConvE: three-piece bf16 images of the FC weight and its transpose (kp_gemm3.hip)
   bool fc3_ready = false;
+  int cv_fused = 1;        // ConvE d = 200: fused encoder kernels (kp_cv_fused.hpp), KP_CV_FUSED
+  DevBuf cvf_fw3, cvf_bw3;  // their permuted split images of the FC weight (built once)
+  bool cvf_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
   std::vector<hipEvent_t> evpool;

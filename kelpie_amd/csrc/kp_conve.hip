@@ -23,6 +23,7 @@
 
 #include "kp_attn.hpp"
 #include "kp_attn3.hpp"
+#include "kp_cv_fused.hpp"
 
 int cx_pick_db(int dim);
 
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) void kp_cv_dx(int M, CvConst k, const CvInst* 
                                                 const int32_t* __restrict__ tails, const float* __restrict__ E,
                                                 const float* __restrict__ X, const int32_t* __restrict__ bits,
                                                 const float* __restrict__ bna, float* __restrict__ dfc,
-                                                float* __restrict__ gk) {
+                                                float* __restrict__ gk, __bf16* __restrict__ g3) {
   __shared__ float red[4];
   __shared__ float xi[640], xk[640];
   const int i = blockIdx.x;
@@ -187,9 +188,23 @@ __global__ __launch_bounds__(256) void kp_cv_dx(int M, CvConst k, const CvInst* 
     if (d < k.dim) {
       const float nz = k.has_mask ? noise_at(bits, I.mask_off, I.pos * k.dim + d, k.scale) : 1.0f;
       const float relu = xi[d] > 0.f ? 1.0f : 0.0f;
-      dfc[(size_t)i * k.dim + d] = dx * relu * a3[d] * nz;
+      const float v = dx * relu * a3[d] * nz;
+      dfc[(size_t)i * k.dim + d] = v;
+      if (g3) {  // kp_cv_bwd_fused's A operand: [3][M][KB] bf16 pieces
+        __bf16 h, m, l;
+        split3(v, h, m, l);
+        const size_t o = (size_t)i * kpcvf::KB + d, ps = (size_t)M * kpcvf::KB;
+        g3[o] = h;
+        g3[ps + o] = m;
+        g3[2 * ps + o] = l;
+      }
     }
   }
+  if (g3)
+    for (int d = k.dim + tid; d < kpcvf::KB; d += 256) {
+      const size_t o = (size_t)i * kpcvf::KB + d, ps = (size_t)M * kpcvf::KB;
+      g3[o] = g3[ps + o] = g3[2 * ps + o] = (__bf16)0.f;
+    }
 }
 
 // dL/dflat -> ReLU / BN2 -> transposed 3x3 conv -> BN1 -> the lhs half of the image
@@ -402,6 +417,24 @@ void encode_eval(kp_ctx* c, int n, const int2* dsrc, const float* dX, float* dQ)
 
 float* conve_fc_wt(kp_ctx* c);
 
+// kp_cv_fused.hpp's weight images (built once per context; the FC layer is frozen)
+static void conve_fused_images(kp_ctx* c, const __bf16** fw, const __bf16** bw) {
+  if (!c->cvf_ready) {
+    const long long n1 = (long long)kpcvf::NR * kpcvf::HID, n2 = (long long)kpcvf::NBL * kpcvf::KB;
+    __bf16* a = reinterpret_cast<__bf16*>(c->cvf_fw3.ensure(3 * sizeof(__bf16) * (size_t)n1));
+    __bf16* b = reinterpret_cast<__bf16*>(c->cvf_bw3.ensure(3 * sizeof(__bf16) * (size_t)n2));
+    hipLaunchKernelGGL(kpcvf::kp_cv_fwd_image, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, c->stream,
+                       c->d_fc_w, c->dim, a);
+    KP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(kpcvf::kp_cv_bwd_image, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, c->stream,
+                       c->d_fc_w, c->dim, b);
+    KP_HIP(hipGetLastError());
+    c->cvf_ready = true;
+  }
+  *fw = c->cvf_fw3.as<__bf16>();
+  *bw = c->cvf_bw3.as<__bf16>();
+}
+
 void conve_encode_dev(kp_ctx* c, int n, const int2* d_src, float* d_out) { encode_eval(c, n, d_src, nullptr, d_out); }
 
 void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
@@ -558,10 +591,22 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     launch_gemm_abt(c, dflat, c->hidden, nfp, c->d_fc_w, c->hidden, c->dim, c->hidden, dFcf, c->dim, c->d_fc_b, 0, 1);
   }
   // step workspaces
-  const int KS = 8;  // split-K of the FC forward
+  // fused encoder kernels (kp_cv_fused.hpp) for d = 200: the feature map stays on chip
+  const bool fused = c->cv_fused && c->dim == 200 && c->hidden == kpcvf::HID;
+  const int KS = fused ? kpcvf::NSPLIT : 8;  // split-K of the FC forward
   const int mk = std::max(1, max_k);
-  float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)std::max(mk, nfp) * c->hidden));
+  float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)std::max(fused ? 1 : mk, nfp) * c->hidden));
   float* dslab = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * (size_t)KS * mk * c->dim));
+  const __bf16* cvf_fw = nullptr;
+  const __bf16* cvf_bw = nullptr;
+  uint8_t* dRelu = nullptr;
+  __bf16* dG3 = nullptr;
+  if (fused) {
+    conve_fused_images(c, &cvf_fw, &cvf_bw);
+    dRelu = reinterpret_cast<uint8_t*>(c->ws[24].ensure((size_t)mk * kpcvf::MASK_B));
+    dG3 = reinterpret_cast<__bf16*>(c->ws[25].ensure(3 * sizeof(__bf16) * (size_t)mk * kpcvf::KB));
+  }
+  const int n_dl = fused ? kpcvf::NSPLIT : 1;  // lhs image-gradient slabs per pair (kp_cv_bwd_fused, reduced in slab 0)
   float* dQ = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)mk * DP));
   int2* dSrc = reinterpret_cast<int2*>(c->ws[15].ensure(sizeof(int2) * (size_t)std::max<size_t>(1, kinst.size())));
   float* dgs = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)std::max<size_t>(1, kinst.size())));
@@ -598,8 +643,8 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float* dO = reinterpret_cast<float*>(c->ws[17].ensure(sizeof(float) * o_rows * DP));
   float* ddfc = reinterpret_cast<float*>(c->ws[18].ensure(sizeof(float) * (size_t)mk * c->dim));
   float* dgk = reinterpret_cast<float*>(c->ws[19].ensure(sizeof(float) * (size_t)mk));
-  float* ddflat = reinterpret_cast<float*>(c->ws[20].ensure(sizeof(float) * (size_t)mk * c->hidden));
-  float* ddl = reinterpret_cast<float*>(c->ws[21].ensure(sizeof(float) * (size_t)mk * DP));
+  float* ddflat = reinterpret_cast<float*>(c->ws[20].ensure(sizeof(float) * (size_t)(fused ? 1 : mk) * c->hidden));
+  float* ddl = reinterpret_cast<float*>(c->ws[21].ensure(sizeof(float) * (size_t)n_dl * mk * DP));
   float* dWt = conve_fc_wt(c);
   // kp_gemm3_abt stages 8-value chunks: other widths (d = 60 in the goldens) stay on fp32
   const int fcm = (c->dim % 8 == 0 && c->hidden % 8 == 0) ? c->fc_mode : 0;
@@ -624,15 +669,23 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     const CvInst* KI = dKI + kin_off[t];
     if (nk > 0) {
       const int n_split = step_plan[t].wk.n_parts;
-      KP_CONV_FWD(dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
-                         kc, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
-      KP_HIP(hipGetLastError());
-      if (fcm & 1)
-        launch_gemm3_abt(c, dflat, true, c->hidden, nk, conve_fc3(c, false), c->hidden, c->dim, c->hidden, dslab,
-                         c->dim, c->d_fc_b, 0, KS);
-      else
-        launch_gemm_abt(c, dflat, c->hidden, nk, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b, 0,
-                        KS);
+      const int cvf_grid = kpcvf::NSPLIT * ((nk + kpcvf::MT - 1) / kpcvf::MT);
+      if (fused) {
+        hipLaunchKernelGGL(kpcvf::kp_cv_fwd_fused, dim3(cvf_grid), dim3(512), kpcvf::FWD_LDS, c->stream, nk,
+                           dSrc + kin_off[t], c->dE, dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b,
+                           cvf_fw, c->d_fc_b, c->dim, dslab, dRelu);
+        KP_HIP(hipGetLastError());
+      } else {
+        KP_CONV_FWD(dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
+                    kc, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
+        KP_HIP(hipGetLastError());
+        if (fcm & 1)
+          launch_gemm3_abt(c, dflat, true, c->hidden, nk, conve_fc3(c, false), c->hidden, c->dim, c->hidden, dslab,
+                           c->dim, c->d_fc_b, 0, KS);
+        else
+          launch_gemm_abt(c, dflat, c->hidden, nk, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b,
+                          0, KS);
+      }
       hipLaunchKernelGGL(kp_cv_post_fc, dim3(nk), dim3(256), 0, c->stream, nk, dslab, KS, kc, KI, dBits, c->d_bn_a,
                          c->d_bn_b, dQ);
       KP_HIP(hipGetLastError());
@@ -666,18 +719,28 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       }
       ++launches;
       hipLaunchKernelGGL(kp_cv_dx, dim3(nk), dim3(256), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE, dX,
-                         dBits, c->d_bn_a, ddfc, dgk);
+                         dBits, c->d_bn_a, ddfc, dgk, dG3);
       KP_HIP(hipGetLastError());
-      if (fcm & 2) {
+      if (fused) {
+        hipLaunchKernelGGL(kpcvf::kp_cv_bwd_fused, dim3(cvf_grid), dim3(512), kpcvf::BWD_LDS, c->stream, nk, dG3,
+                           cvf_bw, dRelu, c->d_conv_w, c->d_bn_a, DP, ddl);
+        KP_HIP(hipGetLastError());
+        const long long nr = (long long)nk * kpcvf::LR * kpcvf::IW;
+        hipLaunchKernelGGL(kpcvf::kp_cv_dl_reduce, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, c->stream, nk, DP,
+                           ddl);
+        KP_HIP(hipGetLastError());
+      } else if (fcm & 2) {
         split3_rows(c, ddfc, nk, c->dim, c->dim, ddfc3);
         launch_gemm3_abt(c, ddfc3, false, c->dim, nk, conve_fc3(c, true), c->dim, c->hidden, c->dim, ddflat,
                          c->hidden, nullptr, 0, 1);
       } else {
         launch_gemm_abt(c, ddfc, c->dim, nk, dWt, c->dim, c->hidden, c->dim, ddflat, c->hidden, nullptr, 0, 1);
       }
-      hipLaunchKernelGGL(kp_cv_conv_bwd, dim3(nk), dim3(256), shm_cbwd, c->stream, nk, kc, ddflat, dflat, c->d_conv_w,
-                         c->d_bn_a, ddl);
-      KP_HIP(hipGetLastError());
+      if (!fused) {
+        hipLaunchKernelGGL(kp_cv_conv_bwd, dim3(nk), dim3(256), shm_cbwd, c->stream, nk, kc, ddflat, dflat, c->d_conv_w,
+                           c->d_bn_a, ddl);
+        KP_HIP(hipGetLastError());
+      }
     }
     const double step = (double)(t + 1);
     opt.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, step)));

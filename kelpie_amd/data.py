@@ -245,20 +245,55 @@ class KelpieView:
         k, s = self.kelpie_entity, self.original_entity
         rep = Dataset.replace_entity_in_triple
         self.base_triples = [rep(t, s, k) for t in dataset.entity_to_training_triples.get(s, [])]
-        kva = [rep(t, s, k) for t in dataset.entity_to_validation_triples.get(s, [])]
-        kte = [rep(t, s, k) for t in dataset.entity_to_testing_triples.get(s, [])]
-        R = dataset.num_relations
-        # only keys whose head is the kelpie entity can be ranked
-        self.filter = defaultdict(Counter)
-        for a, p, b in self.base_triples + kva + kte:
-            if a == k:
-                self.filter[p][b] += 1
-            if b == k:
-                self.filter[p + R][a] += 1
-        self.index = {t: i for i, t in enumerate(self.base_triples)}
-        self._filter_lists = {}  # rel -> filter_for(rel) without a delta (shared: callers copy or only read)
         self.base_arr = np.asarray(self.base_triples, dtype=np.int32).reshape(-1, 3)
-        self.base_rows = self._rows(self.base_arr)
+        self.n_base_rows = 2 * len(self.base_triples)
+        self._filter = self._index = self._base_rows = self._native = None
+        self._filter_lists = {}  # rel -> filter_for(rel) without a delta (shared: callers copy or only read)
+
+    def _other_triples(self):
+        """The kelpie entity's validation and test triples (they only enter the filters)."""
+        k, s = self.kelpie_entity, self.original_entity
+        rep = Dataset.replace_entity_in_triple
+        ds = self.dataset
+        return ([rep(t, s, k) for t in ds.entity_to_validation_triples.get(s, [])]
+                + [rep(t, s, k) for t in ds.entity_to_testing_triples.get(s, [])])
+
+    @property
+    def filter(self):
+        """rank key (kelpie, p) -> Counter of filtered objects (train + valid + test)."""
+        if self._filter is None:
+            k, R = self.kelpie_entity, self.dataset.num_relations
+            # only keys whose head is the kelpie entity can be ranked
+            f = defaultdict(Counter)
+            for a, p, b in self.base_triples + self._other_triples():
+                if a == k:
+                    f[p][b] += 1
+                if b == k:
+                    f[p + R][a] += 1
+            self._filter = f
+        return self._filter
+
+    @property
+    def index(self):
+        if self._index is None:
+            self._index = {t: i for i, t in enumerate(self.base_triples)}
+        return self._index
+
+    @property
+    def base_rows(self):
+        if self._base_rows is None:
+            self._base_rows = self._rows(self.base_arr)
+        return self._base_rows
+
+    @property
+    def native(self):
+        """This view in the library's host scheduler (kp_view_create, csrc/kp_sched.cpp)."""
+        if self._native is None:
+            from . import _lib
+            extra = np.asarray(self._other_triples(), dtype=np.int32).reshape(-1, 3)
+            self._native = _lib.NativeView(self.kelpie_entity, self.dataset.num_relations, self.original_entity,
+                                           self.base_arr, extra)
+        return self._native
 
     def _rows(self, t):
         """Kelpie rows followed by their inverses (o, p + |R|, s), the optimizers' order

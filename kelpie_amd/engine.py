@@ -42,6 +42,9 @@ class _Slot:
     # False: another rank post-trains this slot (kelpie_amd.distributed); only the
     # generators were advanced past its draws, and x0 / rows / rng / filt may be None
     own: bool = True
+    # rows and filter held by the library's host scheduler instead of rows / filt:
+    # (SchedBatch, its slot index, row count, filter length) (kelpie_amd/_lib.py)
+    native: tuple = None
 
 
 def _contiguous_draws(slots, total):
@@ -128,7 +131,8 @@ class PostTrainingEngine(RelevanceEngine):
         RelevanceEngine.__init__(self, model=model, dataset=dataset)
         self.hp = hp
         self.rng = rng or ReferenceRNG()
-        self._fused = []  # TransE calls whose draws _flush_fused makes in one library call
+        self._fused = []  # TransE calls whose edits and draws _flush_fused makes in two library calls
+        self._sched = None
         self._kp_hp = model.kp_hp(hp)
         if getattr(model, "is_kelpie", False):
             raise Exception("Already a post-trainable KelpieModel.")
@@ -226,69 +230,92 @@ class PostTrainingEngine(RelevanceEngine):
         return len(slots) - 1, pred
 
     def _schedule_fused(self, pred, view, triples, mode, slots, pending_base):
-        """_schedule for TransE: the call's slots are appended now and its draws are
-        queued; :meth:`_flush_fused` makes every queued call's draws in one library call
-        (ReferenceRNG.transe_calls), in order.  The row edit draws nothing, so it runs
-        first; if it raises, the draws the reference makes before raising (everything but
-        the post-trained model's epochs) are consumed, then the error propagates."""
+        """_schedule for TransE: the call's slots are appended now and the call is queued;
+        :meth:`_flush_fused` then makes the edits and rank filters of every queued call in
+        one library call (kp_sched_add_calls, csrc/kp_sched.cpp) and their draws in another
+        (ReferenceRNG.transe_calls), in order.  The edit draws nothing; if it fails, the
+        flush makes the draws the reference makes before raising (everything but the
+        post-trained model's epochs), drops the calls after it, and raises its error."""
         kp = view.as_kelpie_triple(pred)
         need_base = pred not in self.base_pt_results and pred not in pending_base
         sharded = self._sharded()
-        own_base = need_base and (not sharded or self.sharding.claim(max(1, len(view.base_rows))))
-        edit = view.removed if mode == "necessary" else view.added
-        err = None
-        try:
-            if sharded:
-                # another rank's slot needs only the row count (kelpie_amd.distributed)
-                n_pt, _ = edit(triples, rows=False)
-                own_pt = self.sharding.claim(max(1, n_pt))
-                rows, delta = edit(triples) if own_pt else (None, None)
-            else:
-                rows, delta = edit(triples)
-                n_pt, own_pt = len(rows), True
-        except Exception as e:  # noqa: BLE001 -- re-raised below, after the reference's draws
-            err, rows, own_pt = e, None, False
-        call = {"R_base": len(view.base_rows) if need_base else -1, "R_pt": -1 if err else n_pt,
-                "want": (1 if own_base else 0) | (2 if own_pt else 0), "base": None, "pt": None}
+        nb = view.n_base_rows
+        own_base = need_base and (not sharded or self.sharding.claim(max(1, nb)))
+        if sharded:
+            # owners from row counts known before the edit: the base rows +- the rule's
+            # rows (kelpie_amd.distributed); every rank still runs every edit's checks
+            est = nb + 2 * len(triples) if mode == "sufficient" else nb - 2 * len(triples)
+            own_pt = self.sharding.claim(max(1, est))
+        else:
+            own_pt = True
+        base = None
         if need_base:
             pending_base[pred] = len(slots)
-            call["base"] = _Slot(x0=None, rows=view.base_rows, rng=None, pred=kp,
-                                 filt=list(view.filter_for(kp[1])) if own_base else None, own=own_base)
-            slots.append(call["base"])
-        self._fused.append(call)
-        if err is not None:
-            self._flush_fused()
-            raise err
-        call["pt"] = _Slot(x0=None, rows=rows, rng=None, pred=kp,
-                           filt=list(view.filter_for(kp[1], delta.get(kp[1]))) if own_pt else None, own=own_pt)
-        slots.append(call["pt"])
+            base = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_base)
+            slots.append(base)
+        pt = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_pt)
+        slots.append(pt)
+        self._fused.append({"view": view, "kp": kp, "triples": [tuple(int(v) for v in t) for t in triples],
+                            "flags": (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
+                            | (8 if mode == "sufficient" else 0), "base": base, "pt": pt})
         if len(self._fused) >= self._FUSED_FLUSH:
             # hand the draws to the library's workers early: their numpy shuffles then run
-            # while this thread edits the next calls' rows
+            # while this thread queues the next calls
             self._flush_fused()
         return len(slots) - 1, pred
 
     _FUSED_FLUSH = 24  # queued TransE calls per library call
 
+    @staticmethod
+    def _edit_error(call, code, k):
+        """The exception KelpieView.removed / added raise (kelpie_dataset.py:92-158)."""
+        if code == 1:
+            return AssertionError()
+        if code == 2:
+            v = call["view"]
+            o, kel = v.original_entity, v.kelpie_entity
+            t = call["triples"][k]
+            return KeyError((kel if t[0] == o else t[0], t[1], kel if t[2] == o else t[2]))
+        return ValueError("list.remove(x): x not in list")
+
     def _flush_fused(self):
         calls, self._fused = self._fused, []
         if not calls:
             return
+        from . import _lib
         m, hp = self.model, self.hp
-        want = [c["want"] for c in calls] if self._sharded() else None
-        xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, [c["R_base"] for c in calls],
-                                              [c["R_pt"] for c in calls], int(hp["epochs"]),
+        if self._sched is None:
+            self._sched = _lib.SchedBatch()
+        sb = self._sched
+        nviews = [c["view"].native for c in calls]
+        sb.views.extend(nviews)  # its C++ slots point into these views: they live as long as the batch
+        off = np.zeros(len(calls) + 1, np.int32)
+        off[1:] = np.cumsum([len(c["triples"]) for c in calls])
+        idx, rows, nf, (fc, code, k) = sb.add_calls([v.h for v in nviews], [c["kp"][1] for c in calls],
+                                                   [c["flags"] for c in calls], off,
+                                                   [t for c in calls for t in c["triples"]])
+        if fc >= 0:
+            calls = calls[:fc + 1]  # the reference stops at the failing call
+        r_base = [int(rows[i, 0]) if c["flags"] & 1 else -1 for i, c in enumerate(calls)]
+        r_pt = [int(rows[i, 1]) if i != fc else -1 for i in range(len(calls))]
+        want = [(c["flags"] >> 1) & 3 for c in calls] if self._sharded() else None
+        xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, r_base, r_pt, int(hp["epochs"]),
                                               int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1,
                                               want=want)
         for i, c in enumerate(calls):
             db, dp = draws[i]
             if c["base"] is not None:
                 c["base"].x0, c["base"].rng = xb[i], db
-            if c["pt"] is not None:
+                c["base"].native = (sb, int(idx[i, 0]), int(rows[i, 0]), int(nf[i, 0]))
+            if i != fc:
                 c["pt"].x0, c["pt"].rng = xp[i], dp
+                c["pt"].native = (sb, int(idx[i, 1]), int(rows[i, 1]), int(nf[i, 1]))
+        if fc >= 0:
+            raise self._edit_error(calls[fc], code, k)
 
     def _schedule_all(self, items, checkpoints):
         """_schedule_multi, with every queued TransE call's draws made before it returns or raises."""
+        self._sched = None  # this batch's natively assembled slots (TransE), made on first use
         if self._sharded():
             self.sharding.begin_batch()
         try:
@@ -335,11 +362,12 @@ class PostTrainingEngine(RelevanceEngine):
             s.result = {"target_score": float(all_s[i]), "target_rank": int(all_r[i])}
         stats["gather_s"] = time.perf_counter() - t0
 
-    def _run_slots(self, slots, ctx, fill):
-        t_run = time.perf_counter()
+    def _pack(self, slots):
+        """The library call's batch arrays (x0, row_off, rows, rng_off, rng, pred, filt_off, filt)."""
         n = len(slots)
-        D = self.model.dimension
         x0 = np.stack([s.x0 for s in slots]).astype(np.float32)
+        if slots and slots[0].native is not None:
+            return (x0, *self._pack_native(slots))
         row_off = np.zeros(n + 1, np.int32)
         row_off[1:] = np.cumsum([len(s.rows) for s in slots])
         rows = np.concatenate([s.rows.reshape(-1, 3) for s in slots]).astype(np.int32) if row_off[-1] \
@@ -350,16 +378,42 @@ class PostTrainingEngine(RelevanceEngine):
         pred = np.array([s.pred for s in slots], np.int32)
         filt_off = np.zeros(n + 1, np.int32)
         filt_off[1:] = np.cumsum([len(s.filt) for s in slots])
-        filt = np.array([e for s in slots for e in s.filt], np.int32) if filt_off[-1] else np.zeros(1, np.int32)
-        assert x0.shape == (n, D)
+        filt = np.concatenate([np.asarray(s.filt, np.int32) for s in slots]) if filt_off[-1] \
+            else np.zeros(1, np.int32)
+        assert x0.shape == (n, self.model.dimension)
+        return x0, row_off, rows, rng_off, rng, pred, filt_off, filt
+
+    def _pack_native(self, slots):
+        """_pack's rows and filters written by the library's scheduler (kp_sched_pack)."""
+        n = len(slots)
+        nat = [s.native for s in slots]
+        sb = nat[0][0]
+        assert all(t is not None and t[0] is sb for t in nat), "one scheduler batch per device batch"
+        row_off = np.zeros(n + 1, np.int32)
+        row_off[1:] = np.cumsum([t[2] for t in nat])
+        filt_off = np.zeros(n + 1, np.int32)
+        filt_off[1:] = np.cumsum([t[3] for t in nat])
+        rows = np.empty((int(row_off[-1]), 3), np.int32)
+        filt = np.empty(max(1, int(filt_off[-1])), np.int32)
+        sb.pack([t[1] for t in nat], rows, filt)
+        rng_off = np.zeros(n + 1, np.int64)
+        rng_off[1:] = np.cumsum([s.rng.size for s in slots])
+        rng = _contiguous_draws(slots, int(rng_off[-1]))
+        pred = np.array([s.pred for s in slots], np.int32)
+        return row_off, rows, rng_off, rng, pred, filt_off, filt
+
+    def _run_slots(self, slots, ctx, fill):
+        t_run = time.perf_counter()
+        n = len(slots)
+        packed = self._pack(slots)
         t_lib = time.perf_counter()
         ctx = ctx or self.model.ctx
-        score, rank, _ = ctx.posttrain_rank(self._kp_hp, x0, row_off, rows, rng_off, rng, pred, filt_off, filt)
+        score, rank, _ = ctx.posttrain_rank(self._kp_hp, *packed)
         t_end = time.perf_counter()
         if fill:
             for i, s in enumerate(slots):
                 s.result = {"target_score": float(score[i]), "target_rank": int(rank[i])}
-        stats = {"slots": n, "rows": int(row_off[-1]), "pack_s": t_lib - t_run, "lib_s": t_end - t_lib,
+        stats = {"slots": n, "rows": int(packed[1][-1]), "pack_s": t_lib - t_run, "lib_s": t_end - t_lib,
                  **ctx.last_timing()}
         if not fill:
             stats["_score"], stats["_rank"] = np.array(score), np.array(rank)

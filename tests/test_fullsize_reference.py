@@ -85,8 +85,9 @@ def test_fixture_well_formed(path):
     for run in fx["runs"].values():
         assert len(run["rank_deltas"]) == len(fx["candidates"]) * n_conv
         split_results(run, len(fx["candidates"]), n_conv)
-    # the reference's own fp32 / fp64 / reduction-order spread (ConvE YAGO3-10: 5 places)
-    assert spread(fx) <= 8
+    # the reference's own fp32 / fp64 / reduction-order spread (ConvE YAGO3-10: 5 places,
+    # ComplEx DB100K sufficient: 10 places over 99,605 ranked rows)
+    assert spread(fx) <= 16
 
 
 @pytest.mark.gpu

@@ -353,6 +353,57 @@ def test_attention_contractions_agree(model_name, monkeypatch):
         assert a[0] == b[0] and a[2] == b[2], (a, b)
 
 
+def test_conve_fused_encoder_agrees(monkeypatch):
+    """ConvE d = 200: the fused encoder kernels (kp_cv_fused.hpp: conv + FC forward with the
+    feature map on chip, FC^T + transposed conv backward; the default) against the separate
+    kernels (KP_CV_FUSED=0: fp32 conv map through HBM, fp32 MFMA GEMMs) on the same
+    post-trainings (several 128-pair tiles per step, a partial last tile): kelpie rows within
+    2e-5 of their scale, target scores within 1e-5 relative, ranks equal.  The two differ in
+    the FC products (bf16x3 against fp32 MFMA, both exact to fp32 rounding) and in summation
+    order only."""
+    from kelpie_amd import synth
+    g = synth.make_graph("small", seed=5)
+    ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    deg = ds.entity_to_degree
+    test = [tuple(int(v) for v in t) for t in g.test]
+    preds = [t for t in test if 20 <= deg.get(t[0], 0) <= 60][:2]
+    w = synth.make_weights("ConvE", g.num_entities, g.num_relations, 200, seed=5, conve_random_bn=True,
+                           trained_scale=0.5)
+    bn = {i: {"weight": w[f"bn{i}_weight"], "bias": w[f"bn{i}_bias"], "running_mean": w[f"bn{i}_mean"],
+              "running_var": w[f"bn{i}_var"]} for i in (1, 2, 3)}
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("KP_CV_FUSED", mode)
+        model = ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
+                         w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn, hidden_dropout_rate=0.2)
+        seed_all(42)
+        eng = ka.NecessaryPostTrainingEngine(model, ds, dict(CV_HP, epochs=10))
+        res, xs = [], []
+        orig = model.ctx.posttrain_rank
+
+        def pr(*a, **k):
+            k["want_x"] = True
+            s, r, x = orig(*a, **k)
+            xs.append(np.array(x))
+            return s, r, x
+
+        model.ctx.posttrain_rank = pr
+        for pred in preds:
+            eng.set_cache()
+            cands = sorted(ds.entity_to_training_triples[pred[0]])[:8]
+            eng.compute_relevance_batch(pred, [[c] for c in cands])
+            res += [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+                    for pt, b in eng.last_results]
+        out[mode] = (res, np.concatenate(xs))
+    x0, x1 = out["0"][1], out["1"][1]
+    assert x0.shape == x1.shape and x0.shape[0] >= 16
+    assert np.max(np.abs(x1 - x0)) <= 2e-5 * np.max(np.abs(x0)), np.max(np.abs(x1 - x0))
+    for a, b in zip(out["1"][0], out["0"][0]):
+        assert abs(a[1] - b[1]) <= 1e-5 * max(1e-3, abs(b[1])), (a, b)
+        assert abs(a[3] - b[3]) <= 1e-5 * max(1e-3, abs(b[3])), (a, b)
+        assert a[0] == b[0] and a[2] == b[2], (a, b)
+
+
 @pytest.mark.parametrize("part", PARTS)
 def test_complex_sufficient_vs_oracle_full_width(part, monkeypatch):
     """Sufficient mode at the production width (D = 400): every conversion entity's base

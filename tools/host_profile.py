@@ -42,6 +42,15 @@ def main():
         orig_wait()
         waits.append(time.perf_counter() - t)
     krng._lib.rng_wait = timed_wait
+    calls_t = []
+    orig_calls = krng._lib.transe_calls
+
+    def timed_calls(*a, **k):
+        t = time.perf_counter()
+        r = orig_calls(*a, **k)
+        calls_t.append(time.perf_counter() - t)
+        return r
+    krng._lib.transe_calls = timed_calls
 
     def items(ps):
         out = []
@@ -56,6 +65,7 @@ def main():
     for k in range(args.repeats + 1):
         eng.set_cache()
         waits.clear()
+        calls_t.clear()
         prof = cProfile.Profile() if k == args.repeats else None
         t0 = time.perf_counter()
         if prof:
@@ -65,9 +75,12 @@ def main():
         if prof:
             prof.disable()
         dt = time.perf_counter() - t0
-        rows = sum(len(s.rows) for s in slots)
+        rows = sum(s.native[2] if s.native is not None else len(s.rows) for s in slots)
+        t1 = time.perf_counter()
+        eng._pack(slots)
+        dp = time.perf_counter() - t1
         print(f"batch {k}: schedule {dt * 1e3:.2f} ms  final draw wait {sum(waits) * 1e3:.2f} ms  "
-              f"slots {len(slots)}  rows {rows}", flush=True)
+              f"pack {dp * 1e3:.2f} ms  kp_rng_transe_calls {sum(calls_t) * 1e3:.2f} ms  slots {len(slots)}  rows {rows}", flush=True)
     pstats.Stats(prof).sort_stats("tottime").print_stats(16)
 
 
