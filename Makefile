@@ -34,12 +34,12 @@ stamps:
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o kelpie_amd/libkelpie_hip_stamps.so build/stamps/*.o $(patsubst kelpie_amd/csrc/%.cpp,build/%.cpp.o,$(CPP))
 
 # timing-only diagnostic variants (wrong results), never the product library:
-#   make diag DIAG="nos:-DKP_DIAG_NO_S noo:-DKP_DIAG_NO_O nodma:-DKP_ATTN_NODMA"
+#   make diag DIAG="nos:-DKP_DIAG_NO_S noo:-DKP_DIAG_NO_O nodma:-DKP_ATTN_NODMA"  (commas: several defines)
 # builds variants/lib_<name>.so, loaded by tools/attn_phase_ab.sh through KELPIE_HIP_LIB
 DIAG ?= nos:-DKP_DIAG_NO_S noo:-DKP_DIAG_NO_O nodma:-DKP_ATTN_NODMA
 diag: $(patsubst kelpie_amd/csrc/%.cpp,build/%.cpp.o,$(CPP))
 	@mkdir -p variants
-	for v in $(DIAG); do n=$${v%%:*}; d=$${v#*:}; mkdir -p build/diag_$$n; \
+	for v in $(DIAG); do n=$${v%%:*}; d=$$(echo $${v#*:} | tr , ' '); mkdir -p build/diag_$$n; \
 	  for f in $(SRC); do $(HIPCC) $(FLAGS) -DKP_DIAGNOSTIC_BUILD $$d -c $$f -o build/diag_$$n/$$(basename $$f .hip).o || exit 1; done; \
 	  $(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o variants/lib_$$n.so build/diag_$$n/*.o $^ || exit 1; done
 

@@ -267,6 +267,21 @@ int kp_rng_transe_calls(uint8_t* torch_state, size_t torch_len, uint32_t* np_key
                         const int32_t* R_pt, const uint8_t* want, int32_t epochs, int32_t ratio,
                         int64_t n_entities, float* x_base, float* x_pt, int32_t* out);
 
+/* kp_rng_transe_calls with the torch-stream walk on the library's walker thread: returns
+ * at once; x_base, x_pt and out are complete after kp_rng_wait().  The walk starts from
+ * torch_state unless an earlier asynchronous walk still carries the stream (it then
+ * continues that one and torch_state is not read); kp_rng_torch_take hands the stream
+ * back.  Lets the scheduling thread queue calls while the generator is advanced past
+ * their draws (the randint outputs alone are ~22 M words per TransE batch). */
+int kp_rng_transe_calls_async(const uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos,
+                              int32_t normal_cap, int32_t D, int32_t d, float xavier_std, int32_t n,
+                              const int32_t* R_base, const int32_t* R_pt, const uint8_t* want, int32_t epochs,
+                              int32_t ratio, int64_t n_entities, float* x_base, float* x_pt, int32_t* out);
+
+/* Wait for every asynchronous walk; if one carries the torch stream, store it into
+ * torch_state (*taken = 1) and release it, else *taken = 0 and torch_state is untouched. */
+int kp_rng_torch_take(uint8_t* torch_state, size_t torch_len, int32_t* taken);
+
 /* Block until every slot queued by kp_rng_transe_enqueue is written. */
 int kp_rng_wait(void);
 
@@ -361,6 +376,10 @@ int kp_sched_add_calls(kp_sched_batch* b, int32_t n, kp_view* const* views, cons
  * batch slots idx[0 .. n), back to back, into rows[rows_cap] / filt[filt_cap] (int32). */
 int kp_sched_pack(const kp_sched_batch* b, int32_t n, const int32_t* idx, int32_t* rows, int64_t rows_cap,
                   int32_t* filt, int64_t filt_cap);
+
+/* out[...] = the n int32 arrays (address ptrs[i], counts[i] values) back to back (the
+ * slots' draws gathered into one upload buffer without holding the caller's lock). */
+int kp_gather_i32(int32_t n, const uint64_t* ptrs, const int64_t* counts, int32_t* out, int64_t cap);
 
 /* Library version string. */
 const char* kp_version(void);

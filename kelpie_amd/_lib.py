@@ -23,7 +23,8 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
            "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals", "kp_rng_normal",
            "kp_rng_transe_calls", "kp_train_epoch", "kp_read_tables", "kp_view_create", "kp_view_destroy",
-           "kp_sched_batch_create", "kp_sched_batch_destroy", "kp_sched_add_calls", "kp_sched_pack"]
+           "kp_sched_batch_create", "kp_sched_batch_destroy", "kp_sched_add_calls", "kp_sched_pack",
+           "kp_gather_i32", "kp_rng_transe_calls_async", "kp_rng_torch_take"]
 
 
 class ModelDesc(C.Structure):
@@ -110,6 +111,9 @@ def lib():
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_sched_pack.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                     C.c_int64]
+        L.kp_gather_i32.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        L.kp_rng_transe_calls_async.argtypes = L.kp_rng_transe_calls.argtypes
+        L.kp_rng_torch_take.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -206,6 +210,33 @@ def transe_calls(state: np.ndarray, np_key: int, np_pos: int, cap: int, D: int, 
                                     int(D), int(d), float(std), n, _ptr(rb), _ptr(rp), _ptr(w), int(epochs),
                                     int(ratio), int(n_entities), _ptr(xb), _ptr(xp), _ptr(out)))
     return xb, xp
+
+
+def transe_calls_async(state: np.ndarray, np_key: int, np_pos: int, cap: int, D: int, d: int, std: float,
+                       R_base, R_pt, epochs: int, ratio: int, n_entities: int, out: np.ndarray | None,
+                       want: np.ndarray | None = None):
+    """kp_rng_transe_calls_async: :func:`transe_calls` with the torch-stream walk on the
+    library's walker thread, starting from ``state`` unless a walk already carries the
+    stream.  Everything (x_base, x_pt, ``out``) is complete after :func:`rng_wait`; the
+    stream comes back with :func:`torch_take`."""
+    n = len(R_base)
+    rb = np.ascontiguousarray(R_base, dtype=np.int32)
+    rp = np.ascontiguousarray(R_pt, dtype=np.int32)
+    w = None if want is None else np.ascontiguousarray(want, dtype=np.uint8)
+    xb = np.empty((n, d), np.float32)
+    xp = np.empty((n, d), np.float32)
+    check(lib().kp_rng_transe_calls_async(_ptr(state), state.size, C.c_void_p(np_key), C.c_void_p(np_pos), int(cap),
+                                          int(D), int(d), float(std), n, _ptr(rb), _ptr(rp), _ptr(w), int(epochs),
+                                          int(ratio), int(n_entities), _ptr(xb), _ptr(xp), _ptr(out)))
+    return xb, xp
+
+
+def torch_take(state: np.ndarray) -> bool:
+    """Wait for the asynchronous walks and write the torch stream they carry into ``state``
+    (True), or leave ``state`` alone when none carries it (False)."""
+    taken = np.zeros(1, np.int32)
+    check(lib().kp_rng_torch_take(_ptr(state), state.size, _ptr(taken)))
+    return bool(taken[0])
 
 
 def rng_wait():
@@ -424,7 +455,7 @@ class NativeView:
 
     def __del__(self):
         h = getattr(self, "h", None)
-        if h:
+        if h and C is not None:  # not at interpreter shutdown (module globals cleared)
             self._lib.kp_view_destroy(C.c_void_p(h))
             self.h = None
 
@@ -443,7 +474,7 @@ class SchedBatch:
 
     def __del__(self):
         h = getattr(self, "h", None)
-        if h:
+        if h and C is not None:  # not at interpreter shutdown (module globals cleared)
             self._lib.kp_sched_batch_destroy(C.c_void_p(h))
             self.h = None
 
@@ -470,3 +501,14 @@ class SchedBatch:
         assert rows.dtype == np.int32 and rows.flags.c_contiguous and filt.dtype == np.int32
         check(self._lib.kp_sched_pack(C.c_void_p(self.h), len(i), _ptr(i), _ptr(rows), rows.size, _ptr(filt),
                                       filt.size))
+
+
+def gather_i32(arrays, out: np.ndarray) -> np.ndarray:
+    """``out[:total]`` = the int32 arrays back to back, copied by the library (kp_gather_i32:
+    the interpreter lock is released for the copy)."""
+    ptrs = np.array([a.__array_interface__["data"][0] for a in arrays], dtype=np.uint64)
+    cnt = np.array([a.size for a in arrays], dtype=np.int64)
+    assert out.dtype == np.int32 and out.flags.c_contiguous
+    assert all(a.dtype.itemsize == 4 and (a.size == 0 or a.flags.c_contiguous) for a in arrays)
+    check(lib().kp_gather_i32(len(arrays), _ptr(ptrs), _ptr(cnt), _ptr(out), out.size))
+    return out[:int(cnt.sum())]

@@ -2,7 +2,7 @@
 // shared by the ComplEx (softmax cross-entropy) and ConvE (sigmoid BCE)
 // post-training steps.
 #pragma once
-#if defined(KP_ATTN_NODMA) && !defined(KP_DIAGNOSTIC_BUILD)
+#if (defined(KP_ATTN_NODMA) || defined(KP_DIAG_M0SAVE)) && !defined(KP_DIAGNOSTIC_BUILD)
 #error "KP_ATTN_NODMA is a timing-only diagnostic (wrong results): build it with make diag"
 #endif
 #include <algorithm>
@@ -59,7 +59,16 @@ __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
   if constexpr (BUILTIN) {
     __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(uintptr_t)lds_base, 16, 0, 0);
   } else {
+#ifdef KP_DIAG_M0SAVE
+    // diagnostic: M0 saved and restored around the DMA (the compiler's M0 preserved)
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(lds_base), "v"(gp)
+                 : "memory");
+#else
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
+#endif
   }
 }
 

@@ -61,7 +61,8 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 // KP_DIAGNOSTIC_BUILD, which `make diag` sets for the variants/ libraries; the product
 // library can never carry one by a stray define.
 #if (defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O) || defined(KP_ATTN_NODMA) || defined(KP_DIAG_DMA_LGKM0) || \
-     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4)) && !defined(KP_DIAGNOSTIC_BUILD)
+     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE)) && \
+    !defined(KP_DIAGNOSTIC_BUILD)
 #error "kp_attn3 diagnostic define without KP_DIAGNOSTIC_BUILD (these builds compute wrong results: make diag)"
 #endif
 // KP_DMA_SPREAD: the next tile's LDS-DMA goes out one piece per O block instead of one
@@ -632,6 +633,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                 issue_piece(tn, (t + 1) & 1, m);
 #ifdef KP_DIAG_DMA_LGKM0
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // diagnostic: drain after each piece
+#endif
+#ifdef KP_DIAG_DMA_VM0
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: each piece lands before what follows
 #endif
               }
               if (m == DB - 1)

@@ -653,6 +653,138 @@ int te_enqueue(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_
   return KP_OK;
 }
 
+// The torch-stream walk of kp_rng_transe_calls_async on a thread of its own: tasks run in
+// submission order on one TorchMt carried from task to task (loaded from the caller's
+// state by the first task after a kp_rng_torch_take, handed back by the next take), so the
+// scheduling thread only queues.  The walk itself queues the numpy shuffles and randint
+// fills on the DrawQueue, in order.
+class TorchWalker {
+ public:
+  static TorchWalker& get() {
+    static TorchWalker* w = new TorchWalker();  // never destroyed: the thread is detached
+    return *w;
+  }
+  // false: no thread (the caller runs the task inline on the carried / loaded state)
+  bool submit(const uint8_t* ts, std::function<int(TorchMt&)> task) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!ensure_locked()) return false;
+    if (!carried_) {
+      mt_.load(ts);
+      carried_ = true;
+    }
+    q_.push_back(std::move(task));
+    ++pending_;
+    cv_work_.notify_all();
+    return true;
+  }
+  // wait for every queued walk; then, if a walk carries the stream, store it into ts and
+  // release it (*taken = 1)
+  int take(uint8_t* ts, int32_t* taken) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_done_.wait(lk, [this] { return pending_ == 0; });
+    if (taken) *taken = 0;
+    if (carried_ && ts) {
+      mt_.store(ts);
+      carried_ = false;
+      if (taken) *taken = 1;
+    }
+    const int rc = fail_rc_;
+    fail_rc_ = KP_OK;
+    return rc;
+  }
+  int wait() { return take(nullptr, nullptr); }
+
+ private:
+  bool ensure_locked() {
+    const pid_t me = getpid();
+    if (pid_ == me) return true;
+    q_.clear();
+    pending_ = 0;
+    carried_ = false;
+    try {
+      std::thread([this] { loop(); }).detach();
+    } catch (...) {
+      return false;
+    }
+    pid_ = me;
+    return true;
+  }
+  void loop() {
+    const pid_t me = getpid();
+    for (;;) {
+      std::function<int(TorchMt&)> t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_work_.wait(lk, [&] { return !q_.empty(); });
+        if (pid_ != me) return;
+        t = std::move(q_.front());
+        q_.pop_front();
+      }
+      int rc;
+      try {
+        rc = t(mt_);  // mt_ is only touched here and under mu_ with the queue empty
+      } catch (const std::invalid_argument&) {
+        rc = KP_EINVAL;
+      } catch (...) {
+        rc = KP_ENOMEM;
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      if (rc != KP_OK && fail_rc_ == KP_OK) fail_rc_ = rc;
+      if (--pending_ == 0) cv_done_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_work_, cv_done_;
+  std::deque<std::function<int(TorchMt&)>> q_;
+  int64_t pending_ = 0;
+  int fail_rc_ = KP_OK;
+  bool carried_ = false;
+  TorchMt mt_;
+  pid_t pid_ = 0;
+};
+
+// every draw of n TransE compute_relevance calls from the torch stream `mt` (see
+// kp_rng_transe_calls)
+int transe_calls_walk(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t cap, int32_t D, int32_t d,
+                      float xavier_std, int32_t n, const int32_t* R_base, const int32_t* R_pt, const uint8_t* want,
+                      int32_t epochs, int32_t ratio, uint32_t nent, float* x_base, float* x_pt, int32_t* out) {
+  int32_t* o = out;
+  for (int32_t i = 0; i < n; ++i) {
+    mt.skip((uint64_t)D);  // torch.rand(1, D): one output per element, values unused
+    const int w = want ? want[i] : 3;  // bit 0: base draws wanted here, bit 1: the pt draws
+    normal_draw(mt, d, 0.0f, xavier_std, cap, x_base + (size_t)i * d);  // base KelpieTransE's xavier_normal_
+    if (R_base[i] >= 0) {
+      const int rc = te_enqueue(mt, np_key, np_pos, R_base[i], epochs, ratio, nent, (w & 1) ? o : nullptr);
+      if (rc != KP_OK) return rc;
+      if (w & 1) o += (size_t)epochs * 3 * R_base[i];
+    }
+    normal_draw(mt, d, 0.0f, xavier_std, cap, x_pt + (size_t)i * d);  // the post-trained one's
+    if (R_pt[i] >= 0) {
+      const int rc = te_enqueue(mt, np_key, np_pos, R_pt[i], epochs, ratio, nent, (w & 2) ? o : nullptr);
+      if (rc != KP_OK) return rc;
+      if (w & 2) o += (size_t)epochs * 3 * R_pt[i];
+    }
+  }
+  return KP_OK;
+}
+
+int transe_calls_check(size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t cap, int32_t D, int32_t d, int32_t n,
+                       const int32_t* R_base, const int32_t* R_pt, const uint8_t* want, int32_t epochs, int32_t ratio,
+                       int64_t n_entities, float* x_base, float* x_pt, int32_t* out) {
+  if (tlen < 24 + kN * 8 || !np_key || !np_pos || (cap != 0 && cap != 1) || D < 0 || d < 16 || n < 0 ||
+      (n > 0 && (!R_base || !R_pt || !x_base || !x_pt)) || epochs < 0 || ratio < 1 || n_entities < 1 ||
+      n_entities >= (1LL << 32))
+    return KP_EINVAL;
+  int64_t words = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if (R_base[i] < -1 || R_pt[i] < -1) return KP_EINVAL;
+    const int w = want ? want[i] : 3;
+    words += (int64_t)epochs * 3 * ((w & 1 ? std::max(R_base[i], 0) : 0) + (w & 2 ? std::max(R_pt[i], 0) : 0));
+  }
+  if (words > 0 && !out) return KP_EINVAL;
+  return KP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -713,38 +845,20 @@ int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_
                         int32_t d, float xavier_std, int32_t n, const int32_t* R_base, const int32_t* R_pt,
                         const uint8_t* want, int32_t epochs, int32_t ratio, int64_t n_entities, float* x_base,
                         float* x_pt, int32_t* out) {
-  if (!ts || tlen < 24 + kN * 8 || !np_key || !np_pos || (cap != 0 && cap != 1) || D < 0 || d < 16 || n < 0 ||
-      (n > 0 && (!R_base || !R_pt || !x_base || !x_pt)) || epochs < 0 || ratio < 1 || n_entities < 1 ||
-      n_entities >= (1LL << 32))
-    return KP_EINVAL;
-  int64_t words = 0;
-  for (int32_t i = 0; i < n; ++i) {
-    if (R_base[i] < -1 || R_pt[i] < -1) return KP_EINVAL;
-    const int w = want ? want[i] : 3;
-    words += (int64_t)epochs * 3 * ((w & 1 ? std::max(R_base[i], 0) : 0) + (w & 2 ? std::max(R_pt[i], 0) : 0));
-  }
-  if (words > 0 && !out) return KP_EINVAL;
+  if (!ts) return KP_EINVAL;
+  int rc = transe_calls_check(tlen, np_key, np_pos, cap, D, d, n, R_base, R_pt, want, epochs, ratio, n_entities,
+                              x_base, x_pt, out);
+  if (rc != KP_OK) return rc;
   try {
+    // a stream still carried by an asynchronous walk continues from where it ends
+    int32_t taken = 0;
+    rc = TorchWalker::get().take(ts, &taken);
+    if (rc != KP_OK) return rc;
     TorchMt mt;
     mt.load(ts);
-    const uint32_t nent = (uint32_t)n_entities;
-    int32_t* o = out;
-    for (int32_t i = 0; i < n; ++i) {
-      mt.skip((uint64_t)D);  // torch.rand(1, D): one output per element, values unused
-      const int w = want ? want[i] : 3;  // bit 0: base draws wanted here, bit 1: the pt draws
-      normal_draw(mt, d, 0.0f, xavier_std, cap, x_base + (size_t)i * d);  // base KelpieTransE's xavier_normal_
-      if (R_base[i] >= 0) {
-        const int rc = te_enqueue(mt, np_key, np_pos, R_base[i], epochs, ratio, nent, (w & 1) ? o : nullptr);
-        if (rc != KP_OK) return rc;
-        if (w & 1) o += (size_t)epochs * 3 * R_base[i];
-      }
-      normal_draw(mt, d, 0.0f, xavier_std, cap, x_pt + (size_t)i * d);  // the post-trained one's
-      if (R_pt[i] >= 0) {
-        const int rc = te_enqueue(mt, np_key, np_pos, R_pt[i], epochs, ratio, nent, (w & 2) ? o : nullptr);
-        if (rc != KP_OK) return rc;
-        if (w & 2) o += (size_t)epochs * 3 * R_pt[i];
-      }
-    }
+    rc = transe_calls_walk(mt, np_key, np_pos, cap, D, d, xavier_std, n, R_base, R_pt, want, epochs, ratio,
+                           (uint32_t)n_entities, x_base, x_pt, out);
+    if (rc != KP_OK) return rc;
     mt.store(ts);
   } catch (const std::invalid_argument&) {
     return KP_EINVAL;
@@ -752,6 +866,42 @@ int kp_rng_transe_calls(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_
     return KP_ENOMEM;
   }
   return KP_OK;
+}
+
+int kp_rng_transe_calls_async(const uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np_pos, int32_t cap,
+                              int32_t D, int32_t d, float xavier_std, int32_t n, const int32_t* R_base,
+                              const int32_t* R_pt, const uint8_t* want, int32_t epochs, int32_t ratio,
+                              int64_t n_entities, float* x_base, float* x_pt, int32_t* out) {
+  if (!ts) return KP_EINVAL;
+  const int rc = transe_calls_check(tlen, np_key, np_pos, cap, D, d, n, R_base, R_pt, want, epochs, ratio,
+                                    n_entities, x_base, x_pt, out);
+  if (rc != KP_OK) return rc;
+  try {
+    std::vector<int32_t> rb(R_base, R_base + n), rp(R_pt, R_pt + n);
+    std::vector<uint8_t> wv;
+    if (want) wv.assign(want, want + n);
+    const uint32_t nent = (uint32_t)n_entities;
+    auto task = [=](TorchMt& mt) {
+      return transe_calls_walk(mt, np_key, np_pos, cap, D, d, xavier_std, n, rb.data(), rp.data(),
+                               wv.empty() ? nullptr : wv.data(), epochs, ratio, nent, x_base, x_pt, out);
+    };
+    if (!TorchWalker::get().submit(ts, task)) {
+      // no walker thread: walk here (the caller's state is current: nothing is carried)
+      TorchMt mt;
+      mt.load(ts);
+      const int r2 = task(mt);
+      if (r2 != KP_OK) return r2;
+      mt.store(const_cast<uint8_t*>(ts));
+    }
+  } catch (...) {
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+int kp_rng_torch_take(uint8_t* ts, size_t tlen, int32_t* taken) {
+  if (!ts || tlen < 24 + kN * 8 || !taken) return KP_EINVAL;
+  return TorchWalker::get().take(ts, taken);
 }
 
 int kp_rng_conve_masks_enqueue(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim,
@@ -791,7 +941,12 @@ int kp_rng_conve_masks_enqueue(uint8_t* ts, size_t tlen, int32_t n_steps, const 
   return KP_OK;
 }
 
-int kp_rng_wait(void) { return DrawQueue::get().wait(); }
+int kp_rng_wait(void) {
+  // the torch walks queue draws: they finish first
+  const int rw = TorchWalker::get().wait();
+  const int rd = DrawQueue::get().wait();
+  return rw != KP_OK ? rw : rd;
+}
 
 int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim, double keep,
                        uint32_t* out) {

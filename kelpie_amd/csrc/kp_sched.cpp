@@ -288,4 +288,15 @@ int kp_sched_pack(const kp_sched_batch* b, int32_t n, const int32_t* idx, int32_
   return KP_OK;
 }
 
+int kp_gather_i32(int32_t n, const uint64_t* ptrs, const int64_t* counts, int32_t* out, int64_t cap) {
+  if (n < 0 || (n > 0 && (!ptrs || !counts)) || cap < 0) return KP_EINVAL;
+  int64_t o = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if (counts[i] < 0 || o + counts[i] > cap || (counts[i] > 0 && !ptrs[i])) return KP_EINVAL;
+    if (counts[i]) std::memcpy(out + o, reinterpret_cast<const int32_t*>(ptrs[i]), sizeof(int32_t) * counts[i]);
+    o += counts[i];
+  }
+  return KP_OK;
+}
+
 }  // extern "C"

@@ -47,14 +47,25 @@ class _Slot:
     native: tuple = None
 
 
-def _contiguous_draws(slots, total):
-    """The slots' draws as one fresh int32 array.  Handing the library a view of the
-    deferred draw arena instead (no copy) measured slower end to end: its upload from
-    the arena's pages, first touched by the RNG worker threads, took 10-20 ms per TransE
-    batch against 3 ms after this copy (profiles/r02zd_transe_draws_upload.txt)."""
+def _contiguous_draws(slots, total, ctx=None):
+    """The slots' draws as one int32 array.  Handing the library a view of the deferred
+    draw arena instead (no copy) measured slower end to end: its upload from the arena's
+    pages, first touched by the RNG worker threads, took 10-20 ms per TransE batch against
+    3 ms after this copy (profiles/r02zd_transe_draws_upload.txt).  The copy goes into a
+    buffer kept with the device context ``ctx`` (no fresh pages per batch; the context's
+    previous batch is done with it) and runs in the library without the interpreter lock,
+    so the next batch's scheduling thread is not held up."""
     if total == 0:
         return np.zeros(1, np.int32)
-    return np.concatenate([s.rng.reshape(-1) for s in slots]).astype(np.int32, copy=False)
+    arrays = [s.rng.reshape(-1) for s in slots]
+    if ctx is None or any(a.dtype.itemsize != 4 for a in arrays):
+        return np.concatenate(arrays).astype(np.int32, copy=False)
+    from . import _lib
+    buf = getattr(ctx, "_draw_buf", None)
+    if buf is None or buf.size < total:
+        buf = np.empty(int(total * 1.25) + 1024, np.int32)
+        ctx._draw_buf = buf
+    return _lib.gather_i32([np.ascontiguousarray(a) for a in arrays], buf)
 
 
 class RelevanceEngine:
@@ -362,19 +373,19 @@ class PostTrainingEngine(RelevanceEngine):
             s.result = {"target_score": float(all_s[i]), "target_rank": int(all_r[i])}
         stats["gather_s"] = time.perf_counter() - t0
 
-    def _pack(self, slots):
+    def _pack(self, slots, ctx=None):
         """The library call's batch arrays (x0, row_off, rows, rng_off, rng, pred, filt_off, filt)."""
         n = len(slots)
         x0 = np.stack([s.x0 for s in slots]).astype(np.float32)
         if slots and slots[0].native is not None:
-            return (x0, *self._pack_native(slots))
+            return (x0, *self._pack_native(slots, ctx))
         row_off = np.zeros(n + 1, np.int32)
         row_off[1:] = np.cumsum([len(s.rows) for s in slots])
         rows = np.concatenate([s.rows.reshape(-1, 3) for s in slots]).astype(np.int32) if row_off[-1] \
             else np.zeros((0, 3), np.int32)
         rng_off = np.zeros(n + 1, np.int64)
         rng_off[1:] = np.cumsum([s.rng.size for s in slots])
-        rng = _contiguous_draws(slots, int(rng_off[-1]))
+        rng = _contiguous_draws(slots, int(rng_off[-1]), ctx)
         pred = np.array([s.pred for s in slots], np.int32)
         filt_off = np.zeros(n + 1, np.int32)
         filt_off[1:] = np.cumsum([len(s.filt) for s in slots])
@@ -383,7 +394,7 @@ class PostTrainingEngine(RelevanceEngine):
         assert x0.shape == (n, self.model.dimension)
         return x0, row_off, rows, rng_off, rng, pred, filt_off, filt
 
-    def _pack_native(self, slots):
+    def _pack_native(self, slots, ctx=None):
         """_pack's rows and filters written by the library's scheduler (kp_sched_pack)."""
         n = len(slots)
         nat = [s.native for s in slots]
@@ -398,16 +409,16 @@ class PostTrainingEngine(RelevanceEngine):
         sb.pack([t[1] for t in nat], rows, filt)
         rng_off = np.zeros(n + 1, np.int64)
         rng_off[1:] = np.cumsum([s.rng.size for s in slots])
-        rng = _contiguous_draws(slots, int(rng_off[-1]))
+        rng = _contiguous_draws(slots, int(rng_off[-1]), ctx)
         pred = np.array([s.pred for s in slots], np.int32)
         return row_off, rows, rng_off, rng, pred, filt_off, filt
 
     def _run_slots(self, slots, ctx, fill):
         t_run = time.perf_counter()
         n = len(slots)
-        packed = self._pack(slots)
-        t_lib = time.perf_counter()
         ctx = ctx or self.model.ctx
+        packed = self._pack(slots, ctx)
+        t_lib = time.perf_counter()
         score, rank, _ = ctx.posttrain_rank(self._kp_hp, *packed)
         t_end = time.perf_counter()
         if fill:

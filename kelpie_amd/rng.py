@@ -46,6 +46,20 @@ def _set_state(st):
     torch.set_rng_state(torch.from_numpy(st))
 
 
+_STATE_LEN = None
+
+# KP_RNG_ASYNC=0: the TransE torch-stream walk on the scheduling thread (A/B switch)
+_ASYNC = __import__('os').environ.get('KP_RNG_ASYNC', '1') != '0'
+
+
+def _state_shape():
+    """A buffer shaped like torch's generator state (for calls that do not read it)."""
+    global _STATE_LEN
+    if _STATE_LEN is None:
+        _STATE_LEN = torch.get_rng_state().numel()
+    return np.zeros(_STATE_LEN, np.uint8)
+
+
 def _np_mt_state_address() -> int:
     """Address of the global RandomState's ``mt19937_state`` (numpy/random/src/mt19937/mt19937.h)."""
     return int(np.random.mtrand._rand._bit_generator.ctypes.state_address)
@@ -68,8 +82,24 @@ _inflight = []
 _skip = 0
 
 
+# True while a library walk (kp_rng_transe_calls_async) carries the torch stream: torch's
+# own state is stale until _torch_current() takes the stream back
+_torch_async = False
+
+
+def _torch_current():
+    """Make torch's generator current: take the stream back from an asynchronous walk."""
+    global _torch_async
+    if _torch_async:
+        _torch_async = False
+        st = torch.get_rng_state().numpy()
+        _lib.torch_take(st)
+        _set_state(st)
+
+
 def _flush_skip():
     global _skip
+    _torch_current()
     if _skip:
         n, _skip = _skip, 0
         st = _get_state()
@@ -85,7 +115,7 @@ def sync():
         _outstanding = False
         _lib.rng_wait()
     _inflight.clear()
-    _flush_skip()
+    _flush_skip()  # also takes the torch stream back from an asynchronous walk
 
 
 class ReferenceRNG:
@@ -195,24 +225,40 @@ class ReferenceRNG:
         are complete on leaving :meth:`deferred` (or at once outside it).  ``want[i]``
         (bit 0 base, bit 1 pt; default all): an unwanted post-training's draws are not
         made, only the generators advance past them (its entry is an empty array)."""
-        global _outstanding
-        _flush_skip()
-        st = _get_state()
+        global _outstanding, _torch_async
         addr = _np_mt_state_address()
-        if not self._defer_depth:
-            sync()
         w = [3] * len(R_base) if want is None else list(want)
         sizes = [(epochs * 3 * max(rb, 0) if wi & 1 else 0, epochs * 3 * max(rp, 0) if wi & 2 else 0)
                  for rb, rp, wi in zip(R_base, R_pt, w)]
         total = sum(a + b for a, b in sizes)
-        out = (self._take(total) if self._defer_depth else np.empty(total, np.int32)) if total else None
-        xb, xp = _lib.transe_calls(st, addr, addr + 4 * 624, _lib.normal_cap(), D, d,
-                                   float(np.float32(math.sqrt(2.0 / float(d + 1)))), R_base, R_pt, epochs, ratio,
-                                   n_entities, out, None if want is None else np.array(w, np.uint8))
-        _outstanding = True
-        if not self._defer_depth:
-            sync()
-        _set_state(st)
+        std = float(np.float32(math.sqrt(2.0 / float(d + 1))))
+        wa = None if want is None else np.array(w, np.uint8)
+        if self._defer_depth and _ASYNC:
+            # the torch-stream walk runs on the library's walker thread; a walk already
+            # carrying the stream continues it (the state passed is then not read)
+            if _skip or not _torch_async:
+                _flush_skip()
+                st = _get_state()
+            else:
+                st = _state_shape()
+            out = self._take(total) if total else None
+            xb, xp = _lib.transe_calls_async(st, addr, addr + 4 * 624, _lib.normal_cap(), D, d, std, R_base, R_pt,
+                                             epochs, ratio, n_entities, out, wa)
+            _inflight.extend((xb, xp))  # the walk writes them until sync(), wanted or not
+            _torch_async = True
+            _outstanding = True
+        else:
+            _flush_skip()
+            if not self._defer_depth:
+                sync()
+            st = _get_state()
+            out = (self._take(total) if self._defer_depth else np.empty(total, np.int32)) if total else None
+            xb, xp = _lib.transe_calls(st, addr, addr + 4 * 624, _lib.normal_cap(), D, d, std, R_base, R_pt, epochs,
+                                       ratio, n_entities, out, wa)
+            _outstanding = True
+            if not self._defer_depth:
+                sync()
+            _set_state(st)
         draws, off, empty = [], 0, np.zeros(0, np.int32)
         for a, b in sizes:
             draws.append((out[off:off + a] if a else empty, out[off + a:off + a + b] if b else empty))

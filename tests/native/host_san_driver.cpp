@@ -173,6 +173,38 @@ int main(int argc, char** argv) {
   ok(kp_graph_dijkstra_pairs(g, (int32_t)ds.size(), ds.data(), dd.data(), w.data()), "dijkstra");
   put(w);
   kp_graph_destroy(g);
+
+  // 6. the asynchronous torch walk (kp_rng_transe_calls_async, two chained calls, then
+  //    kp_rng_wait + kp_rng_torch_take) against the synchronous call on copies of the same
+  //    generator states: identical draws, rows and end states (checked here, nothing written)
+  {
+    std::vector<uint8_t> tsA = ts, tsB = ts, dummy(ts.size(), 0);
+    std::vector<uint32_t> keyA = key, keyB = key;
+    int32_t posA = pos, posB = pos;
+    std::vector<int32_t> oA(tot + 1), oB(tot + 1);
+    std::vector<float> xbA(xb.size()), xpA(xp.size()), xbB(xb.size()), xpB(xp.size());
+    ok(kp_rng_transe_calls(tsA.data(), tsA.size(), keyA.data(), &posA, 1, 32, 32, 0.2425f, n_calls, rb.data(),
+                           rp.data(), nullptr, 4, 5, 14542, xbA.data(), xpA.data(), oA.data()),
+       "transe_calls (sync reference)");
+    ok(kp_rng_wait(), "wait");
+    const int h = n_calls / 2;
+    size_t off1 = 0;
+    for (int i = 0; i < h; ++i) off1 += (size_t)4 * 3 * ((rb[i] > 0 ? rb[i] : 0) + (rp[i] > 0 ? rp[i] : 0));
+    ok(kp_rng_transe_calls_async(tsB.data(), tsB.size(), keyB.data(), &posB, 1, 32, 32, 0.2425f, h, rb.data(),
+                                 rp.data(), nullptr, 4, 5, 14542, xbB.data(), xpB.data(), oB.data()),
+       "transe_calls_async 1");
+    ok(kp_rng_transe_calls_async(dummy.data(), dummy.size(), keyB.data(), &posB, 1, 32, 32, 0.2425f, n_calls - h,
+                                 rb.data() + h, rp.data() + h, nullptr, 4, 5, 14542, xbB.data() + (size_t)h * 32,
+                                 xpB.data() + (size_t)h * 32, oB.data() + off1),
+       "transe_calls_async 2");
+    ok(kp_rng_wait(), "wait");
+    int32_t taken = 0;
+    ok(kp_rng_torch_take(tsB.data(), tsB.size(), &taken), "torch_take");
+    if (!taken || tsA != tsB || keyA != keyB || posA != posB || oA != oB || xbA != xbB || xpA != xpB) {
+      std::fprintf(stderr, "asynchronous walk differs from the synchronous one\n");
+      return 1;
+    }
+  }
   std::fclose(g_out);
   return 0;
 }
