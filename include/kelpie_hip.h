@@ -187,6 +187,28 @@ int kp_train_epoch(kp_ctx* ctx, const kp_hp* hp, int32_t n, const int32_t* tripl
  * (the trained model's state_dict tensors). */
 int kp_read_tables(kp_ctx* ctx, float* entity, float* relation);
 
+/* ConvE full-model training (BCEOptimizer.train, bce_optimizer.py:45-150, on ConvE.forward
+ * in train mode, conve.py:133-158), for verification's retraining
+ * (verify_explanations.py:141-143): the context's tables, conv and FC layers are the
+ * starting point and are trained in place; kp_conve_train_begin adds the three batch
+ * norms' affine parameters and running statistics (1 + 32 + dim values each: BN1, BN2,
+ * BN3) and resets Adam's state.  One kp_conve_train_step = one optimizer step on a batch
+ * of B (head, relation) pairs: tails of pair b = tails[tail_off[b] .. tail_off[b+1])
+ * (the er_vocab targets); in_noise [B][40 h], fm_noise [B][32], hid_noise [B][dim]: the
+ * dropouts' multipliers (0 or 1 / (1 - p), drawn by the caller from the torch generator
+ * in the forward's order; null = no dropout); lr = the epoch's learning rate
+ * (ExponentialLR); bn_train = 0 runs the batch norms in eval mode (a one-pair batch).
+ * Adam with torch's defaults on every parameter.  kp_conve_train_read copies the trained
+ * layers back (the tables: kp_read_tables).  The context's eval-mode batch norm is not
+ * updated: build a new context from the trained parameters to score with them. */
+int kp_conve_train_begin(kp_ctx* ctx, const float* bn_weight, const float* bn_bias, const float* bn_mean,
+                         const float* bn_var);
+int kp_conve_train_step(kp_ctx* ctx, int32_t B, const int32_t* pairs, const int32_t* tail_off, const int32_t* tails,
+                        const float* in_noise, const float* fm_noise, const float* hid_noise, float lr,
+                        float label_smoothing, int32_t bn_train);
+int kp_conve_train_read(kp_ctx* ctx, float* conv_w, float* conv_b, float* fc_w, float* fc_b, float* bn_weight,
+                        float* bn_bias, float* bn_mean, float* bn_var);
+
 /* Data-poisoning relevance, ComplEx (src/relevance_engines/data_poisoning_engine.py:
  * DPEngine.get_gradient :21-49, NecessaryDPEngine.compute_relevance :52-94,
  * SufficientDPEngine.compute_individual_relevance :97-137; the other models have no

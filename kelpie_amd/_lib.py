@@ -24,7 +24,8 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals", "kp_rng_normal",
            "kp_rng_transe_calls", "kp_train_epoch", "kp_read_tables", "kp_view_create", "kp_view_destroy",
            "kp_sched_batch_create", "kp_sched_batch_destroy", "kp_sched_add_calls", "kp_sched_pack",
-           "kp_gather_i32", "kp_rng_transe_calls_async", "kp_rng_torch_take"]
+           "kp_gather_i32", "kp_rng_transe_calls_async", "kp_rng_torch_take", "kp_conve_train_begin",
+           "kp_conve_train_step", "kp_conve_train_read"]
 
 
 class ModelDesc(C.Structure):
@@ -114,6 +115,10 @@ def lib():
         L.kp_gather_i32.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
         L.kp_rng_transe_calls_async.argtypes = L.kp_rng_transe_calls.argtypes
         L.kp_rng_torch_take.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+        L.kp_conve_train_begin.argtypes = [C.c_void_p] * 5
+        L.kp_conve_train_step.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6 + [C.c_float, C.c_float,
+                                                                                      C.c_int32]
+        L.kp_conve_train_read.argtypes = [C.c_void_p] * 9
         _LIB = L
     return _LIB
 
@@ -354,6 +359,34 @@ class Context:
         pm = np.ascontiguousarray(aux, dtype=np.int32)
         assert len(pm) == len(t)
         check(lib().kp_train_epoch(self.h, C.byref(hp), len(t), _ptr(t), _ptr(pm), int(epoch)), self.h)
+
+    def conve_train_begin(self, bn_w, bn_b, bn_m, bn_v):
+        """kp_conve_train_begin: batch-norm parameters and running statistics (1 + 32 + dim each)."""
+        a = [np.ascontiguousarray(v, dtype=np.float32).reshape(-1) for v in (bn_w, bn_b, bn_m, bn_v)]
+        assert all(len(v) == 33 + self.dim for v in a)
+        check(lib().kp_conve_train_begin(self.h, *[_ptr(v) for v in a]), self.h)
+
+    def conve_train_step(self, pairs, tail_off, tails, in_noise, fm_noise, hid_noise, lr, label_smoothing,
+                         bn_train):
+        """kp_conve_train_step: one BCEOptimizer step on the batch ``pairs`` [B][2]."""
+        pr = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1, 2))
+        to = np.ascontiguousarray(tail_off, dtype=np.int32)
+        tl = np.ascontiguousarray(tails, dtype=np.int32) if len(tails) else np.zeros(1, np.int32)
+        nz = [None if v is None else np.ascontiguousarray(v, dtype=np.float32) for v in (in_noise, fm_noise, hid_noise)]
+        check(lib().kp_conve_train_step(self.h, len(pr), _ptr(pr), _ptr(to), _ptr(tl), *[_ptr(v) for v in nz],
+                                        float(lr), float(label_smoothing), int(bool(bn_train))), self.h)
+
+    def conve_train_read(self):
+        """kp_conve_train_read: the trained layers (the tables: :meth:`read_tables`)."""
+        d = self.dim
+        hid = 32 * 38 * (d // 20 - 2)
+        out = {"conv_w": np.zeros((32, 9), np.float32), "conv_b": np.zeros(32, np.float32),
+               "fc_w": np.zeros((d, hid), np.float32), "fc_b": np.zeros(d, np.float32)}
+        for k in ("bn_w", "bn_b", "bn_m", "bn_v"):
+            out[k] = np.zeros(33 + d, np.float32)
+        check(lib().kp_conve_train_read(self.h, *[_ptr(out[k]) for k in ("conv_w", "conv_b", "fc_w", "fc_b", "bn_w",
+                                                                        "bn_b", "bn_m", "bn_v")]), self.h)
+        return out
 
     def read_tables(self, n_rel2: int):
         """kp_read_tables: (entity [n_ent][dim], relation [n_rel2][dim]) float32."""

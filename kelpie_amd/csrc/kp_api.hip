@@ -132,6 +132,7 @@ int kp_ctx_destroy(kp_ctx* c) {
   c->cvf_fw3.release();
   c->cvf_bw3.release();
   train_state_free(c);
+  cv_train_free(c);
   for (auto e : c->evpool) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -219,6 +220,34 @@ int kp_train_epoch(kp_ctx* c, const kp_hp* hp, int32_t n, const int32_t* triples
       transe_train_epoch(c, hp, n, triples, aux, epoch);
     else
       complex_train_epoch(c, hp, n, triples, aux, epoch);
+  });
+}
+
+int kp_conve_train_begin(kp_ctx* c, const float* bn_weight, const float* bn_bias, const float* bn_mean,
+                         const float* bn_var) {
+  if (!c || !bn_weight || !bn_bias || !bn_mean || !bn_var) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_HIP(hipSetDevice(c->device));
+    conve_train_begin(c, bn_weight, bn_bias, bn_mean, bn_var);
+  });
+}
+
+int kp_conve_train_step(kp_ctx* c, int32_t B, const int32_t* pairs, const int32_t* tail_off, const int32_t* tails,
+                        const float* in_noise, const float* fm_noise, const float* hid_noise, float lr,
+                        float label_smoothing, int32_t bn_train) {
+  if (!c || B <= 0 || !pairs || !tail_off || (tail_off[B] > 0 && !tails)) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_HIP(hipSetDevice(c->device));
+    conve_train_step(c, B, pairs, tail_off, tails, in_noise, fm_noise, hid_noise, lr, label_smoothing, bn_train);
+  });
+}
+
+int kp_conve_train_read(kp_ctx* c, float* conv_w, float* conv_b, float* fc_w, float* fc_b, float* bn_weight,
+                        float* bn_bias, float* bn_mean, float* bn_var) {
+  if (!c || !conv_w || !conv_b || !fc_w || !fc_b || !bn_weight || !bn_bias || !bn_mean || !bn_var) return KP_EINVAL;
+  return guarded(c, [&] {
+    KP_HIP(hipSetDevice(c->device));
+    conve_train_read(c, conv_w, conv_b, fc_w, fc_b, bn_weight, bn_bias, bn_mean, bn_var);
   });
 }
 

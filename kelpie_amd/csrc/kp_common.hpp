@@ -69,6 +69,7 @@ struct Timing {
 };
 
 struct kp_train_state;  // kp_train.hip: optimizer state of a full-model training run
+struct kp_cv_train;     // kp_train_conve.hip: ConvE full-model training state
 
 struct kp_ctx {
   int device = 0;
@@ -112,6 +113,7 @@ struct kp_ctx {
   bool cvf_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
+  kp_cv_train* cvtrain = nullptr;   // kp_conve_train_*'s state (freed with the context)
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<double, double>> hot_pairs;  // (work units, seconds) per hot launch
   std::vector<double> hot_iv;  // [start, end] per hot launch, seconds since the device's time base
@@ -192,6 +194,14 @@ void complex_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* tripl
 // kp_train.hip: one PairwiseRankingOptimizer epoch (TransE): positive and corrupted rows in order
 void transe_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* pos, const int32_t* neg, int epoch);
 void train_state_free(kp_ctx* c);
+// kp_train_conve.hip: ConvE BCEOptimizer training (see include/kelpie_hip.h kp_conve_train_*)
+void cv_train_free(kp_ctx* c);
+void conve_train_begin(kp_ctx* c, const float* bn_w, const float* bn_b, const float* bn_m, const float* bn_v);
+void conve_train_step(kp_ctx* c, int B, const int32_t* pairs, const int32_t* tail_off, const int32_t* tails,
+                      const float* in_noise, const float* fm_noise, const float* hid_noise, float lr,
+                      float label_smoothing, int bn_train);
+void conve_train_read(kp_ctx* c, float* conv_w, float* conv_b, float* fc_w, float* fc_b, float* bn_w, float* bn_b,
+                      float* bn_m, float* bn_v);
 // out[z][m][n] = act(sum_{k in split z} A[m][k] B[n][k] + (z == 0 ? bias[n] : 0)), fp32 MFMA
 void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
                      int ldo, const float* bias, int act, int ksplit);

@@ -10,9 +10,12 @@ its draws are consumed before ``load_state_dict``), the new model's initialisati
 ``torch.randperm`` per epoch (multiclass_nll_optimizer.py:102) come from the same
 torch CPU generator, in that order (TransE: its xavier_normal_ tables and per epoch the
 numpy shuffle and torch.randint negatives of pairwise_ranking_optimizer.py:102-118).
-Supported: ComplEx with its MultiClassNLLOptimizer (Adagrad / Adam / SGD, N3) and
-TransE with its PairwiseRankingOptimizer (Adam, margin ranking, L2); ConvE raises
-``NotImplementedError``.
+Supported: ComplEx with its MultiClassNLLOptimizer (Adagrad / Adam / SGD, N3),
+TransE with its PairwiseRankingOptimizer (Adam, margin ranking, L2) and ConvE with its
+BCEOptimizer (Adam on every layer, train-mode batch norms, the three dropouts; the
+dropout noise is drawn here from the torch generator in the forward's order, the numpy
+shuffle of the (head, relation) pairs once per epoch; ``kp_conve_train_step``,
+``csrc/kp_train_conve.hip``).
 """
 from __future__ import annotations
 
@@ -23,7 +26,7 @@ import numpy as np
 import torch
 
 from .data import MANY_TO_ONE, ONE_TO_ONE, Dataset
-from .models import ComplEx, TransE
+from .models import ComplEx, ConvE, TransE
 
 
 def set_seeds(seed: int = 42):
@@ -53,13 +56,104 @@ def _transe_init(dataset: Dataset, dimension: int):
     return E.numpy(), R.numpy()
 
 
+def _conve_init(dataset: Dataset, model_params: dict):
+    """ConvE(dataset, hp, init_random=True) (conve.py:23-61): the Conv2d(1, 32, 3x3) and
+    Linear(hidden_layer_size, dimension) default initialisations, then the torch.rand
+    tables and xavier_normal_ over each, all from the CPU generator in that order."""
+    d, hidden = int(model_params["dimension"]), int(model_params["hidden_layer_size"])
+    conv = torch.nn.Conv2d(1, 32, (3, 3), 1, 0, bias=True)
+    fc = torch.nn.Linear(hidden, d)
+    E = torch.rand(dataset.num_entities, d)
+    R = torch.rand(2 * dataset.num_relations, d)
+    torch.nn.init.xavier_normal_(E)
+    torch.nn.init.xavier_normal_(R)
+    f = lambda t: t.detach().numpy().copy()  # noqa: E731
+    return E.numpy(), R.numpy(), {"conv_w": f(conv.weight).reshape(32, 3, 3), "conv_b": f(conv.bias),
+                                  "fc_w": f(fc.weight), "fc_b": f(fc.bias)}
+
+
 def model_init(model_name: str, dataset: Dataset, model_params: dict):
-    """The tables of ``MODEL_REGISTRY[model_name](dataset, hp, init_random=True)``."""
+    """The parameters of ``MODEL_REGISTRY[model_name](dataset, hp, init_random=True)``:
+    (E, R) for ComplEx / TransE, (E, R, layers) for ConvE."""
     if model_name == "ComplEx":
         return _complex_init(dataset, model_params["dimension"], model_params["init_scale"])
     if model_name == "TransE":
         return _transe_init(dataset, model_params["dimension"])
-    raise NotImplementedError(f"device retraining supports ComplEx and TransE, not {model_name}")
+    if model_name == "ConvE":
+        return _conve_init(dataset, model_params)
+    raise NotImplementedError(f"device retraining supports ComplEx, TransE and ConvE, not {model_name}")
+
+
+def _dropout_noise(shape, p: float):
+    """nn.Dropout / nn.Dropout2d's CPU multiplier (torch _dropout_impl): nothing drawn for
+    p == 0, zeros for p == 1, else ``empty(shape).bernoulli_(1 - p).div_(1 - p)``."""
+    if p == 0:
+        return None
+    if p == 1:
+        return np.zeros(shape, np.float32)
+    return torch.empty(shape).bernoulli_(1 - p).div_(1 - p).numpy()
+
+
+def _retrain_conve(dataset: Dataset, model_params: dict, training: dict, device, context_factory):
+    """BCEOptimizer.train (bce_optimizer.py:45-150) for a fresh ConvE on the device."""
+    E, R, L = _conve_init(dataset, model_params)
+    d = E.shape[1]
+    h = d // 20
+    model = ConvE(dataset, E, R, L["conv_w"], L["conv_b"], L["fc_w"], L["fc_b"], device=device)
+    if context_factory is not None:
+        model._ctx = context_factory(model)
+    ctx = model.ctx
+    c3 = 33 + d
+    ctx.conve_train_begin(np.ones(c3, np.float32), np.zeros(c3, np.float32), np.zeros(c3, np.float32),
+                          np.ones(c3, np.float32))
+    train = dataset.training_triples
+    stack = np.vstack([train, dataset.invert_triples(train)]).astype(np.int64)
+    # extract_er_vocab: (head, relation) keys in first-occurrence order, tails in row order
+    keys, inv = np.unique(stack[:, 0] * (2 * dataset.num_relations) + stack[:, 1], return_inverse=True)
+    first = np.full(len(keys), len(stack), np.int64)
+    np.minimum.at(first, inv, np.arange(len(stack)))
+    key_order = np.argsort(first, kind="stable")  # pair index -> key index
+    rank_of_key = np.empty(len(keys), np.int64)
+    rank_of_key[key_order] = np.arange(len(keys))
+    pair_of_row = rank_of_key[inv]
+    by_pair = np.argsort(pair_of_row, kind="stable")
+    counts = np.bincount(pair_of_row, minlength=len(keys))
+    off = np.concatenate([[0], np.cumsum(counts)])
+    tails_sorted = stack[by_pair, 2].astype(np.int32)
+    pairs = stack[by_pair[off[:-1]], :2].astype(np.int32)  # [P][2] in er_vocab order
+    P = len(pairs)
+    order = np.arange(P)
+    bs = int(training["batch_size"])
+    ls = float(training["label_smoothing"])
+    lr, decay = float(training["lr"]), float(training["decay"])
+    pin = float(model_params["input_dropout_rate"])
+    pfm = float(model_params["feature_map_dropout_rate"])
+    phid = float(model_params["hidden_dropout_rate"])
+    for _ in range(int(training["epochs"])):
+        np.random.shuffle(order)  # the in-place shuffle of er_vocab_pairs, epoch after epoch
+        for b0 in range(0, P, bs):
+            idx = order[b0:b0 + bs]
+            B = len(idx)
+            cnt = counts[idx]
+            toff = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+            tails = np.concatenate([tails_sorted[off[i]:off[i + 1]] for i in idx]) if B else np.zeros(0, np.int32)
+            nin = _dropout_noise((B, 1, 40, h), pin)
+            nfm = _dropout_noise((B, 32, 1, 1), pfm)
+            nhid = _dropout_noise((B, d), phid)
+            ctx.conve_train_step(pairs[idx], toff, tails, nin, nfm, nhid, lr, ls, B > 1)
+        if decay:
+            lr = lr * decay  # ExponentialLR.step
+    E2, R2 = ctx.read_tables(2 * dataset.num_relations)
+    T = ctx.conve_train_read()
+    sl = [(0, 1), (1, 33), (33, c3)]
+    bn = {i + 1: {"weight": T["bn_w"][a:b], "bias": T["bn_b"][a:b], "running_mean": T["bn_m"][a:b],
+                  "running_var": T["bn_v"][a:b]} for i, (a, b) in enumerate(sl)}
+    out = ConvE(dataset, E2, R2, T["conv_w"].reshape(32, 3, 3), T["conv_b"], T["fc_w"], T["fc_b"], bn=bn,
+                device=device)
+    if context_factory is not None:
+        out._ctx = context_factory(out)
+    out.trained_layers = T
+    return out
 
 
 def _transe_epoch_rows(stack: np.ndarray, ratio: int, n_entities: int):
@@ -86,6 +180,8 @@ def retrain(model_name: str, dataset: Dataset, model_params: dict, training: dic
     pairwise_ranking_optimizer.py:55-100), on the device.  Consumes the torch / numpy
     generators like the reference.  ``context_factory(model)``, if given, supplies the
     model's context (tests)."""
+    if model_name == "ConvE":
+        return _retrain_conve(dataset, model_params, training, device, context_factory)
     E, R = model_init(model_name, dataset, model_params)
     if model_name == "ComplEx":
         model = ComplEx(dataset, E, R, init_scale=model_params["init_scale"], device=device)
@@ -129,8 +225,8 @@ def verify_explanations(explanations: list, dataset: Dataset, model, model_confi
     if mode not in ("necessary", "sufficient"):
         raise ValueError(mode)
     name = model_config["model"]
-    if name not in ("ComplEx", "TransE"):
-        raise NotImplementedError(f"device retraining supports ComplEx and TransE, not {name}")
+    if name not in ("ComplEx", "TransE", "ConvE"):
+        raise NotImplementedError(f"device retraining supports ComplEx, TransE and ConvE, not {name}")
     set_seeds(42)
     # the original model's init_random=True construction (verify_explanations.py:59)
     model_init(name, dataset, model_config["model_params"])

@@ -472,6 +472,74 @@ class TransETrainer:
 # =============================================================================
 # post-training (one trainable kelpie row; SURVEY App. C gradients)
 # =============================================================================
+class ConvETrainer:
+    """Full-model ConvE training, one BCEOptimizer step at a time (bce_optimizer.py:
+    45-150 on conve.py:133-158 in train mode): the reference's layer sequence restated
+    with torch.nn.functional on the CPU (autograd for the gradients), the dropout noise
+    given (the product draws it on the host in the forward's order), Adam with torch's
+    defaults on every parameter, batch norms in eval mode for a one-pair batch."""
+
+    def __init__(self, E, R, conv_w, conv_b, fc_w, fc_b, bn_w, bn_b, bn_m, bn_v):
+        d = E.shape[1]
+        t = lambda a: torch.tensor(np.asarray(a, np.float32), requires_grad=True)  # noqa: E731
+        self.d = d
+        self.params = {"E": t(E), "R": t(R), "cw": t(np.asarray(conv_w).reshape(32, 1, 3, 3)), "cb": t(conv_b),
+                       "fw": t(fc_w), "fb": t(fc_b)}
+        sl = [(0, 1), (1, 33), (33, 33 + d)]
+        for i, (a0, a1) in enumerate(sl, 1):
+            self.params[f"w{i}"] = t(np.asarray(bn_w)[a0:a1])
+            self.params[f"b{i}"] = t(np.asarray(bn_b)[a0:a1])
+        self.rm = [torch.tensor(np.asarray(bn_m, np.float32)[a0:a1]) for a0, a1 in sl]
+        self.rv = [torch.tensor(np.asarray(bn_v, np.float32)[a0:a1]) for a0, a1 in sl]
+        self.opt = torch.optim.Adam(list(self.params.values()), lr=1e-3)
+
+    def step(self, pairs, tail_off, tails, in_noise, fm_noise, hid_noise, lr, label_smoothing, bn_train):
+        import torch.nn.functional as F
+        P = self.params
+        for g in self.opt.param_groups:
+            g["lr"] = lr
+        d, H = self.d, self.d // 20
+        pairs = torch.as_tensor(np.asarray(pairs, np.int64).reshape(-1, 2))
+        B = len(pairs)
+        lhs = P["E"][pairs[:, 0]].view(-1, 1, 20, H)
+        rel = P["R"][pairs[:, 1]].view(-1, 1, 20, H)
+        x = torch.cat([lhs, rel], 2)
+        x = F.batch_norm(x, self.rm[0], self.rv[0], P["w1"], P["b1"], bool(bn_train), 0.1, 1e-5)
+        if in_noise is not None:
+            x = x * torch.as_tensor(np.asarray(in_noise, np.float32).reshape(B, 1, 40, H))
+        x = F.conv2d(x, P["cw"], P["cb"])
+        x = F.batch_norm(x, self.rm[1], self.rv[1], P["w2"], P["b2"], bool(bn_train), 0.1, 1e-5)
+        x = torch.relu(x)
+        if fm_noise is not None:
+            x = x * torch.as_tensor(np.asarray(fm_noise, np.float32).reshape(B, 32, 1, 1))
+        x = x.view(B, -1)
+        x = F.linear(x, P["fw"], P["fb"])
+        if hid_noise is not None:
+            x = x * torch.as_tensor(np.asarray(hid_noise, np.float32).reshape(B, d))
+        x = F.batch_norm(x, self.rm[2], self.rv[2], P["w3"], P["b3"], bool(bn_train), 0.1, 1e-5)
+        x = torch.relu(x)
+        p = torch.sigmoid(torch.mm(x, P["E"].transpose(1, 0)))
+        N = P["E"].shape[0]
+        tgt = torch.zeros(B, N)
+        for b in range(B):
+            for e in tails[tail_off[b]:tail_off[b + 1]]:
+                tgt[b, int(e)] = 1.0
+        if label_smoothing:
+            tgt = (1.0 - label_smoothing) * tgt
+            tgt += 1.0 / N
+        self.opt.zero_grad()
+        torch.nn.functional.binary_cross_entropy(p, tgt).backward()
+        self.opt.step()
+
+    def read(self):
+        g = lambda k: self.params[k].detach().numpy().copy()  # noqa: E731
+        cat = lambda xs: np.concatenate([np.asarray(v, np.float32) for v in xs])  # noqa: E731
+        return {"E": g("E"), "R": g("R"), "conv_w": g("cw").reshape(32, 9), "conv_b": g("cb"), "fc_w": g("fw"),
+                "fc_b": g("fb"), "bn_w": cat([g(f"w{i}") for i in (1, 2, 3)]),
+                "bn_b": cat([g(f"b{i}") for i in (1, 2, 3)]), "bn_m": cat([m.numpy() for m in self.rm]),
+                "bn_v": cat([v.numpy() for v in self.rv])}
+
+
 def _rows_with_inverses(ds, triples):
     t = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
     return np.vstack([t, ds.invert_triples(t)])

@@ -175,7 +175,23 @@ class OracleBackedContext:
         self.om.E, self.om.R = self._trainer.E, self._trainer.R
 
     def read_tables(self, n_rel2):
+        if getattr(self, "_cvtrainer", None) is not None:
+            r = self._cvtrainer.read()
+            return r["E"], r["R"]
         return self.om.E.copy(), self.om.R.copy()
+
+    # stand-ins for kp_conve_train_* (the oracle's ConvE trainer on this context's weights)
+    def conve_train_begin(self, bn_w, bn_b, bn_m, bn_v):
+        m = self.model
+        self._cvtrainer = ko.ConvETrainer(m.entity_embeddings, m.relation_embeddings, m.conv_weight, m.conv_bias,
+                                          m.fc_weight, m.fc_bias, bn_w, bn_b, bn_m, bn_v)
+
+    def conve_train_step(self, pairs, tail_off, tails, in_noise, fm_noise, hid_noise, lr, label_smoothing, bn_train):
+        self._cvtrainer.step(pairs, tail_off, tails, in_noise, fm_noise, hid_noise, lr, label_smoothing, bn_train)
+
+    def conve_train_read(self):
+        r = self._cvtrainer.read()
+        return {k: r[k] for k in ("conv_w", "conv_b", "fc_w", "fc_b", "bn_w", "bn_b", "bn_m", "bn_v")}
 
 
 def _dp_relevance(self, items, epsilon, lambd, step_sign, rel_sign):

@@ -11,7 +11,7 @@ recorded.
 A direct training run (set_seeds(42), ComplEx(init_random=True), optimizer.train on
 the unedited training set) records the trained tables, to pin the trainer itself.
 
-    python tests/golden/make_verify_golden.py      -> tests/golden/verify_golden.json
+    python tests/golden/make_verify_golden.py [case ...]   -> tests/golden/verify_golden.json
 """
 from __future__ import annotations
 
@@ -40,6 +40,16 @@ CASES_VERIFY = {
                            "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0.05},
             "adam": {"optimizer_name": "Adam", "batch_size": 128, "epochs": 3, "lr": 0.01, "decay1": 0.9,
                      "decay2": 0.999, "regularizer_name": "N3", "regularizer_weight": 0.0},
+        },
+    },
+    "conve60_tiny": {
+        "model": "ConvE",
+        # the explained model's shape (make_golden.py), every dropout of the reference
+        # configs switched on for the retraining (ConvE_*_training.json use 0.2 / 0.3 / 0.1-0.2)
+        "model_params": {"dimension": 60, "input_dropout_rate": 0.2, "feature_map_dropout_rate": 0.3,
+                         "hidden_dropout_rate": 0.2, "hidden_layer_size": 1216},
+        "training": {
+            "bce": {"batch_size": 256, "label_smoothing": 0.1, "lr": 0.003, "decay": 0.995, "epochs": 3},
         },
     },
     "transe_tiny": {
@@ -119,6 +129,17 @@ def run_case(src, name, spec, ver, MODEL_REGISTRY):
                          "E_abs_sum": float(np.abs(E.astype(np.float64)).sum()),
                          "R_abs_sum": float(np.abs(R.astype(np.float64)).sum()),
                          "E_sha256": digest(E), "R_sha256": digest(R)}
+        if spec["model"] == "ConvE":
+            # the frozen layers the retraining also trains, and the batch-norm running statistics
+            f64 = lambda t: t.detach().cpu().numpy().astype(np.float64)  # noqa: E731
+            direct[tname]["layers"] = {
+                "conv_w_abs_sum": float(np.abs(f64(m.convolutional_layer.weight)).sum()),
+                "conv_b": f64(m.convolutional_layer.bias).tolist(),
+                "fc_w_abs_sum": float(np.abs(f64(m.hidden_layer.weight)).sum()),
+                "fc_b": f64(m.hidden_layer.bias).tolist(),
+                **{f"bn{i}_{k}": f64(getattr(bn, k)).tolist()
+                   for i, bn in ((1, m.batch_norm_1), (2, m.batch_norm_2), (3, m.batch_norm_3))
+                   for k in ("weight", "bias", "running_mean", "running_var")}}
     out["direct"] = direct
     return out
 
@@ -130,8 +151,16 @@ def main():
     # utils.set_seeds (utils/utils.py:15-21) without its torch.cuda state touch: the
     # same three CPU seeds
     ver.set_seeds = ref_harness.seed_all
-    out = {"cases": {name: run_case(src, name, spec, ver, MODEL_REGISTRY) for name, spec in CASES_VERIFY.items()}}
-    with open(os.path.join(HERE, "verify_golden.json"), "w") as f:
+    path = os.path.join(HERE, "verify_golden.json")
+    only = sys.argv[1:]  # case names to (re)generate; the others are kept as recorded
+    out = {"cases": {}}
+    if only and os.path.exists(path):
+        with open(path) as f:
+            out = json.load(f)
+    for name, spec in CASES_VERIFY.items():
+        if not only or name in only:
+            out["cases"][name] = run_case(src, name, spec, ver, MODEL_REGISTRY)
+    with open(path, "w") as f:
         json.dump(out, f)
 
 
