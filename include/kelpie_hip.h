@@ -134,6 +134,13 @@ int kp_ctx_create(int device, const kp_model_desc* model, kp_ctx** out);
 int kp_ctx_destroy(kp_ctx* ctx);
 const char* kp_last_error(const kp_ctx* ctx);
 
+/* Page-locked host memory (hipHostMalloc) for the buffers the caller fills and a
+ * context uploads every batch: the deferred-draw arenas of kelpie_amd.rng, which
+ * kp_posttrain_rank then reads by DMA with no staging copy (the reference has no
+ * counterpart: its draws never leave the host).  KP_EDEVICE without a usable GPU. */
+int kp_host_alloc(size_t bytes, void** out);
+int kp_host_free(void* p);
+
 /* Post-train every slot of the batch and rank its target triple.
  * Replaces, per slot: KelpieX(...) construction, Kelpie*Optimizer.train
  * (pairwise_ranking_optimizer.py:160-203, multiclass_nll_optimizer.py:138-164,

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -25,7 +26,7 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
            "kp_rng_transe_calls", "kp_train_epoch", "kp_read_tables", "kp_view_create", "kp_view_destroy",
            "kp_sched_batch_create", "kp_sched_batch_destroy", "kp_sched_add_calls", "kp_sched_pack",
            "kp_gather_i32", "kp_rng_transe_calls_async", "kp_rng_torch_take", "kp_conve_train_begin",
-           "kp_conve_train_step", "kp_conve_train_read"]
+           "kp_conve_train_step", "kp_conve_train_read", "kp_host_alloc", "kp_host_free"]
 
 
 class ModelDesc(C.Structure):
@@ -65,6 +66,8 @@ def lib():
         L.kp_ctx_destroy.argtypes = [C.c_void_p]
         L.kp_last_error.argtypes = [C.c_void_p]
         L.kp_last_error.restype = C.c_char_p
+        L.kp_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+        L.kp_host_free.argtypes = [C.c_void_p]
         L.kp_posttrain_rank.argtypes = [C.c_void_p, C.POINTER(HP), C.POINTER(Batch)]
         L.kp_all_scores.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_convertible.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
@@ -534,6 +537,42 @@ class SchedBatch:
         assert rows.dtype == np.int32 and rows.flags.c_contiguous and filt.dtype == np.int32
         check(self._lib.kp_sched_pack(C.c_void_p(self.h), len(i), _ptr(i), _ptr(rows), rows.size, _ptr(filt),
                                       filt.size))
+
+
+# Page-locked int32 arenas (kp_host_alloc), pooled for the life of the process: the
+# deferred-draw arenas of kelpie_amd.rng come from here when a GPU is present, so a
+# batch's draws reach the device by DMA straight from where the RNG workers wrote them.
+_PINNED = []
+_PINNED_MAX = int(os.environ.get("KP_PINNED_ARENAS", "6"))
+_PINNED_OK = None
+
+
+def pinned_i32(n: int):
+    """An idle pooled page-locked int32 array of at least ``n`` words, or None (pool
+    full and busy, or no usable GPU: then the caller takes pageable memory).  An array
+    is idle when nothing but the pool references it (every view of it holds it as its
+    ``base``), so an arena returns to the pool once the batch using it is dropped."""
+    global _PINNED_OK
+    for a in _PINNED:
+        # references while idle: the pool list, the loop variable, getrefcount's argument
+        if a.size >= n and sys.getrefcount(a) <= 3:
+            return a
+    if _PINNED_OK is False or len(_PINNED) >= _PINNED_MAX:
+        return None
+    p = C.c_void_p()
+    if lib().kp_host_alloc(4 * int(n), C.byref(p)) != 0 or not p.value:
+        _PINNED_OK = False
+        return None
+    _PINNED_OK = True
+    a = np.ctypeslib.as_array((C.c_int32 * int(n)).from_address(p.value))
+    _PINNED.append(a)
+    return _PINNED[-1]
+
+
+def is_pinned(a: np.ndarray) -> bool:
+    """``a`` is (a view of) a pooled page-locked arena."""
+    b = a if a.base is None or not isinstance(a.base, np.ndarray) else a.base
+    return any(b is p for p in _PINNED)
 
 
 def gather_i32(arrays, out: np.ndarray) -> np.ndarray:

@@ -48,6 +48,23 @@ const char* kp_version(void) { return "kelpie_hip 0.1 (gfx950)"; }
 
 const char* kp_last_error(const kp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_tls_err.c_str(); }
 
+int kp_host_alloc(size_t bytes, void** out) {
+  if (!out) return KP_EINVAL;
+  *out = nullptr;
+  return guarded(nullptr, [&] {
+    KP_REQUIRE(bytes > 0, "kp_host_alloc: zero bytes");
+    void* p = nullptr;
+    KP_HIP(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    *out = p;
+  });
+}
+
+int kp_host_free(void* p) {
+  return guarded(nullptr, [&] {
+    if (p) KP_HIP(hipHostFree(p));
+  });
+}
+
 int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
   if (!out || !m) return KP_EINVAL;
   *out = nullptr;

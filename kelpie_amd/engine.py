@@ -48,19 +48,35 @@ class _Slot:
 
 
 def _contiguous_draws(slots, total, ctx=None):
-    """The slots' draws as one int32 array.  Handing the library a view of the deferred
-    draw arena instead (no copy) measured slower end to end: its upload from the arena's
-    pages, first touched by the RNG worker threads, took 10-20 ms per TransE batch against
-    3 ms after this copy (profiles/r02zd_transe_draws_upload.txt).  The copy goes into a
+    """The slots' draws as one int32 array.  When they lie back to back in one pooled
+    page-locked arena (rng.ReferenceRNG._take with a GPU present), that span itself: the
+    library reads it by DMA, no copy.  Otherwise a copy: handing the library a view of a
+    pageable arena measured slower end to end (its upload from pages first touched by
+    the RNG worker threads took 10-20 ms per TransE batch against 3 ms after a copy into
+    a reused buffer, profiles/r02zd_transe_draws_upload.txt).  The copy goes into a
     buffer kept with the device context ``ctx`` (no fresh pages per batch; the context's
     previous batch is done with it) and runs in the library without the interpreter lock,
     so the next batch's scheduling thread is not held up."""
     if total == 0:
         return np.zeros(1, np.int32)
     arrays = [s.rng.reshape(-1) for s in slots]
+    from . import _lib
+    live = [a for a in arrays if a.size]
+    if live and _lib.is_pinned(live[0]):
+        # the draws were written back to back into one page-locked arena in slot order
+        # (the usual case): hand the library that span, which it uploads by DMA
+        base = live[0].base if isinstance(live[0].base, np.ndarray) else live[0]
+        start = live[0].__array_interface__["data"][0]
+        pos = start
+        for a in live:
+            if a.base is not base or a.__array_interface__["data"][0] != pos or a.dtype.itemsize != 4:
+                break
+            pos += 4 * a.size
+        else:
+            off = (start - base.__array_interface__["data"][0]) // 4
+            return base[off:off + total]
     if ctx is None or any(a.dtype.itemsize != 4 for a in arrays):
         return np.concatenate(arrays).astype(np.int32, copy=False)
-    from . import _lib
     buf = getattr(ctx, "_draw_buf", None)
     if buf is None or buf.size < total:
         buf = np.empty(int(total * 1.25) + 1024, np.int32)

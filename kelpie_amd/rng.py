@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 
 import numpy as np
 import torch
@@ -74,6 +75,7 @@ _outstanding = False
 # until sync(): a caller that drops its draw arrays early must not free them under the
 # workers
 _inflight = []
+_PINNED_ARENAS = os.environ.get("KP_PINNED_ARENA", "1") != "0"
 
 
 # torch-generator outputs owed by draws whose values nobody needs (the slots another
@@ -148,7 +150,11 @@ class ReferenceRNG:
 
     def _take(self, n: int) -> np.ndarray:
         if self._arena is None or self._arena_pos + n > self._arena.size:
-            self._arena, self._arena_pos = np.empty(max(self._ARENA, n), np.int32), 0
+            size = max(self._ARENA, n)
+            # page-locked and reused when the library can give it (the device reads the
+            # batch's draws from here by DMA, engine._contiguous_draws); else pageable
+            a = _lib.pinned_i32(size) if _PINNED_ARENAS else None
+            self._arena, self._arena_pos = (a if a is not None else np.empty(size, np.int32)), 0
             _inflight.append(self._arena)
         out = self._arena[self._arena_pos:self._arena_pos + n]
         self._arena_pos += n
