@@ -272,7 +272,7 @@ int kp_rng_transe_epochs(uint8_t* torch_state, size_t torch_len, uint32_t* np_ke
  * snapshots the torch state, advances it past the slot's randints at once, and
  * queues the draws.  One worker thread runs the queued numpy shuffles in queue
  * order on the live numpy state at np_key / np_pos (which nobody else may touch
- * until kp_rng_wait returns); a small pool (KP_RNG_THREADS, default 2) fills the
+ * until kp_rng_wait returns); a small pool (KP_RNG_THREADS, default 4) fills the
  * randints from each snapshot.  `out` must stay valid until kp_rng_wait.
  * Same draws, same final states as calling kp_rng_transe_epochs per slot. */
 int kp_rng_transe_enqueue(uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos, int32_t R,

@@ -48,6 +48,16 @@ __device__ unsigned long long g_attn3_stamps[8];
 #define KP3_ACC(i, a, b) (void)0
 #endif
 
+#ifdef KP_ATTN3_CLOCK
+#ifndef KP_DIAGNOSTIC_BUILD
+#error "KP_ATTN3_CLOCK is a diagnostic build (tools/attn_micro.sh)"
+#endif
+// diagnostic: the in-kernel clock (MI355X_MICROARCH 'DVFS give-back' item 6): thread 0 of
+// each workgroup stamps s_memtime and s_memrealtime (100 MHz) when it starts and when it
+// leaves; the stamps go only to this buffer, nothing else reads them
+__device__ unsigned long long g_attn3_clock[4096][4];
+#endif
+
 #ifndef KP_O_AHEAD
 #define KP_O_AHEAD 1
 #endif
@@ -310,6 +320,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
     for (int k = 0; k < NPW; ++k)
       if ((k * NSLOT) / NPW == slot) issue_piece(tile, buf, k);
   };
+#ifdef KP_ATTN3_CLOCK
+  if (tid == 0 && blockIdx.x < 4096) {
+    g_attn3_clock[blockIdx.x][0] = __builtin_amdgcn_s_memtime();
+    g_attn3_clock[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   const int QT = (nq + 63) / 64;
   // work segments: stream-K ranges (wk.ranges == 0) or XCD-grouped units (attn_plan_ranges)
   const long long total = (long long)QT * wk.ktq;
@@ -770,6 +786,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #ifdef KP_ATTN3_STAMPS
   if (lane == 0)
     for (int i = 0; i < 5; ++i) atomicAdd(&g_attn3_stamps[i], st_acc[i]);
+#endif
+#ifdef KP_ATTN3_CLOCK
+  if (tid == 0 && blockIdx.x < 4096) {
+    g_attn3_clock[blockIdx.x][2] = __builtin_amdgcn_s_memtime();
+    g_attn3_clock[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+  }
 #endif
 }
 

@@ -472,48 +472,74 @@ void bernoulli_words(TorchMt& mt, uint64_t n, double p, uint32_t* out, std::vect
 // Both write disjoint parts of the slot's output ([row order | entity | head_or_tail]
 // per epoch).  kp_rng_wait() returns once every queued slot is complete.
 
-void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np,
-                 std::vector<int32_t>& idx) {
+// The shuffles of one slot come in two parts:
+//  * te_draws (sequential, on the live numpy state): every epoch's random_interval(i)
+//    draws, i = R - 1 .. 1 (masked rejection, numpy's consumption is data-dependent), the
+//    draw for i left at out[e*3R + i] (its row-order slot, used as scratch);
+//  * te_perms (any thread, after te_draws): the permutation chain -- epoch e shuffles the
+//    order left by epoch e - 1 with those draws -- written over the same slots.
+// Only te_draws is on the batch's sequential chain.
+// ui - (v <= ui) as ui - 1 + borrow(ui - v): a two-instruction carried chain (cmp, adc)
+inline uint32_t accept_step(uint32_t ui, uint32_t v) {
+#if defined(__x86_64__)
+  asm("cmpl %1, %0\n\tadcl $-1, %0" : "+r"(ui) : "r"(v) : "cc");
+  return ui;
+#else
+  return ui - (uint32_t)(v <= ui);
+#endif
+}
+
+void te_draws(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np) {
   // validated here, on the thread that owns the live numpy state while draws are queued
   // (the enqueueing thread must not read it: the sequential worker may be writing it)
   if (*np_pos < 0 || *np_pos > kN) throw std::invalid_argument("numpy MT19937 pos out of range");
   np.load(np_key, np_pos);
-  idx.resize(2 * (size_t)std::max(R, 1));
-  int32_t* perm = idx.data();
-  int32_t* jv = perm + std::max(R, 1);  // jv[i] = the interval(i) draw of this epoch
-  for (int i = 0; i < R; ++i) perm[i] = i;
   for (int e = 0; e < epochs; ++e) {
-    // for i in reversed(range(1, n)): j = random_interval(i) (masked rejection): one draw
-    // per iteration, branch-free; a rejected draw leaves i unchanged and its jv[i] is
-    // overwritten by the next one (the draws consumed are numpy's, in its order)
-    int i = R - 1;
-    while (i >= 1) {
+    int32_t* jv = out ? out + (size_t)e * 3 * R : nullptr;  // null: advance only
+    // for i in reversed(range(1, R)): j = random_interval(i).  The mask of i is fixed while
+    // i stays above half of it, so the inner loop's carried chain is compare -> subtract; a
+    // rejected draw leaves i unchanged and its jv[i] is overwritten by the next one
+    uint32_t ui = (uint32_t)(R - 1);
+    while (ui >= 1) {
       if (np.pos >= kN) {
         mt_twist(np.key);
         np.temper_all();
         np.pos = 0;
       }
-      const int n = kN - np.pos;  // draws left in this block
+      const uint32_t mask = 0xFFFFFFFFu >> __builtin_clz(ui), lo = mask >> 1;
       const uint32_t* tb = np.tb + np.pos;
-      // the loop-carried chain is only compare -> subtract: the mask for i - 1 is derived
-      // from i and the current mask alongside (it halves when i - 1 drops below its top bit)
-      uint32_t ui = (uint32_t)i, mask = 0xFFFFFFFFu >> __builtin_clz(ui);
+      const int n = kN - np.pos;  // draws left in this block
       int k = 0;
-      for (; k < n && ui >= 1; ++k) {
-        const uint32_t v = tb[k] & mask;
-        jv[ui] = (int32_t)v;
-        const uint32_t m1 = (ui - 1 > (mask >> 1)) ? mask : (mask >> 1);
-        const bool acc = v <= ui;
-        mask = acc ? m1 : mask;
-        ui -= acc;
+      if (jv) {
+        for (; k < n && ui > lo; ++k) {
+          const uint32_t v = tb[k] & mask;
+          jv[ui] = (int32_t)v;
+          ui = accept_step(ui, v);
+        }
+      } else {
+        for (; k < n && ui > lo; ++k) ui = accept_step(ui, tb[k] & mask);
       }
-      i = (int)ui;
       np.pos += k;
     }
-    for (int t = R - 1; t >= 1; --t) std::swap(perm[t], perm[jv[t]]);
-    if (out) std::memcpy(out + (size_t)e * 3 * R, perm, sizeof(int32_t) * R);  // null: advance only
   }
   np.store(np_key, np_pos);
+}
+
+void te_perms(int32_t R, int32_t epochs, int32_t* out, std::vector<int32_t>& idx) {
+  idx.resize((size_t)std::max(R, 1));
+  int32_t* perm = idx.data();
+  for (int i = 0; i < R; ++i) perm[i] = i;
+  for (int e = 0; e < epochs; ++e) {
+    int32_t* o = out + (size_t)e * 3 * R;
+    for (int t = R - 1; t >= 1; --t) std::swap(perm[t], perm[o[t]]);
+    std::memcpy(o, perm, sizeof(int32_t) * R);
+  }
+}
+
+void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np,
+                 std::vector<int32_t>& idx) {
+  te_draws(np_key, np_pos, R, epochs, out, np);
+  if (out) te_perms(R, epochs, out, idx);
 }
 
 // torch.randint(high=N) = random() % N and randint(high=2), ratio*R each per epoch;
@@ -554,15 +580,18 @@ class DrawQueue {
   bool enqueue(Task seq, Task fill) {
     std::lock_guard<std::mutex> lk(mu_);
     if (!ensure_locked()) return false;
+    // one wake-up per queued task, on the queue's own condition variable (a notify_all on a
+    // shared one woke every pool thread for each of a batch's ~600 tasks)
     if (seq) {
       seq_.push_back(std::move(seq));
       ++pending_;
+      cv_seq_.notify_one();
     }
     if (fill) {
       fills_.push_back(std::move(fill));
       ++pending_;
+      cv_fill_.notify_one();
     }
-    cv_work_.notify_all();
     return true;
   }
   int wait() {
@@ -581,7 +610,7 @@ class DrawQueue {
     seq_.clear();
     fills_.clear();
     pending_ = 0;
-    int nfill = 2;
+    int nfill = 4;
     if (const char* e = std::getenv("KP_RNG_THREADS")) nfill = std::max(1, std::min(16, std::atoi(e)));
     try {
       std::thread([this] { loop(true); }).detach();
@@ -600,7 +629,7 @@ class DrawQueue {
       {
         std::unique_lock<std::mutex> lk(mu_);
         auto& q = sequential ? seq_ : fills_;
-        cv_work_.wait(lk, [&] { return !q.empty(); });
+        (sequential ? cv_seq_ : cv_fill_).wait(lk, [&] { return !q.empty(); });
         if (pid_ != me) return;
         t = std::move(q.front());
         q.pop_front();
@@ -619,7 +648,7 @@ class DrawQueue {
     }
   }
   std::mutex mu_;
-  std::condition_variable cv_work_, cv_done_;
+  std::condition_variable cv_seq_, cv_fill_, cv_done_;
   std::deque<Task> seq_, fills_;
   int64_t pending_ = 0;
   int fail_rc_ = KP_OK;  // first failure of a queued task since the last wait()
@@ -635,7 +664,12 @@ int te_enqueue(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_
   if (R == 0 || epochs == 0) return KP_OK;  // np.random.shuffle of an empty array draws nothing
   const TorchMt snap = mt;
   mt.skip((uint64_t)epochs * 2u * (uint64_t)ratio * (uint64_t)R);
-  Task seq = [=](Scratch& sc) { te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx); };
+  Task seq = [=](Scratch& sc) {
+    te_draws(np_key, np_pos, R, epochs, out, sc.np);
+    // the permutation chain leaves the sequential worker for the pool
+    if (out && !DrawQueue::get().enqueue(Task(), [=](Scratch& s2) { te_perms(R, epochs, out, s2.idx); }))
+      te_perms(R, epochs, out, sc.idx);
+  };
   Task fill;
   if (out)
     fill = [=](Scratch& sc) {

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <random>
 
 #include "kp_attn3.hpp"  // -I selects the source tree under test (tools/attn_micro.sh)
@@ -159,6 +160,24 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
     const double n = (double)(st[4] ? st[4] : 1);
     printf("{\"stamps\": {\"S\": %.0f, \"softmax\": %.0f, \"O\": %.0f, \"tile_end\": %.0f, \"wave_tiles\": %llu}}\n",
            st[0] / n, st[1] / n, st[2] / n, st[3] / n, st[4]);
+  }
+#endif
+#ifdef KP_ATTN3_CLOCK
+  {
+    // >= 2 s of back-to-back launches on the random inputs, then one stamped launch:
+    // median over workgroups of the in-kernel clock = d(memtime) / d(realtime) x 100 MHz
+    const int warm = std::max(1, (int)(2000.0 / std::max(ms, 1e-3f)));
+    for (int i = 0; i < warm; ++i) launch();
+    KP_HIP(hipStreamSynchronize(c.stream));
+    static unsigned long long ck[4096][4];
+    KP_HIP(hipMemcpyFromSymbol(ck, HIP_SYMBOL(g_attn3_clock), sizeof(ck)));
+    std::vector<double> f;
+    for (int b = 0; b < std::min(plan.n_wg, 4096); ++b)
+      if (ck[b][3] > ck[b][1]) f.push_back((double)(ck[b][2] - ck[b][0]) / (double)(ck[b][3] - ck[b][1]) * 0.1);
+    std::sort(f.begin(), f.end());
+    const double med = f.empty() ? 0.0 : f[f.size() / 2];
+    printf("{\"clock_ghz_median\": %.4f, \"clock_ghz_min\": %.4f, \"clock_ghz_max\": %.4f, \"workgroups\": %zu, "
+           "\"warm_launches\": %d}\n", med, f.empty() ? 0.0 : f.front(), f.empty() ? 0.0 : f.back(), f.size(), warm);
   }
 #endif
   printf("{\"DB\": %d, \"mode\": %d, \"n_ent\": %d, \"nq\": %d, \"parts\": %d, \"ranges\": %d, \"n_wg\": %d, "
