@@ -232,11 +232,17 @@ class OracleModel:
         img_bn = (img * a1[0] + b1[0]).astype(F32)
         W = self.w["conv_weight"][:, 0]  # (32,3,3)
         H, Wd = 38, self.eh - 2
-        conv = np.zeros((b, 32, H, Wd), F32)
-        for ky in range(3):
-            for kx in range(3):
-                patch = img_bn[:, ky:ky + H, kx:kx + Wd]  # (b,H,Wd)
-                conv += W[None, :, ky, kx, None, None] * patch[:, None]
+        # per channel: the nine taps accumulated in (ky, kx) order on cache-sized arrays
+        # (the same float32 operations, in the same order, as one pass per tap)
+        patches = [np.ascontiguousarray(img_bn[:, ky:ky + H, kx:kx + Wd]) for ky in range(3) for kx in range(3)]
+        conv = np.empty((b, 32, H, Wd), F32)
+        tmp = np.empty((b, H, Wd), F32)
+        for ch in range(32):
+            acc = np.zeros((b, H, Wd), F32)
+            for k in range(9):
+                np.multiply(patches[k], W[ch, k // 3, k % 3], out=tmp)
+                acc += tmp
+            conv[:, ch] = acc
         conv += self.w["conv_bias"][None, :, None, None]
         a2, b2 = self.bn[2]
         c_bn = (conv * a2[None, :, None, None] + b2[None, :, None, None]).astype(F32)
