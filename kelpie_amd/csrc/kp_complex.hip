@@ -117,33 +117,49 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
     // one-sided ulp error of a fast exp / log here (every row, every step, the same
     // sign) became a one-sided drift of those coordinates of the kelpie row (measured
     // ~-4e-6 against the fp64 reference, tools/headline_probe.py).
-    float mm = kNegInf;
-    for (int sp = 0; sp < n_split; ++sp) mm = fmaxf(mm, att_m[(size_t)sp * nq + item]);
-    double ll = 0.0;
-    for (int sp = 0; sp < n_split; ++sp) {
-      const float ms = att_m[(size_t)sp * nq + item];
-      ll += (ms == kNegInf) ? 0.0 : (double)att_l[(size_t)sp * nq + item] * exp((double)ms - (double)mm);
-    }
-    const double lse_f = (double)mm + log(ll);
+    // The split statistics one split per lane (n_split <= 64): the max, the fp64 sum of
+    // the rescaled l's (a butterfly, deterministic) and each split's weight, so a wave
+    // makes two fp64 exp per lane instead of 2 n_split in sequence on every lane.
+    const bool has = lane < n_split;
+    const float ms_l = has ? att_m[(size_t)lane * nq + item] : kNegInf;
+    const float ls_l = has ? att_l[(size_t)lane * nq + item] : 0.f;
+    const float mm = wave_max(ms_l);
+    double e_l = (ms_l == kNegInf) ? 0.0 : (double)ls_l * exp((double)ms_l - (double)mm);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) e_l += __shfl_xor(e_l, o, 64);
+    const double lse_f = (double)mm + log(e_l);
     const double hi = fmax(lse_f, (double)z), lo = fmin(lse_f, (double)z);
     const double lse = hi + log1p(exp(lo - hi));
     const double pk = exp((double)z - lse);
-    // merge the partials split by split: each split's loads for all of this lane's
-    // dimensions are in flight together, with few live registers (occupancy)
+    const double wv_l = (ms_l == kNegInf) ? 0.0 : exp((double)ms_l - lse);
+    // merge the partials split by split (increasing split order), two splits' loads in
+    // flight together, few live registers (occupancy)
     constexpr int NI = (DP / 2 + 63) / 64;
     double ore_k[NI], oim_k[NI];
 #pragma unroll
     for (int k = 0; k < NI; ++k) ore_k[k] = oim_k[k] = 0.0;
-    for (int sp = 0; sp < n_split; ++sp) {
-      const float ms = att_m[(size_t)sp * nq + item];
-      const double wv = (ms == kNegInf) ? 0.0 : exp((double)ms - lse);
-      const float* Op = att_O + ((size_t)sp * nq + item) * DP;
+    for (int sp = 0; sp < n_split; sp += 2) {
+      const bool two = sp + 1 < n_split;
+      const double w0 = __shfl(wv_l, sp, 64), w1 = __shfl(wv_l, two ? sp + 1 : sp, 64);
+      const float* O0 = att_O + ((size_t)sp * nq + item) * DP;
+      const float* O1 = att_O + ((size_t)(two ? sp + 1 : sp) * nq + item) * DP;
+      float a0[NI], b0[NI], a1[NI], b1[NI];
 #pragma unroll
       for (int k = 0; k < NI; ++k) {
         const int i = lane + 64 * k;
-        if (i < half) {
-          ore_k[k] += wv * (double)Op[i];
-          oim_k[k] += wv * (double)Op[i + half];
+        const bool in = i < half;
+        a0[k] = in ? O0[i] : 0.f;
+        b0[k] = in ? O0[i + half] : 0.f;
+        a1[k] = (in && two) ? O1[i] : 0.f;
+        b1[k] = (in && two) ? O1[i + half] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < NI; ++k) {
+        ore_k[k] += w0 * (double)a0[k];
+        oim_k[k] += w0 * (double)b0[k];
+        if (two) {
+          ore_k[k] += w1 * (double)a1[k];
+          oim_k[k] += w1 * (double)b1[k];
         }
       }
     }
@@ -378,6 +394,7 @@ void launch_update(kp_ctx* c, int n_act, const int4* act, const CxPlan* plans, c
                    float* X, float* S1, float* S2, const CxOpt& opt) {
   if (n_act <= 0) return;
   const int half = c->dim / 2;
+  KP_REQUIRE(n_split >= 1 && n_split <= 64, "cx contrib: one attention split per lane");
   if (nq + nt > 0) {
     hipLaunchKernelGGL((kp_cx_contrib<16 * DB>), dim3((nq + nt + 3) / 4), dim3(256), 0, c->stream, half, stepq, nq,
                        stept, nt, pq, X, c->dR, tsum, qpair, lsef, am, al, aO, n_split, contrib);

@@ -25,6 +25,8 @@
 //     (SURVEY A-Q2): the others are skipped by twisting, without tempering.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <condition_variable>
 #include <cstdlib>
@@ -489,13 +491,13 @@ inline uint32_t accept_step(uint32_t ui, uint32_t v) {
 #endif
 }
 
-void te_draws(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np) {
+void te_draws(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* jv0, size_t stride, NumpyMt& np) {
   // validated here, on the thread that owns the live numpy state while draws are queued
   // (the enqueueing thread must not read it: the sequential worker may be writing it)
   if (*np_pos < 0 || *np_pos > kN) throw std::invalid_argument("numpy MT19937 pos out of range");
   np.load(np_key, np_pos);
   for (int e = 0; e < epochs; ++e) {
-    int32_t* jv = out ? out + (size_t)e * 3 * R : nullptr;  // null: advance only
+    int32_t* jv = jv0 ? jv0 + (size_t)e * stride : nullptr;  // null: advance only
     // for i in reversed(range(1, R)): j = random_interval(i).  The mask of i is fixed while
     // i stays above half of it, so the inner loop's carried chain is compare -> subtract; a
     // rejected draw leaves i unchanged and its jv[i] is overwritten by the next one
@@ -525,22 +527,32 @@ void te_draws(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int3
   np.store(np_key, np_pos);
 }
 
-void te_perms(int32_t R, int32_t epochs, int32_t* out, std::vector<int32_t>& idx) {
+void te_perms(int32_t R, int32_t epochs, const int32_t* jv0, size_t stride, int32_t* out, std::vector<int32_t>& idx) {
   idx.resize((size_t)std::max(R, 1));
   int32_t* perm = idx.data();
   for (int i = 0; i < R; ++i) perm[i] = i;
   for (int e = 0; e < epochs; ++e) {
-    int32_t* o = out + (size_t)e * 3 * R;
-    for (int t = R - 1; t >= 1; --t) std::swap(perm[t], perm[o[t]]);
-    std::memcpy(o, perm, sizeof(int32_t) * R);
+    const int32_t* jv = jv0 + (size_t)e * stride;
+    for (int t = R - 1; t >= 1; --t) std::swap(perm[t], perm[jv[t]]);
+    std::memcpy(out + (size_t)e * 3 * R, perm, sizeof(int32_t) * R);
   }
 }
 
+// both parts on one thread: the draws into a local scratch (cache-resident), then the chain
 void te_shuffles(uint32_t* np_key, int32_t* np_pos, int32_t R, int32_t epochs, int32_t* out, NumpyMt& np,
-                 std::vector<int32_t>& idx) {
-  te_draws(np_key, np_pos, R, epochs, out, np);
-  if (out) te_perms(R, epochs, out, idx);
+                 std::vector<int32_t>& idx, std::vector<int32_t>& jv) {
+  if (!out) {
+    te_draws(np_key, np_pos, R, epochs, nullptr, 0, np);
+    return;
+  }
+  jv.resize((size_t)std::max(R, 1) * std::max(epochs, 1));
+  te_draws(np_key, np_pos, R, epochs, jv.data(), (size_t)R, np);
+  te_perms(R, epochs, jv.data(), (size_t)R, out, idx);
 }
+
+// KP_RNG_PERMS_INLINE=1: the permutation chain stays on the sequential worker (A/B of
+// where it runs; default: the pool)
+const bool g_perms_inline = std::getenv("KP_RNG_PERMS_INLINE") && std::atoi(std::getenv("KP_RNG_PERMS_INLINE")) == 1;
 
 // torch.randint(high=N) = random() % N and randint(high=2), ratio*R each per epoch;
 // only the first R of each are stepped
@@ -563,10 +575,44 @@ void te_randints(TorchMt& mt, int32_t R, int32_t epochs, int32_t ratio, uint32_t
 // A queued task runs with the worker's scratch (numpy copy, index and draw buffers).
 struct Scratch {
   NumpyMt np;
-  std::vector<int32_t> idx;
+  std::vector<int32_t> idx, jv;
   std::vector<uint32_t> draw;
 };
 using Task = std::function<void(Scratch&)>;
+
+// KP_RNG_STATS=1: per batch (at each kp_rng_wait), the busy time of the walker, the
+// sequential worker and the pool, and when the last task ended relative to the wait
+// call, on stderr (a diagnostic of where a batch's draw time goes; off by default)
+struct RngStats {
+  const bool on = std::getenv("KP_RNG_STATS") != nullptr;
+  std::atomic<int64_t> walk_ns{0}, seq_ns{0}, pool_ns{0}, seq_tasks{0}, pool_tasks{0}, last_end_ns{0},
+      first_start_ns{0};
+  static int64_t now() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+  void span(std::atomic<int64_t>& acc, int64_t t0) {
+    const int64_t t1 = now();
+    acc += t1 - t0;
+    int64_t prev = last_end_ns.load();
+    while (prev < t1 && !last_end_ns.compare_exchange_weak(prev, t1)) {
+    }
+    int64_t z = 0;
+    first_start_ns.compare_exchange_strong(z, t0);
+  }
+  void report(int64_t t_wait) {
+    std::fprintf(stderr,
+                 "[kp_rng] walk %.2f ms | seq %.2f ms (%lld tasks) | pool %.2f ms (%lld tasks) | first task %.2f ms "
+                 "before the wait, last ended %.2f ms after it\n",
+                 walk_ns / 1e6, seq_ns / 1e6, (long long)seq_tasks.load(), pool_ns / 1e6, (long long)pool_tasks.load(),
+                 (t_wait - first_start_ns) / 1e6, (last_end_ns - t_wait) / 1e6);
+    walk_ns = seq_ns = pool_ns = seq_tasks = pool_tasks = last_end_ns = first_start_ns = 0;
+  }
+};
+RngStats& rng_stats() {
+  static RngStats* s = new RngStats();
+  return *s;
+}
 
 class DrawQueue {
  public:
@@ -635,12 +681,18 @@ class DrawQueue {
         q.pop_front();
       }
       int rc = KP_OK;
+      RngStats& st = rng_stats();
+      const int64_t t0 = st.on ? RngStats::now() : 0;
       try {
         t(sc);
       } catch (const std::invalid_argument&) {
         rc = KP_EINVAL;
       } catch (...) {
         rc = KP_ENOMEM;
+      }
+      if (st.on) {
+        st.span(sequential ? st.seq_ns : st.pool_ns, t0);
+        ++(sequential ? st.seq_tasks : st.pool_tasks);
       }
       std::lock_guard<std::mutex> lk(mu_);
       if (rc != KP_OK && fail_rc_ == KP_OK) fail_rc_ = rc;
@@ -665,10 +717,15 @@ int te_enqueue(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_
   const TorchMt snap = mt;
   mt.skip((uint64_t)epochs * 2u * (uint64_t)ratio * (uint64_t)R);
   Task seq = [=](Scratch& sc) {
-    te_draws(np_key, np_pos, R, epochs, out, sc.np);
-    // the permutation chain leaves the sequential worker for the pool
-    if (out && !DrawQueue::get().enqueue(Task(), [=](Scratch& s2) { te_perms(R, epochs, out, s2.idx); }))
-      te_perms(R, epochs, out, sc.idx);
+    if (g_perms_inline || !out) {
+      te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx, sc.jv);
+      return;
+    }
+    // the draws go to the slot's row-order slots of `out` (scratch there) and the
+    // permutation chain leaves the sequential worker for the pool
+    te_draws(np_key, np_pos, R, epochs, out, (size_t)3 * R, sc.np);
+    if (!DrawQueue::get().enqueue(Task(), [=](Scratch& s2) { te_perms(R, epochs, out, (size_t)3 * R, out, s2.idx); }))
+      te_perms(R, epochs, out, (size_t)3 * R, out, sc.idx);
   };
   Task fill;
   if (out)
@@ -755,6 +812,8 @@ class TorchWalker {
         q_.pop_front();
       }
       int rc;
+      RngStats& st = rng_stats();
+      const int64_t t0 = st.on ? RngStats::now() : 0;
       try {
         rc = t(mt_);  // mt_ is only touched here and under mu_ with the queue empty
       } catch (const std::invalid_argument&) {
@@ -762,6 +821,7 @@ class TorchWalker {
       } catch (...) {
         rc = KP_ENOMEM;
       }
+      if (st.on) st.span(st.walk_ns, t0);
       std::lock_guard<std::mutex> lk(mu_);
       if (rc != KP_OK && fail_rc_ == KP_OK) fail_rc_ = rc;
       if (--pending_ == 0) cv_done_.notify_all();
@@ -832,8 +892,8 @@ int kp_rng_transe_epochs(uint8_t* ts, size_t tlen, uint32_t* np_key, int32_t* np
   try {
     auto shuffles = [&] {
       NumpyMt np;
-      std::vector<int32_t> idx;
-      te_shuffles(np_key, np_pos, R, epochs, out, np, idx);
+      std::vector<int32_t> idx, jv;
+      te_shuffles(np_key, np_pos, R, epochs, out, np, idx, jv);
     };
     auto randints = [&] {
       TorchMt mt;
@@ -976,9 +1036,11 @@ int kp_rng_conve_masks_enqueue(uint8_t* ts, size_t tlen, int32_t n_steps, const 
 }
 
 int kp_rng_wait(void) {
+  const int64_t t_wait = rng_stats().on ? RngStats::now() : 0;
   // the torch walks queue draws: they finish first
   const int rw = TorchWalker::get().wait();
   const int rd = DrawQueue::get().wait();
+  if (rng_stats().on) rng_stats().report(t_wait);
   return rw != KP_OK ? rw : rd;
 }
 

@@ -81,7 +81,7 @@ def main():
         dp = time.perf_counter() - t1
         print(f"batch {k}: schedule {dt * 1e3:.2f} ms  final draw wait {sum(waits) * 1e3:.2f} ms  "
               f"pack {dp * 1e3:.2f} ms  kp_rng_transe_calls {sum(calls_t) * 1e3:.2f} ms  slots {len(slots)}  rows {rows}", flush=True)
-    pstats.Stats(prof).sort_stats("tottime").print_stats(16)
+    pstats.Stats(prof).sort_stats(os.environ.get("HP_SORT", "tottime")).print_stats(int(os.environ.get("HP_N", "16")))
 
 
 if __name__ == "__main__":

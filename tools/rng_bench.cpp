@@ -2,7 +2,7 @@
 // the bench's transe-fb15k237-necessary step (289 calls, ~34k rows, 65 epochs, ratio 5):
 // the three chains timed apart (torch-stream walk, numpy shuffles, randint fills) and the
 // whole kp_rng_transe_calls + kp_rng_wait.  Not a test: timing only.
-//   g++ -O3 -std=c++17 -mavx2 -mfma -ffp-contract=off -pthread -Iinclude tools/rng_bench.cpp -o build/rng_bench
+//   g++ -O3 -std=c++17 -mavx2 -mfma -ffp-contract=off -pthread -Iinclude tools/rng_bench.cpp -o variants/rng_bench
 #include "../kelpie_amd/csrc/kp_rng.cpp"
 
 #include <chrono>
@@ -62,26 +62,26 @@ int main(int argc, char** argv) {
     int32_t* o = out.data();
     for (int i = 0; i < n; ++i) {
       if (rb[i] >= 0) {
-        te_draws(key.data(), &pos, rb[i], epochs, o, np);
+        te_draws(key.data(), &pos, rb[i], epochs, o, (size_t)3 * rb[i], np);
         o += (size_t)epochs * 3 * rb[i];
       }
-      te_draws(key.data(), &pos, rp[i], epochs, o, np);
+      te_draws(key.data(), &pos, rp[i], epochs, o, (size_t)3 * rp[i], np);
       o += (size_t)epochs * 3 * rp[i];
     }
     double t4 = now_ms();
     o = out.data();
     for (int i = 0; i < n; ++i) {
       if (rb[i] >= 0) {
-        te_perms(rb[i], epochs, o, idx);
+        te_perms(rb[i], epochs, o, (size_t)3 * rb[i], o, idx);
         o += (size_t)epochs * 3 * rb[i];
       }
-      te_perms(rp[i], epochs, o, idx);
+      te_perms(rp[i], epochs, o, (size_t)3 * rp[i], o, idx);
       o += (size_t)epochs * 3 * rp[i];
     }
     double t4b = now_ms();
     for (int i = 0; i < n; ++i) {
-      if (rb[i] >= 0) te_draws(key.data(), &pos, rb[i], epochs, nullptr, np);
-      te_draws(key.data(), &pos, rp[i], epochs, nullptr, np);
+      if (rb[i] >= 0) te_draws(key.data(), &pos, rb[i], epochs, nullptr, 0, np);
+      te_draws(key.data(), &pos, rp[i], epochs, nullptr, 0, np);
     }
     std::printf("  draws without stores %.2f ms\n", now_ms() - t4b);
     t4b = now_ms();
