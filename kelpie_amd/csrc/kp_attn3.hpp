@@ -89,6 +89,9 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_ASM_ALL
 #define KP_ASM_ALL 0  // 1: the asm read form for every DB (ConvE included)
 #endif
+#ifndef KP_O_NT
+#define KP_O_NT 0  // 1: nontemporal stores of the O partials (A/B)
+#endif
 #ifndef KP_BUF_DMA
 #define KP_BUF_DMA 1  // interleaved schedule: LDS-DMA by buffer_load ... lds with scalar offsets
 #endif
@@ -765,8 +768,14 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         // O^T block m: lane (g, c) holds dims 16 m + 4 g + r of query c
         float* dst = out_O + o * DP;
 #pragma unroll
-        for (int m = 0; m < DB; ++m)
+        for (int m = 0; m < DB; ++m) {
+#if KP_O_NT
+          // streamed past L2: the partials are read once, by the next kernel
+          __builtin_nontemporal_store(O[m], reinterpret_cast<f32x4*>(dst + 16 * m + 4 * g));
+#else
           *reinterpret_cast<float4*>(dst + 16 * m + 4 * g) = make_float4(O[m][0], O[m][1], O[m][2], O[m][3]);
+#endif
+        }
       }
     }
     if (fill_rest && valid) {

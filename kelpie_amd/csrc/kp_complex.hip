@@ -55,6 +55,22 @@ __global__ void kp_cx_qpair(const float* __restrict__ E, const float* __restrict
   for (int d = threadIdx.x; d < dp; d += blockDim.x) out[(size_t)p * dp + d] = cx_q(lhs, rel, d, half);
 }
 
+// lsef[p] = the frozen-head pair's log-sum-exp over the frozen entities, merged from the
+// attention's split statistics (one thread per pair; fp64 sum of the rescaled l's)
+__global__ void kp_cx_lse_merge(int npairs, int n_split, const float* __restrict__ am, const float* __restrict__ al,
+                                float* __restrict__ lsef) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npairs) return;
+  float mm = kNegInf;
+  for (int s = 0; s < n_split; ++s) mm = fmaxf(mm, am[(size_t)s * npairs + p]);
+  double ll = 0.0;
+  for (int s = 0; s < n_split; ++s) {
+    const float ms = am[(size_t)s * npairs + p];
+    if (ms != kNegInf) ll += (double)al[(size_t)s * npairs + p] * exp((double)ms - (double)mm);
+  }
+  lsef[p] = (float)((double)mm + log(ll));
+}
+
 // Tsum[q] = sum of frozen target rows of a plan query
 __global__ void kp_cx_tsum(const float* __restrict__ E, int dp, const CxQuery* __restrict__ pq, int nq,
                            const int32_t* __restrict__ targets, float* __restrict__ tsum) {
@@ -655,23 +671,10 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
                        dQpair);
     KP_HIP(hipGetLastError());
     CX_DISPATCH(DBV, launch_attn<DB>(c, false, dQpair, npairs, plan_pairs, dAm, dAl, nullptr));
-    // combine splits into lsef (host-free: small kernel via update-style math on host is avoided)
-    std::vector<float> hm((size_t)npairs * split_pairs), hl((size_t)npairs * split_pairs);
-    KP_HIP(hipMemcpyAsync(hm.data(), dAm, sizeof(float) * hm.size(), hipMemcpyDeviceToHost, c->stream));
-    KP_HIP(hipMemcpyAsync(hl.data(), dAl, sizeof(float) * hl.size(), hipMemcpyDeviceToHost, c->stream));
-    KP_HIP(hipStreamSynchronize(c->stream));
-    std::vector<float> lse(npairs);
-    for (int p = 0; p < npairs; ++p) {
-      float mm = -INFINITY;
-      for (int s = 0; s < split_pairs; ++s) mm = std::max(mm, hm[(size_t)s * npairs + p]);
-      double ll = 0;
-      for (int s = 0; s < split_pairs; ++s) {
-        float ms = hm[(size_t)s * npairs + p];
-        if (ms != -INFINITY) ll += (double)hl[(size_t)s * npairs + p] * std::exp((double)ms - mm);
-      }
-      lse[p] = (float)(mm + std::log(ll));
-    }
-    KP_HIP(hipMemcpyAsync(dLsef, lse.data(), sizeof(float) * npairs, hipMemcpyHostToDevice, c->stream));
+    // combine the splits into lsef on the device (no host round trip inside the batch)
+    hipLaunchKernelGGL(kp_cx_lse_merge, dim3((npairs + 255) / 256), dim3(256), 0, c->stream, npairs, split_pairs, dAm,
+                       dAl, dLsef);
+    KP_HIP(hipGetLastError());
   }
 
   // ---- the epoch/step loop

@@ -176,6 +176,24 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
       if (ck[b][3] > ck[b][1]) f.push_back((double)(ck[b][2] - ck[b][0]) / (double)(ck[b][3] - ck[b][1]) * 0.1);
     std::sort(f.begin(), f.end());
     const double med = f.empty() ? 0.0 : f[f.size() / 2];
+    // workgroup spans on the 100 MHz clock: when they start and end relative to the first
+    // start, and how long each runs (the launch's ms covers all of it plus the launch)
+    unsigned long long t0 = ~0ull, t1 = 0;
+    std::vector<double> dur, st;
+    for (int b = 0; b < std::min(plan.n_wg, 4096); ++b)
+      if (ck[b][3] > ck[b][1]) {
+        t0 = std::min(t0, ck[b][1]);
+        t1 = std::max(t1, ck[b][3]);
+        dur.push_back((ck[b][3] - ck[b][1]) * 0.01);
+      }
+    for (int b = 0; b < std::min(plan.n_wg, 4096); ++b)
+      if (ck[b][3] > ck[b][1]) st.push_back((ck[b][1] - t0) * 0.01);
+    std::sort(dur.begin(), dur.end());
+    std::sort(st.begin(), st.end());
+    if (!dur.empty())
+      printf("{\"wg_us_min\": %.1f, \"wg_us_median\": %.1f, \"wg_us_max\": %.1f, \"start_spread_us\": %.1f, "
+             "\"first_start_to_last_end_us\": %.1f}\n", dur.front(), dur[dur.size() / 2], dur.back(), st.back(),
+             (t1 - t0) * 0.01);
     printf("{\"clock_ghz_median\": %.4f, \"clock_ghz_min\": %.4f, \"clock_ghz_max\": %.4f, \"workgroups\": %zu, "
            "\"warm_launches\": %d}\n", med, f.empty() ? 0.0 : f.front(), f.empty() ? 0.0 : f.back(), f.size(), warm);
   }
