@@ -324,10 +324,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
       if ((k * NSLOT) / NPW == slot) issue_piece(tile, buf, k);
   };
 #ifdef KP_ATTN3_CLOCK
-  if (tid == 0 && blockIdx.x < 4096) {
-    g_attn3_clock[blockIdx.x][0] = __builtin_amdgcn_s_memtime();
-    g_attn3_clock[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
-  }
+  // stamped first thing (the asm's memory clobber keeps every load after it)
+  unsigned long long ck_t0, ck_r0;
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(ck_t0), "=s"(ck_r0)::"memory");
 #endif
   const int QT = (nq + 63) / 64;
   // work segments: stream-K ranges (wk.ranges == 0) or XCD-grouped units (attn_plan_ranges)
@@ -797,9 +796,17 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
     for (int i = 0; i < 5; ++i) atomicAdd(&g_attn3_stamps[i], st_acc[i]);
 #endif
 #ifdef KP_ATTN3_CLOCK
-  if (tid == 0 && blockIdx.x < 4096) {
-    g_attn3_clock[blockIdx.x][2] = __builtin_amdgcn_s_memtime();
-    g_attn3_clock[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+  {
+    // stamped last, after this wave's stores have completed
+    unsigned long long ck_t1, ck_r1;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(ck_t1), "=s"(ck_r1)::"memory");
+    if (tid == 0 && blockIdx.x < 4096) {
+      g_attn3_clock[blockIdx.x][0] = ck_t0;
+      g_attn3_clock[blockIdx.x][1] = ck_r0;
+      g_attn3_clock[blockIdx.x][2] = ck_t1;
+      g_attn3_clock[blockIdx.x][3] = ck_r1;
+    }
   }
 #endif
 }

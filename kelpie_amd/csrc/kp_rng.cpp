@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -721,11 +722,14 @@ int te_enqueue(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_
       te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx, sc.jv);
       return;
     }
-    // the draws go to the slot's row-order slots of `out` (scratch there) and the
-    // permutation chain leaves the sequential worker for the pool
-    te_draws(np_key, np_pos, R, epochs, out, (size_t)3 * R, sc.np);
-    if (!DrawQueue::get().enqueue(Task(), [=](Scratch& s2) { te_perms(R, epochs, out, (size_t)3 * R, out, s2.idx); }))
-      te_perms(R, epochs, out, (size_t)3 * R, out, sc.idx);
+    // the draws go to a buffer of their own in ordinary memory (`out` may be page-locked
+    // memory, where the scattered stores of the draw loop ran ~1.5x slower on the box) and
+    // the permutation chain, which streams whole rows into `out`, leaves the sequential
+    // worker for the pool
+    auto jv = std::make_shared<std::vector<int32_t>>((size_t)R * (size_t)epochs);
+    te_draws(np_key, np_pos, R, epochs, jv->data(), (size_t)R, sc.np);
+    if (!DrawQueue::get().enqueue(Task(), [=](Scratch& s2) { te_perms(R, epochs, jv->data(), (size_t)R, out, s2.idx); }))
+      te_perms(R, epochs, jv->data(), (size_t)R, out, sc.idx);
   };
   Task fill;
   if (out)
