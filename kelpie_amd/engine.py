@@ -536,6 +536,13 @@ class PostTrainingEngine(RelevanceEngine):
         if depth is None:
             depth = int(os.environ.get("KELPIE_PIPELINE_DEPTH", "2"))
         ctxs = self.model.contexts(max(1, depth))
+        # The scheduling thread and the batch threads' packing share the interpreter lock;
+        # KELPIE_GIL_SWITCH_US shortens the interpreter's switch interval while the
+        # pipeline runs (A/B switch; unset: the interpreter's default)
+        import sys
+        old_switch = sys.getswitchinterval()
+        if os.environ.get("KELPIE_GIL_SWITCH_US"):
+            sys.setswitchinterval(float(os.environ["KELPIE_GIL_SWITCH_US"]) * 1e-6)
 
         def run(state):
             try:
@@ -583,6 +590,7 @@ class PostTrainingEngine(RelevanceEngine):
         finally:
             for st in inflight:  # an earlier batch raised: let the others' device work end
                 st["thread"].join()
+            sys.setswitchinterval(old_switch)
         self.last_batch_stats = stats
         return outs
 

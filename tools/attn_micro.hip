@@ -21,6 +21,12 @@
 
 using namespace kpattn;
 
+// an empty kernel with kp_attn3's launch shape (KP_MICRO_EMPTY=1): the dispatch cost alone
+__global__ __launch_bounds__(256, 1) void kp_empty(int* sink) {
+  extern __shared__ int lds_e[];
+  if (threadIdx.x == 1023) sink[blockIdx.x] = lds_e[0];
+}
+
 template <int DB, int MODE>
 static int run(int n_ent, int nq, int iters, float scale, int part) {
   constexpr int DP = 16 * DB;
@@ -71,6 +77,24 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
     (void)use4;
     launch_attn3<DB, MODE>(&c, n_ent, dQ, nq, plan, dm, dl, dO, dqs, ylo);
   };
+  if (std::getenv("KP_MICRO_EMPTY")) {
+    int* sink;
+    KP_HIP(hipMalloc(&sink, 4 * 4096));
+    for (int rep = 0; rep < 2; ++rep) {
+      hipEvent_t a, b;
+      KP_HIP(hipEventCreate(&a));
+      KP_HIP(hipEventCreate(&b));
+      KP_HIP(hipEventRecord(a, c.stream));
+      for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL(kp_empty, dim3(plan.n_wg), dim3(256), attn3_lds_bytes(DB), c.stream, sink);
+      KP_HIP(hipEventRecord(b, c.stream));
+      KP_HIP(hipEventSynchronize(b));
+      float ems = 0.f;
+      KP_HIP(hipEventElapsedTime(&ems, a, b));
+      printf("{\"empty_kernel_us_per_launch\": %.2f, \"n_wg\": %d, \"lds\": %zu}\n", 1e3 * ems / iters, plan.n_wg,
+             attn3_lds_bytes(DB));
+    }
+  }
   launch();
   KP_HIP(hipStreamSynchronize(c.stream));
   hipEvent_t e0, e1;
