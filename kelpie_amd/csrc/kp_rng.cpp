@@ -183,6 +183,24 @@ struct TorchMt {
 // This file is compiled with -ffp-contract=off: every fused operation below is an
 // explicit fmadd.
 // ---------------------------------------------------------------------------------
+// v_log / v_sincos below are an altered restatement of log256_ps / sincos256_ps from
+// avx_mathfun.h (the AVX port by Giovanni Garberoglio, 2012, of sse_mathfun.h by Julien
+// Pommier, 2007; Cephes polynomials), which torch's CPU normal_ uses.  Their notice
+// (the zlib license):
+//   This software is provided 'as-is', without any express or implied warranty.  In no
+//   event will the authors be held liable for any damages arising from the use of this
+//   software.  Permission is granted to anyone to use this software for any purpose,
+//   including commercial applications, and to alter it and redistribute it freely,
+//   subject to the following restrictions:
+//   1. The origin of this software must not be misrepresented; you must not claim that
+//      you wrote the original software.  If you use this software in a product, an
+//      acknowledgment in the product documentation would be appreciated but is not
+//      required.
+//   2. Altered source versions must be plainly marked as such, and must not be
+//      misrepresented as being the original software.
+//   3. This notice may not be removed or altered from any source distribution.
+// Altered here: every multiply that feeds an add is an explicit fmadd, as torch's build
+// contracts them.
 // avx_mathfun's log256_ps and sincos256_ps as torch's AVX2 build runs them: each
 // multiply that feeds an add fused (an explicit fmadd; the rest stay separate, and this
 // file is built with -ffp-contract=off so nothing else is fused)
