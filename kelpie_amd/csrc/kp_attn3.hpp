@@ -71,7 +71,7 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 // KP_DIAGNOSTIC_BUILD, which `make diag` sets for the variants/ libraries; the product
 // library can never carry one by a stray define.
 #if (defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O) || defined(KP_ATTN_NODMA) || defined(KP_DIAG_DMA_LGKM0) || \
-     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE)) && \
+     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE) || defined(KP_DIAG_NO_OSTORE)) && \
     !defined(KP_DIAGNOSTIC_BUILD)
 #error "kp_attn3 diagnostic define without KP_DIAGNOSTIC_BUILD (these builds compute wrong results: make diag)"
 #endif
@@ -763,7 +763,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         out_m[o] = m_ref;
         out_l[o] = l_tot;
       }
+#ifdef KP_DIAG_NO_OSTORE
+      if (false) {  // diagnostic: the O partials are not written (wrong results)
+#else
       if (WITH_O) {
+#endif
         // O^T block m: lane (g, c) holds dims 16 m + 4 g + r of query c
         float* dst = out_O + o * DP;
 #pragma unroll
