@@ -92,6 +92,9 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_O_NT
 #define KP_O_NT 0  // 1: nontemporal stores of the O partials (A/B)
 #endif
+#ifndef KP_O_SC1
+#define KP_O_SC1 0  // 1: write-through (sc1) buffer stores of the O partials (A/B)
+#endif
 #ifndef KP_BUF_DMA
 #define KP_BUF_DMA 1  // interleaved schedule: LDS-DMA by buffer_load ... lds with scalar offsets
 #endif
@@ -279,6 +282,10 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   // everything that varies per piece is scalar (soffset, M0): no VALU per piece
   const __amdgpu_buffer_rsrc_t e3rsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(E3), (short)0, (int)((n_ent + 31) / 32 * 32 * ROW_B + 1024), 0x00020000);
+#if KP_O_SC1
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(out_O, (short)0, 0x7FFFFFFF, 0x00020000);
+#endif
   auto bdma = [&](int tile, int buf, int p) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         e3rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)), 16,
@@ -772,7 +779,13 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         float* dst = out_O + o * DP;
 #pragma unroll
         for (int m = 0; m < DB; ++m) {
-#if KP_O_NT
+#if KP_O_SC1
+          // write-through (sc1): the lines leave L2 as they are written instead of at the
+          // kernel's end (the partials are read once, by the next kernel, on any XCD)
+          typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, O[m]), orsrc,
+                                                 (int)((o * DP + 16 * m + 4 * g) * sizeof(float)), 0, 16);
+#elif KP_O_NT
           // streamed past L2: the partials are read once, by the next kernel
           __builtin_nontemporal_store(O[m], reinterpret_cast<f32x4*>(dst + 16 * m + 4 * g));
 #else
