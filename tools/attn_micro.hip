@@ -21,6 +21,21 @@
 
 using namespace kpattn;
 
+// s_memrealtime calibration (KP_MICRO_RTCAL=1): one wave spins until the counter has
+// advanced by `ticks` (bounded by an iteration cap), timed by HIP events on the host side
+__global__ void kp_rtcal(unsigned long long ticks, unsigned long long* out) {
+  unsigned long long r0, t0, r1 = 0, t1 = 0;
+  asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(r0), "=s"(t0)::"memory");
+  for (long long it = 0; it < (1LL << 32); ++it) {
+    asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1), "=s"(t1)::"memory");
+    if (r1 - r0 >= ticks) break;
+  }
+  if (threadIdx.x == 0) {
+    out[0] = r1 - r0;
+    out[1] = t1 - t0;
+  }
+}
+
 // an empty kernel with kp_attn3's launch shape (KP_MICRO_EMPTY=1): the dispatch cost alone
 __global__ __launch_bounds__(256, 1) void kp_empty(int* sink) {
   extern __shared__ int lds_e[];
@@ -77,6 +92,25 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
     (void)use4;
     launch_attn3<DB, MODE>(&c, n_ent, dQ, nq, plan, dm, dl, dO, dqs, ylo);
   };
+  if (std::getenv("KP_MICRO_RTCAL")) {
+    unsigned long long* dout;
+    KP_HIP(hipMalloc(&dout, 16));
+    for (unsigned long long ticks : {1000000ull, 10000000ull}) {
+      hipEvent_t a, b;
+      KP_HIP(hipEventCreate(&a));
+      KP_HIP(hipEventCreate(&b));
+      KP_HIP(hipEventRecord(a, c.stream));
+      hipLaunchKernelGGL(kp_rtcal, dim3(1), dim3(64), 0, c.stream, ticks, dout);
+      KP_HIP(hipEventRecord(b, c.stream));
+      KP_HIP(hipEventSynchronize(b));
+      float ems = 0.f;
+      KP_HIP(hipEventElapsedTime(&ems, a, b));
+      unsigned long long h[2];
+      KP_HIP(hipMemcpy(h, dout, 16, hipMemcpyDeviceToHost));
+      printf("{\"rtcal_ticks\": %llu, \"memtime_ticks\": %llu, \"event_ms\": %.4f, \"realtime_mhz\": %.3f, "
+             "\"idle_wave_clock_ghz\": %.4f}\n", h[0], h[1], ems, h[0] / (ems * 1e3), h[1] / (ems * 1e6));
+    }
+  }
   if (std::getenv("KP_MICRO_EMPTY")) {
     int* sink;
     KP_HIP(hipMalloc(&sink, 4 * 4096));
