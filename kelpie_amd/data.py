@@ -18,6 +18,7 @@ the kelpie entity, which is everything the post-training rank reads.
 from __future__ import annotations
 
 import csv
+import itertools
 import os
 from collections import Counter, defaultdict
 
@@ -243,12 +244,28 @@ class KelpieView:
         self.kelpie_entity = dataset.num_entities
         self.num_entities = dataset.num_entities + 1
         k, s = self.kelpie_entity, self.original_entity
-        rep = Dataset.replace_entity_in_triple
-        self.base_triples = [rep(t, s, k) for t in dataset.entity_to_training_triples.get(s, [])]
-        self.base_arr = np.asarray(self.base_triples, dtype=np.int32).reshape(-1, 3)
-        self.n_base_rows = 2 * len(self.base_triples)
+        # the entity's training triples as they are now (a snapshot: the dataset may be
+        # edited later), as an int32 array with the original entity replaced; the list of
+        # tuples (base_triples) is built on first use -- the TransE scheduler never needs it
+        self._src = list(dataset.entity_to_training_triples.get(s, []))
+        arr = np.fromiter(itertools.chain.from_iterable(self._src), dtype=np.int32,
+                          count=3 * len(self._src)).reshape(-1, 3)
+        arr[arr[:, 0] == s, 0] = k
+        arr[arr[:, 2] == s, 2] = k
+        self.base_arr = arr
+        self.n_base_rows = 2 * len(self._src)
+        self._base_triples = None
         self._filter = self._index = self._base_rows = self._native = None
         self._filter_lists = {}  # rel -> filter_for(rel) without a delta (shared: callers copy or only read)
+
+    @property
+    def base_triples(self):
+        """The kelpie entity's training triples (tuples, the dataset's order)."""
+        if self._base_triples is None:
+            k, s = self.kelpie_entity, self.original_entity
+            rep = Dataset.replace_entity_in_triple
+            self._base_triples = [rep(t, s, k) for t in self._src]
+        return self._base_triples
 
     def _other_triples(self):
         """The kelpie entity's validation and test triples (they only enter the filters)."""

@@ -282,7 +282,7 @@ class PostTrainingEngine(RelevanceEngine):
             slots.append(base)
         pt = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_pt)
         slots.append(pt)
-        self._fused.append({"view": view, "kp": kp, "triples": [tuple(int(v) for v in t) for t in triples],
+        self._fused.append({"view": view, "kp": kp, "triples": [(int(a), int(b), int(c)) for a, b, c in triples],
                             "flags": (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
                             | (8 if mode == "sufficient" else 0), "base": base, "pt": pt})
         if len(self._fused) >= self._FUSED_FLUSH:
