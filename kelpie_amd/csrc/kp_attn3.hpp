@@ -71,7 +71,7 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 // KP_DIAGNOSTIC_BUILD, which `make diag` sets for the variants/ libraries; the product
 // library can never carry one by a stray define.
 #if (defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O) || defined(KP_ATTN_NODMA) || defined(KP_DIAG_DMA_LGKM0) || \
-     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE) || defined(KP_DIAG_NO_OSTORE)) && \
+     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE) || defined(KP_DIAG_NO_OSTORE) || defined(KP_DIAG_EARLY_EXIT)) && \
     !defined(KP_DIAGNOSTIC_BUILD)
 #error "kp_attn3 diagnostic define without KP_DIAGNOSTIC_BUILD (these builds compute wrong results: make diag)"
 #endif
@@ -265,6 +265,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   extern __shared__ __attribute__((aligned(16))) uint8_t lds3[];  // [2][BUF_B]
 
   const int tid = threadIdx.x;
+#ifdef KP_DIAG_EARLY_EXIT
+  // diagnostic: every workgroup leaves at once (same registers and LDS: the code below
+  // stays reachable for a value the caller never passes), so a launch costs its dispatch
+  if (ylo != 12345.f) return;
+#endif
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;

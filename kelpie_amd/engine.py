@@ -285,13 +285,15 @@ class PostTrainingEngine(RelevanceEngine):
         self._fused.append({"view": view, "kp": kp, "triples": [(int(a), int(b), int(c)) for a, b, c in triples],
                             "flags": (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
                             | (8 if mode == "sufficient" else 0), "base": base, "pt": pt})
-        if len(self._fused) >= self._FUSED_FLUSH:
+        if len(self._fused) >= (self._FUSED_FLUSH if self._sched is not None else self._FUSED_FIRST):
             # hand the draws to the library's workers early: their numpy shuffles then run
-            # while this thread queues the next calls
+            # while this thread queues the next calls (the batch's first flush sooner, so
+            # the sequential numpy chain starts right away)
             self._flush_fused()
         return len(slots) - 1, pred
 
     _FUSED_FLUSH = 24  # queued TransE calls per library call
+    _FUSED_FIRST = 4  # ... for a batch's first one
 
     @staticmethod
     def _edit_error(call, code, k):
