@@ -447,7 +447,7 @@ def main():
         eng.sharding = None  # rank 0 alone: no collective on this path
         pred, cands_s, ents, parity = parity_sample(eng, wl, fixture, (pred, cands, ents))
         log(f"[rank 0] parity sample vs reference: {json.dumps(parity)}")
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 number
             n_cpu = 5  # the first candidate (with the prediction's base post-trainings) + 4 steady
             cpu_cands = (cands_s + [c for c in candidates_of(ds, pred, wl["candidates"]) if c not in cands_s])[:n_cpu]
             try:
