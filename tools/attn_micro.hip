@@ -36,6 +36,34 @@ __global__ void kp_rtcal(unsigned long long ticks, unsigned long long* out) {
   }
 }
 
+// a pure-MFMA kernel (KP_MICRO_MFMA=1): every wave runs `iters` dependent chains of
+// v_mfma_f32_16x16x32_bf16 on register operands, no memory traffic but the final store;
+// thread 0 of each workgroup stamps its start and end (100 MHz realtime) like the clock build
+__global__ __launch_bounds__(256, 1) void kp_mfma_spin(int iters, float* out, unsigned long long* st) {
+  unsigned long long r0;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r0)::"memory");
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  b8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)(0.001f * (threadIdx.x + j));
+    b[j] = (__bf16)(0.002f * (blockIdx.x + j));
+  }
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c3, 0, 0, 0);
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3];
+  unsigned long long r1;
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+  if (threadIdx.x == 0) {
+    st[2 * blockIdx.x] = r0;
+    st[2 * blockIdx.x + 1] = r1;
+  }
+}
+
 // an empty kernel with kp_attn3's launch shape (KP_MICRO_EMPTY=1): the dispatch cost alone
 __global__ __launch_bounds__(256, 1) void kp_empty(int* sink) {
   extern __shared__ int lds_e[];
@@ -109,6 +137,33 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
       KP_HIP(hipMemcpy(h, dout, 16, hipMemcpyDeviceToHost));
       printf("{\"rtcal_ticks\": %llu, \"memtime_ticks\": %llu, \"event_ms\": %.4f, \"realtime_mhz\": %.3f, "
              "\"idle_wave_clock_ghz\": %.4f}\n", h[0], h[1], ems, h[0] / (ems * 1e3), h[1] / (ems * 1e6));
+    }
+  }
+  if (std::getenv("KP_MICRO_MFMA")) {
+    float* dout;
+    unsigned long long* dst;
+    KP_HIP(hipMalloc(&dout, 4 * 256 * 256));
+    KP_HIP(hipMalloc(&dst, 16 * 256));
+    for (int it : {4000, 8000, 16000}) {
+      for (int w = 0; w < 20; ++w) hipLaunchKernelGGL(kp_mfma_spin, dim3(256), dim3(256), 0, c.stream, it, dout, dst);
+      hipEvent_t a, b;
+      KP_HIP(hipEventCreate(&a));
+      KP_HIP(hipEventCreate(&b));
+      KP_HIP(hipEventRecord(a, c.stream));
+      for (int i = 0; i < 30; ++i) hipLaunchKernelGGL(kp_mfma_spin, dim3(256), dim3(256), 0, c.stream, it, dout, dst);
+      KP_HIP(hipEventRecord(b, c.stream));
+      KP_HIP(hipEventSynchronize(b));
+      float ems = 0.f;
+      KP_HIP(hipEventElapsedTime(&ems, a, b));
+      std::vector<unsigned long long> h(512);
+      KP_HIP(hipMemcpy(h.data(), dst, 16 * 256, hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (int i = 0; i < 256; ++i) {
+        t0 = std::min(t0, h[2 * i]);
+        t1 = std::max(t1, h[2 * i + 1]);
+      }
+      printf("{\"mfma_spin_iters\": %d, \"us_per_launch\": %.1f, \"wg_span_us\": %.1f}\n", it, 1e3 * ems / 30,
+             (t1 - t0) * 0.01);
     }
   }
   if (std::getenv("KP_MICRO_EMPTY")) {
