@@ -64,6 +64,51 @@ __global__ __launch_bounds__(256, 1) void kp_mfma_spin(int iters, float* out, un
   }
 }
 
+// the pure-MFMA kernel plus the attention's other traffic (KP_MICRO_MFMA2=1): MODE bit 0 =
+// two ds_read_b128 of the dynamic LDS per four MFMAs, bit 1 = one 16-B global load per four
+// MFMAs streaming through a 35 MB buffer; the loaded values feed the next MFMA operands
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void kp_mfma_spin2(int iters, const uint4* __restrict__ buf, long long nbuf,
+                                                         float* out, unsigned long long* st) {
+  extern __shared__ uint4 lds_s[];
+  unsigned long long r0;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r0)::"memory");
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  b8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)(0.001f * (threadIdx.x + j));
+    b[j] = (__bf16)(0.002f * (blockIdx.x + j));
+  }
+  for (int i = threadIdx.x; i < 9728; i += 256) lds_s[i] = make_uint4(i, i + 1, i + 2, i + 3);
+  __syncthreads();
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+  long long g = (long long)blockIdx.x * 4096 + threadIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    if (MODE & 1) {
+      const uint4 x = lds_s[(threadIdx.x + 64 * (i & 127)) % 9728];
+      const uint4 y = lds_s[(threadIdx.x + 64 * ((i + 37) & 127) + 4800) % 9728];
+      a = __builtin_bit_cast(b8, x);
+      b = __builtin_bit_cast(b8, y);
+    }
+    if (MODE & 2) {
+      const uint4 z = buf[g % nbuf];
+      g += 256 * 248;
+      a = __builtin_bit_cast(b8, __builtin_bit_cast(uint4, a) ^ z);
+    }
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c3, 0, 0, 0);
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3];
+  unsigned long long r1;
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+  if (threadIdx.x == 0) {
+    st[2 * blockIdx.x] = r0;
+    st[2 * blockIdx.x + 1] = r1;
+  }
+}
+
 // an empty kernel with kp_attn3's launch shape (KP_MICRO_EMPTY=1): the dispatch cost alone
 __global__ __launch_bounds__(256, 1) void kp_empty(int* sink) {
   extern __shared__ int lds_e[];
@@ -164,6 +209,44 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
       }
       printf("{\"mfma_spin_iters\": %d, \"us_per_launch\": %.1f, \"wg_span_us\": %.1f}\n", it, 1e3 * ems / 30,
              (t1 - t0) * 0.01);
+    }
+  }
+  if (std::getenv("KP_MICRO_MFMA2")) {
+    float* dout;
+    unsigned long long* dst;
+    uint4* dbuf;
+    const long long nbuf = 35LL * 1024 * 1024 / 16;
+    KP_HIP(hipMalloc(&dout, 4 * 256 * 256));
+    KP_HIP(hipMalloc(&dst, 16 * 256));
+    KP_HIP(hipMalloc(&dbuf, 16 * nbuf));
+    KP_HIP(hipMemset(dbuf, 1, 16 * nbuf));
+    for (int mode = 0; mode < 4; ++mode) {
+      auto go = [&](int it) {
+        if (mode == 0) hipLaunchKernelGGL(kp_mfma_spin2<0>, dim3(248), dim3(256), 155648, c.stream, it, dbuf, nbuf, dout, dst);
+        if (mode == 1) hipLaunchKernelGGL(kp_mfma_spin2<1>, dim3(248), dim3(256), 155648, c.stream, it, dbuf, nbuf, dout, dst);
+        if (mode == 2) hipLaunchKernelGGL(kp_mfma_spin2<2>, dim3(248), dim3(256), 155648, c.stream, it, dbuf, nbuf, dout, dst);
+        if (mode == 3) hipLaunchKernelGGL(kp_mfma_spin2<3>, dim3(248), dim3(256), 155648, c.stream, it, dbuf, nbuf, dout, dst);
+      };
+      const int it = 8000;
+      for (int w = 0; w < 20; ++w) go(it);
+      hipEvent_t a, b;
+      KP_HIP(hipEventCreate(&a));
+      KP_HIP(hipEventCreate(&b));
+      KP_HIP(hipEventRecord(a, c.stream));
+      for (int i = 0; i < 30; ++i) go(it);
+      KP_HIP(hipEventRecord(b, c.stream));
+      KP_HIP(hipEventSynchronize(b));
+      float ems = 0.f;
+      KP_HIP(hipEventElapsedTime(&ems, a, b));
+      std::vector<unsigned long long> h(512);
+      KP_HIP(hipMemcpy(h.data(), dst, 16 * 248, hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (int i = 0; i < 248; ++i) {
+        t0 = std::min(t0, h[2 * i]);
+        t1 = std::max(t1, h[2 * i + 1]);
+      }
+      printf("{\"mfma_spin2_mode\": %d, \"iters\": %d, \"us_per_launch\": %.1f, \"wg_span_us\": %.1f}\n", mode, it,
+             1e3 * ems / 30, (t1 - t0) * 0.01);
     }
   }
   if (std::getenv("KP_MICRO_EMPTY")) {
@@ -282,6 +365,22 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
     const int warm = std::max(1, (int)(2000.0 / std::max(ms, 1e-3f)));
     for (int i = 0; i < warm; ++i) launch();
     KP_HIP(hipStreamSynchronize(c.stream));
+    {
+      // the per-launch time again, now with the clock settled (the first timing above
+      // starts a few launches after the GPU left idle)
+      hipEvent_t a, b;
+      KP_HIP(hipEventCreate(&a));
+      KP_HIP(hipEventCreate(&b));
+      KP_HIP(hipEventRecord(a, c.stream));
+      for (int i = 0; i < iters; ++i) launch();
+      KP_HIP(hipEventRecord(b, c.stream));
+      KP_HIP(hipEventSynchronize(b));
+      float wms = 0.f;
+      KP_HIP(hipEventElapsedTime(&wms, a, b));
+      printf("{\"ms_after_warmup\": %.5f, \"tflops_after_warmup\": %.2f}\n", wms / iters, flops / (wms / iters) / 1e9);
+      launch();  // the stamped launch
+      KP_HIP(hipStreamSynchronize(c.stream));
+    }
     static unsigned long long ck[4096][4];
     KP_HIP(hipMemcpyFromSymbol(ck, HIP_SYMBOL(g_attn3_clock), sizeof(ck)));
     std::vector<double> f;
