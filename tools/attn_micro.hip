@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <chrono>
 #include <random>
 
 #include "kp_attn3.hpp"  // -I selects the source tree under test (tools/attn_micro.sh)
@@ -272,7 +273,15 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
   hipEvent_t e0, e1;
   KP_HIP(hipEventCreate(&e0));
   KP_HIP(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) launch();
+  // >= 1 s of back-to-back launches first: the first ~10 ms of work after the GPU leaves
+  // idle run below the settled clock (profiles/r03zx_attn_warm_vs_spans.jsonl)
+  {
+    const auto w0 = std::chrono::steady_clock::now();
+    while (std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count() < 1.0) {
+      for (int i = 0; i < 20; ++i) launch();
+      KP_HIP(hipStreamSynchronize(c.stream));
+    }
+  }
   KP_HIP(hipEventRecord(e0, c.stream));
   for (int i = 0; i < iters; ++i) launch();
   KP_HIP(hipEventRecord(e1, c.stream));
