@@ -11,7 +11,7 @@ LIB := kelpie_amd/libkelpie_hip.so
 
 all: $(LIB)
 
-build/%.o: kelpie_amd/csrc/%.hip kelpie_amd/csrc/kp_common.hpp kelpie_amd/csrc/kp_attn.hpp kelpie_amd/csrc/kp_attn3.hpp kelpie_amd/csrc/kp_cv_fused.hpp include/kelpie_hip.h
+build/%.o: kelpie_amd/csrc/%.hip kelpie_amd/csrc/kp_common.hpp kelpie_amd/csrc/kp_attn.hpp kelpie_amd/csrc/kp_attn3.hpp kelpie_amd/csrc/kp_cv_fused.hpp kelpie_amd/csrc/kp_attn5.hpp include/kelpie_hip.h
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) -c $< -o $@
 

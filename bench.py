@@ -29,6 +29,7 @@ the 1-rank run.  Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -485,6 +486,8 @@ def main():
                 "rank_delta_match_rate_ref_fp64": (parity.get("fp64") or {}).get("match_rate"),
                 "rank_delta_max_abs_diff_ref_fp64": (parity.get("fp64") or {}).get("max_abs_diff"),
                 "reference_fp32_vs_fp64_max_abs_diff": parity.get("reference_fp32_vs_fp64_max_abs_diff"),
+                # the timed steps' relevances, bit for bit (A/B runs of two builds compare it)
+                "results_sha16": hashlib.sha256(np.asarray([r[0] for r in recs], np.float64).tobytes()).hexdigest()[:16],
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
 

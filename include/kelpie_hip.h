@@ -38,6 +38,9 @@ extern "C" {
 #define KP_ENOMEM (-12)
 #define KP_EDEVICE (-5)
 #define KP_ENOTSUP (-95)
+/* kp_rng_transe_calls_async only: no walker thread could start, so the walk ran inline
+ * on the caller's thread; torch_state then holds the advanced stream (not an error) */
+#define KP_INLINE 1
 
 /* model families (src/link_prediction/__init__.py:5-9, MODEL_REGISTRY) */
 #define KP_MODEL_TRANSE 0
@@ -84,6 +87,8 @@ typedef struct {
   int32_t neg_ratio;     /* TransE negative_triples_ratio */
   float label_smoothing; /* ConvE */
   float hidden_dropout;  /* ConvE hidden dropout rate (masks are inputs) */
+  float input_dropout;   /* ConvE input dropout rate (conve.py:142) */
+  float fmap_dropout;    /* ConvE feature-map Dropout2d rate (conve.py:147) */
 } kp_hp;
 
 /* One batch of post-training slots.  A slot is one KelpieModel post-training
@@ -301,7 +306,8 @@ int kp_rng_transe_calls(uint8_t* torch_state, size_t torch_len, uint32_t* np_key
  * torch_state unless an earlier asynchronous walk still carries the stream (it then
  * continues that one and torch_state is not read); kp_rng_torch_take hands the stream
  * back.  Lets the scheduling thread queue calls while the generator is advanced past
- * their draws (the randint outputs alone are ~22 M words per TransE batch). */
+ * their draws (the randint outputs alone are ~22 M words per TransE batch).  Returns
+ * KP_OK when queued, KP_INLINE when it walked inline (then nothing is carried). */
 int kp_rng_transe_calls_async(const uint8_t* torch_state, size_t torch_len, uint32_t* np_key, int32_t* np_pos,
                               int32_t normal_cap, int32_t D, int32_t d, float xavier_std, int32_t n,
                               const int32_t* R_base, const int32_t* R_pt, const uint8_t* want, int32_t epochs,
@@ -314,16 +320,21 @@ int kp_rng_torch_take(uint8_t* torch_state, size_t torch_len, int32_t* taken);
 /* Block until every slot queued by kp_rng_transe_enqueue is written. */
 int kp_rng_wait(void);
 
-/* ConvE hidden-dropout keep bits for n_steps steps of rows_per_step[i] x dim
- * (torch.empty(b, dim).bernoulli_(keep) each), each step starting on a fresh
- * 32-bit word; advances the torch state. */
+/* ConvE dropout keep bits for n_steps steps of rows_per_step[i] pairs.  Per step, the
+ * forward's draws in order (conve.py:142,147,151): for each segment j < n_seg,
+ * torch.empty(rows, seg_elems[j]).bernoulli_(seg_keep[j]) -- the input dropout over the
+ * 40 x (d/20) image, the feature-map Dropout2d over 32 channels, the hidden dropout over
+ * d -- each segment starting on a fresh 32-bit word.  A segment with keep == 0 (rate 1:
+ * ATen draws nothing and returns zeros) gets zero words and consumes nothing.  Advances
+ * the torch state. */
 int kp_rng_conve_masks(uint8_t* torch_state, size_t torch_len, int32_t n_steps, const int32_t* rows_per_step,
-                       int32_t dim, double keep, uint32_t* out_words);
+                       int32_t n_seg, const int32_t* seg_elems, const double* seg_keep, uint32_t* out_words);
 
 /* Deferred form of kp_rng_conve_masks (see kp_rng_transe_enqueue): advances the
  * torch state now, fills `out_words` on the worker pool; complete after kp_rng_wait. */
 int kp_rng_conve_masks_enqueue(uint8_t* torch_state, size_t torch_len, int32_t n_steps, const int32_t* rows_per_step,
-                               int32_t dim, double keep, uint32_t* out_words);
+                               int32_t n_seg, const int32_t* seg_elems, const double* seg_keep,
+                               uint32_t* out_words);
 
 /* Device time of the last kp_posttrain_rank (HIP events on the context's
  * stream): the whole call, the summed durations of its dominant kernel's

@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import sys
+import weakref
 
 import numpy as np
 
@@ -15,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KELPIE_HIP_LIB", os.path.join(_HERE, "libkelpie_hip.so"))
 
 KP_MODEL = {"TransE": 0, "ComplEx": 1, "ConvE": 2}
+KP_INLINE = 1  # kp_rng_transe_calls_async walked inline (include/kelpie_hip.h)
 KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
 
 # symbols declared by include/kelpie_hip.h
@@ -39,7 +41,7 @@ class HP(C.Structure):
     _fields_ = [("optimizer", C.c_int32), ("epochs", C.c_int32), ("batch_size", C.c_int32), ("lr", C.c_float),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("reg_weight", C.c_float),
                 ("margin", C.c_float), ("neg_ratio", C.c_int32), ("label_smoothing", C.c_float),
-                ("hidden_dropout", C.c_float)]
+                ("hidden_dropout", C.c_float), ("input_dropout", C.c_float), ("fmap_dropout", C.c_float)]
 
 
 class Batch(C.Structure):
@@ -97,8 +99,8 @@ def lib():
         L.kp_rng_transe_calls.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                           C.c_int32, C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
-        L.kp_rng_conve_masks.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_int32, C.c_double,
-                                         C.c_void_p]
+        L.kp_rng_conve_masks.argtypes = [C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                                         C.c_void_p, C.c_void_p]
         L.kp_rng_conve_masks_enqueue.argtypes = L.kp_rng_conve_masks.argtypes
         L.kp_last_timing.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                      C.POINTER(C.c_int64), C.POINTER(C.c_double)]
@@ -226,17 +228,21 @@ def transe_calls_async(state: np.ndarray, np_key: int, np_pos: int, cap: int, D:
     """kp_rng_transe_calls_async: :func:`transe_calls` with the torch-stream walk on the
     library's walker thread, starting from ``state`` unless a walk already carries the
     stream.  Everything (x_base, x_pt, ``out``) is complete after :func:`rng_wait`; the
-    stream comes back with :func:`torch_take`."""
+    stream comes back with :func:`torch_take`.  Returns ``(x_base, x_pt, queued)``:
+    ``queued`` False when no walker thread could start and the walk ran inline (``state``
+    then holds the advanced stream and no walk carries it)."""
     n = len(R_base)
     rb = np.ascontiguousarray(R_base, dtype=np.int32)
     rp = np.ascontiguousarray(R_pt, dtype=np.int32)
     w = None if want is None else np.ascontiguousarray(want, dtype=np.uint8)
     xb = np.empty((n, d), np.float32)
     xp = np.empty((n, d), np.float32)
-    check(lib().kp_rng_transe_calls_async(_ptr(state), state.size, C.c_void_p(np_key), C.c_void_p(np_pos), int(cap),
-                                          int(D), int(d), float(std), n, _ptr(rb), _ptr(rp), _ptr(w), int(epochs),
-                                          int(ratio), int(n_entities), _ptr(xb), _ptr(xp), _ptr(out)))
-    return xb, xp
+    rc = lib().kp_rng_transe_calls_async(_ptr(state), state.size, C.c_void_p(np_key), C.c_void_p(np_pos), int(cap),
+                                         int(D), int(d), float(std), n, _ptr(rb), _ptr(rp), _ptr(w), int(epochs),
+                                         int(ratio), int(n_entities), _ptr(xb), _ptr(xp), _ptr(out))
+    if rc != KP_INLINE:
+        check(rc)
+    return xb, xp, rc != KP_INLINE
 
 
 def torch_take(state: np.ndarray) -> bool:
@@ -251,28 +257,41 @@ def rng_wait():
     check(lib().kp_rng_wait())
 
 
-def mask_words(rows_per_step, dim: int) -> int:
-    """uint32 words of the per-step packed dropout masks (each step starts on a word)."""
+def _segments(segs):
+    """[(elements per pair, keep probability)] -> (int32 elems, float64 keeps)."""
+    e = np.ascontiguousarray([int(n) for n, _ in segs], dtype=np.int32)
+    k = np.ascontiguousarray([float(p) for _, p in segs], dtype=np.float64)
+    return e, k
+
+
+def mask_words(rows_per_step, seg_elems) -> int:
+    """uint32 words of the per-step packed dropout masks: per step, one word-aligned run
+    of keep bits per segment (``seg_elems``: elements per pair, an int or a list)."""
     rows = np.asarray(rows_per_step, dtype=np.int64)
-    return int(((rows * int(dim) + 31) // 32).sum())
+    elems = [seg_elems] if np.isscalar(seg_elems) else list(seg_elems)
+    return int(sum(((rows * int(n) + 31) // 32).sum() for n in elems))
 
 
-def conve_masks_enqueue(torch_state: np.ndarray, rows_per_step, dim: int, keep: float, out: np.ndarray):
+def conve_masks_enqueue(torch_state: np.ndarray, rows_per_step, segs, out: np.ndarray):
     """Deferred :func:`conve_masks` into ``out`` (int32 / uint32, :func:`mask_words`
     elements): advances ``torch_state`` now; ``out`` is complete after :func:`rng_wait`."""
     rows = np.ascontiguousarray(rows_per_step, dtype=np.int32)
-    assert out.dtype.itemsize == 4 and out.flags.c_contiguous and out.size >= mask_words(rows, dim)
-    check(lib().kp_rng_conve_masks_enqueue(_ptr(torch_state), torch_state.size, len(rows), _ptr(rows), int(dim),
-                                           float(keep), _ptr(out)))
+    e, k = _segments(segs)
+    assert out.dtype.itemsize == 4 and out.flags.c_contiguous and out.size >= mask_words(rows, e)
+    check(lib().kp_rng_conve_masks_enqueue(_ptr(torch_state), torch_state.size, len(rows), _ptr(rows), len(e),
+                                           _ptr(e), _ptr(k), _ptr(out)))
     return out
 
 
-def conve_masks(torch_state: np.ndarray, rows_per_step, dim: int, keep: float) -> np.ndarray:
+def conve_masks(torch_state: np.ndarray, rows_per_step, segs) -> np.ndarray:
+    """ConvE dropout keep bits (kp_rng_conve_masks): ``segs`` = [(elements per pair,
+    keep probability)] in the forward's draw order."""
     rows = np.ascontiguousarray(rows_per_step, dtype=np.int32)
-    words = mask_words(rows, dim)
+    e, k = _segments(segs)
+    words = mask_words(rows, e)
     out = np.zeros(max(1, words), np.uint32)
-    check(lib().kp_rng_conve_masks(_ptr(torch_state), torch_state.size, len(rows), _ptr(rows), int(dim),
-                                   float(keep), _ptr(out)))
+    check(lib().kp_rng_conve_masks(_ptr(torch_state), torch_state.size, len(rows), _ptr(rows), len(e), _ptr(e),
+                                   _ptr(k), _ptr(out)))
     return out[:words]
 
 
@@ -542,21 +561,35 @@ class SchedBatch:
 # Page-locked int32 arenas (kp_host_alloc), pooled for the life of the process: the
 # deferred-draw arenas of kelpie_amd.rng come from here when a GPU is present, so a
 # batch's draws reach the device by DMA straight from where the RNG workers wrote them.
-_PINNED = []
-_PINNED_MAX = int(os.environ.get("KP_PINNED_ARENAS", "6"))
+# Page-locked memory is committed and locked, so the pool is small (KP_PINNED_ARENAS).
+_PINNED = []       # the pool's arrays
+_PINNED_IDLE = []  # per pool array: no lease of it is alive
+_PINNED_MAX = int(os.environ.get("KP_PINNED_ARENAS", "4"))
 _PINNED_OK = None
 
 
+class ArenaLease(np.ndarray):
+    """A pooled arena handed to one batch.  Every view taken of it is an ArenaLease whose
+    ``base`` chain leads back to it (numpy does not collapse the chain through a
+    subclass), so the lease -- and with it the arena -- stays busy while any of the
+    batch's draw arrays is alive; when the last one is gone a weakref finalizer returns
+    the arena to the pool.  No reference counting of the pool's own arrays."""
+
+
+def _lease(i: int) -> ArenaLease:
+    _PINNED_IDLE[i] = False
+    lease = _PINNED[i].view(ArenaLease)
+    weakref.finalize(lease, _PINNED_IDLE.__setitem__, i, True)
+    return lease
+
+
 def pinned_i32(n: int):
-    """An idle pooled page-locked int32 array of at least ``n`` words, or None (pool
-    full and busy, or no usable GPU: then the caller takes pageable memory).  An array
-    is idle when nothing but the pool references it (every view of it holds it as its
-    ``base``), so an arena returns to the pool once the batch using it is dropped."""
+    """A lease on an idle pooled page-locked int32 array of at least ``n`` words, or None
+    (pool full and busy, or no usable GPU: then the caller takes pageable memory)."""
     global _PINNED_OK
-    for a in _PINNED:
-        # references while idle: the pool list, the loop variable, getrefcount's argument
-        if a.size >= n and sys.getrefcount(a) <= 3:
-            return a
+    for i, a in enumerate(_PINNED):
+        if _PINNED_IDLE[i] and a.size >= n:
+            return _lease(i)
     if _PINNED_OK is False or len(_PINNED) >= _PINNED_MAX:
         return None
     p = C.c_void_p()
@@ -564,15 +597,25 @@ def pinned_i32(n: int):
         _PINNED_OK = False
         return None
     _PINNED_OK = True
-    a = np.ctypeslib.as_array((C.c_int32 * int(n)).from_address(p.value))
-    _PINNED.append(a)
-    return _PINNED[-1]
+    _PINNED.append(np.ctypeslib.as_array((C.c_int32 * int(n)).from_address(p.value)))
+    _PINNED_IDLE.append(True)
+    return _lease(len(_PINNED) - 1)
+
+
+def arena_of(a: np.ndarray):
+    """The lease ``a`` is (a view of), or None when it is not a pooled arena's."""
+    x = a
+    while isinstance(x, ArenaLease):
+        b = x.base
+        if any(b is p for p in _PINNED):
+            return x
+        x = b
+    return None
 
 
 def is_pinned(a: np.ndarray) -> bool:
     """``a`` is (a view of) a pooled page-locked arena."""
-    b = a if a.base is None or not isinstance(a.base, np.ndarray) else a.base
-    return any(b is p for p in _PINNED)
+    return arena_of(a) is not None
 
 
 def gather_i32(arrays, out: np.ndarray) -> np.ndarray:

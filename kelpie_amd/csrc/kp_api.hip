@@ -93,6 +93,9 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     // the fp32-MFMA kernel of kp_attn.hpp
     c->attn_mode = 1;
     if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "f32") == 0 ? 0 : 1;
+    // ComplEx D = 400 on bf16x3: the dimensions split over a wave pair, two waves per SIMD
+    // (kp_attn5.hpp); KP_ATTN_PAIR=0 keeps kp_attn3
+    if (const char* a = std::getenv("KP_ATTN_PAIR")) c->attn_pair = std::atoi(a) != 0;
     // ConvE FC GEMMs in the step loop (bit 0 forward, bit 1 backward on kp_gemm3_abt):
     // KP_FC=f32 | fwd | bwd | both; fp32 by default (the bf16x3 forms measured slower end to
     // end) and always with the fp32 attention
@@ -104,6 +107,12 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     // (kp_cv_fused.hpp) by default; KP_CV_FUSED=0 selects the separate kernels (A/B)
     c->cv_fused = 1;
     if (const char* a = std::getenv("KP_CV_FUSED")) c->cv_fused = std::atoi(a) != 0;
+    // ConvE rank of the post-trained row on fp64 logits (sigmoid is monotone), as a fp64
+    // reference ranks; KP_CV_RANK=f32 ranks the fp32 sigmoid scores (A/B)
+    if (const char* a = std::getenv("KP_CV_RANK")) c->cv_rank64 = std::strcmp(a, "f32") != 0;
+    // TransE rank of the post-trained row on fp64 squared distances (sqrt is monotone);
+    // KP_TE_RANK=f32 ranks the fp32 norms (A/B)
+    if (const char* a = std::getenv("KP_TE_RANK")) c->te_rank64 = std::strcmp(a, "f32") != 0;
     if (const char* a = std::getenv("KP_ATTN_PART"))
       c->attn_part = std::strcmp(a, "streamk") == 0 ? 1 : std::strcmp(a, "ranges") == 0 ? 2 : 0;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));

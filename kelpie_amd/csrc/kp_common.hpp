@@ -96,6 +96,8 @@ struct kp_ctx {
   bool time_hot = true;
   // attention contraction: 0 = fp32 MFMA (kp_attn.hpp), 1 = bf16x3 MFMA (kp_attn3.hpp)
   int attn_mode = 0;
+  int attn_pair = 0;       // ComplEx D = 400: the wave-pair kernel kp_attn5 (KP_ATTN_PAIR=1)
+  int attn5_wpc = 0;       // co-resident kp_attn5 workgroups per CU (cached)
   int fc_mode = 0;  // ConvE step-loop FC GEMMs on kp_gemm3_abt (bf16x3): bit 0 forward, bit 1 backward
   int attn_part = 0;  // kp_attn3 partition: 0 chosen per launch, 1 stream-K, 2 XCD-grouped ranges (KP_ATTN_PART)
   DevBuf e3;               // kp_attn3's split image of dE, built on first use
@@ -109,6 +111,8 @@ struct kp_ctx {
   DevBuf fc3, fct3;        // ConvE: three-piece bf16 images of the FC weight and its transpose (kp_gemm3.hip)
   bool fc3_ready = false;
   int cv_fused = 1;        // ConvE d = 200: fused encoder kernels (kp_cv_fused.hpp), KP_CV_FUSED
+  int cv_rank64 = 1;       // ConvE post-training rank on fp64 logits (KP_CV_RANK=f32: fp32 sigmoid scores)
+  int te_rank64 = 1;       // TransE post-training rank on fp64 squared distances (KP_TE_RANK=f32: fp32 norms)
   DevBuf cvf_fw3, cvf_bw3;  // their permuted split images of the FC weight (built once)
   bool cvf_ready = false;
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
@@ -220,9 +224,11 @@ enum { RANK_TRIPLE_RESULTS = 0, RANK_PREDICT_TAILS = 1, RANK_SORT_POSITION = 2 }
 // kcol64 [n] the kelpie column scores q . x; rank = #{e not filtered : score_e >= target}
 // over the frozen entities (scores q . E_e summed in fp64, sequentially over d) plus the
 // kelpie column.  The target itself counts unless filtered.
+// launch_rank_f64's score kinds
+enum { RANK64_DOT = 0, RANK64_SIGMOID = 1, RANK64_DIST = 2 };
 void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* d_t64, const double* d_kcol64,
                      const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt, float* d_target,
-                     int64_t* d_rank);
+                     int64_t* d_rank, int act = 0);
 void launch_rank_count(kp_ctx* c, int n_slots, const float* d_scores, int ld, int n_cols,
                        const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt,
                        int minimizer, float* d_target, int64_t* d_rank,

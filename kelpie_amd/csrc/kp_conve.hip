@@ -6,10 +6,13 @@
 //   rows = kelpie triples + inverses -> er_vocab (h, r) -> tails, insertion
 //   order, NOT shuffled; minibatches of batch_size pairs; targets one-hot over
 //   N = |E|+1 entities, smoothed (1-ls) y + 1/N; BCELoss(sigmoid(x . E_all^T));
-//   encoder: BN1 -> conv 3x3 (32) -> BN2 -> ReLU -> FC -> dropout -> BN3 -> ReLU,
-//   with every layer frozen and BN in eval mode, but Dropout in TRAIN mode
-//   (model.py:114-125): the hidden-dropout masks are drawn on the host (RNG as
-//   input, packed keep bits); Adam(lr = 1e-3) on the kelpie row.
+//   encoder: BN1 -> input dropout -> conv 3x3 (32) -> BN2 -> ReLU -> feature-map
+//   Dropout2d -> FC -> hidden dropout -> BN3 -> ReLU, with every layer frozen and BN in
+//   eval mode, but the three dropouts in TRAIN mode (model.py:114-125): their masks are
+//   drawn on the host (RNG as input, packed keep bits: per slot and step one word-aligned
+//   run per dropout, in the forward's draw order); Adam(lr = 1e-3) on the kelpie row.
+//   With an input or feature-map dropout the frozen-head pairs' encodings change every
+//   step, so they are encoded per step with the kelpie pairs (else once per batch).
 //
 // Per step, for the pairs whose head is the kelpie ("kelpie pairs"):
 //   conv forward (kp_cv_conv_fwd) -> FC (fp32 MFMA GEMM, split-K) -> dropout/BN3/ReLU
@@ -30,23 +33,27 @@ int cx_pick_db(int dim);
 namespace {
 using namespace kpattn;
 
+using kpcvf::CvBits;
 struct CvInst {  // one kelpie pair in one step
   int slot, rel, b, pos;
-  long long mask_off;  // word offset of this step's keep bits (-1: no dropout)
+  CvBits mb;
   int tail_begin, tail_count;
 };
 struct CvFInst {  // one frozen-head pair in one step
-  int slot, fp, b, pos;
-  long long mask_off;
+  int slot, fp, b, pos;  // fp: its FC row (per batch), or its encoded row in the step's Q (fr_step)
+  CvBits mb;
 };
 struct CvAct {
   int slot, k_begin, k_count, f_begin, f_count, pad0, pad1, pad2;
 };
 struct CvConst {
   int n_ent, dim, dp, H, hid;
-  float scale;  // 1/(1-p) as float32 (dropout noise value)
+  float scale;  // hidden dropout: 1/(1-p) as float32 (the noise value of a kept element)
   float ylo, yhi;
-  int has_mask;
+  int has_mask;             // hidden dropout drawn
+  int has_in, has_fm;       // input / feature-map dropout drawn
+  float scale_in, scale_fm;
+  int fr_step;              // frozen-head pairs encoded every step (has_in || has_fm)
 };
 
 __device__ __forceinline__ float bce_g(float s, float y, float gs) {
@@ -56,10 +63,13 @@ __device__ __forceinline__ float bce_g(float s, float y, float gs) {
   return ((p - y) / fmaxf(w, 1e-12f) * gs) * w;
 }
 
-__device__ __forceinline__ float noise_at(const int32_t* __restrict__ bits, long long off, int bitidx, float scale) {
-  if (off < 0) return 1.0f;
-  const uint32_t w = (uint32_t)bits[off + (bitidx >> 5)];
-  return ((w >> (bitidx & 31)) & 1u) ? scale : 0.0f;
+// the dropout multiplier of element idx of a pair's run starting at bit base (ATen's
+// noise: bernoulli(keep) / keep, i.e. 1/(1-p) or 0); 1 when that dropout is not drawn
+__device__ __forceinline__ float noise_at(const int32_t* __restrict__ bits, long long base, int idx, float scale) {
+  if (base < 0) return 1.0f;
+  const long long b = base + idx;
+  const uint32_t w = (uint32_t)bits[b >> 5];
+  return ((w >> (b & 31)) & 1u) ? scale : 0.0f;
 }
 
 // image (BN1) -> conv 3x3 + bias -> BN2 -> ReLU -> flat (conve.py:134-146).
@@ -72,6 +82,7 @@ __global__ __launch_bounds__(256) void kp_cv_conv_fwd(int M, const int2* __restr
                                                       const float* __restrict__ R, CvConst k,
                                                       const float* __restrict__ cw, const float* __restrict__ cb,
                                                       const float* __restrict__ bna, const float* __restrict__ bnb,
+                                                      const CvBits* __restrict__ mb, const int32_t* __restrict__ bits,
                                                       float* __restrict__ flat) {
   __shared__ float img[40 * 32];
   __shared__ float w[288], bias[32], a2[32], b2[32];
@@ -82,9 +93,14 @@ __global__ __launch_bounds__(256) void kp_cv_conv_fwd(int M, const int2* __restr
   const float* lhs = sr.x >= 0 ? E + (size_t)sr.x * k.dp : X + (size_t)(-sr.x - 1) * k.dp;
   const float* rel = R + (size_t)sr.y * k.dp;
   const float a1 = bna[0], b1 = bnb[0];
+  const long long in_b = mb ? mb[i].in : -1, fm_b = mb ? mb[i].fm : -1;
   for (int j = tid; j < 20 * k.H; j += 256) {
     img[j] = lhs[j] * a1 + b1;
     img[20 * k.H + j] = rel[j] * a1 + b1;
+    if (in_b >= 0) {  // input dropout on the BN1 image (conve.py:141-142)
+      img[j] *= noise_at(bits, in_b, j, k.scale_in);
+      img[20 * k.H + j] *= noise_at(bits, in_b, 20 * k.H + j, k.scale_in);
+    }
   }
   for (int j = tid; j < 288; j += 256) w[j] = cw[j];
   if (tid < 32) {
@@ -105,13 +121,15 @@ __global__ __launch_bounds__(256) void kp_cv_conv_fwd(int M, const int2* __restr
       for (int kx = 0; kx < 3; ++kx) acc += w[c * 9 + ky * 3 + kx] * img[(y + ky) * k.H + xx + kx];
     acc += bias[c];
     const float v = acc * a2[c] + b2[c];
-    flat[(size_t)i * k.hid + o] = fmaxf(v, 0.f);
+    float f = fmaxf(v, 0.f);
+    if (fm_b >= 0) f *= noise_at(bits, fm_b, c, k.scale_fm);  // feature-map Dropout2d (conve.py:147)
+    flat[(size_t)i * k.hid + o] = f;
   }
 }
 
 // x = ReLU(BN3(dropout(FC))) from the split-K FC slabs; writes dp-padded rows
 __global__ void kp_cv_post_fc(int M, const float* __restrict__ slabs, int ksplit, CvConst k,
-                              const CvInst* __restrict__ inst, const int32_t* __restrict__ bits,
+                              const CvBits* __restrict__ mb, const int32_t* __restrict__ bits,
                               const float* __restrict__ bna, const float* __restrict__ bnb, float* __restrict__ Q) {
   const int i = blockIdx.x;
   if (i >= M) return;
@@ -123,8 +141,8 @@ __global__ void kp_cv_post_fc(int M, const float* __restrict__ slabs, int ksplit
       float fc = 0.f;
       for (int z = 0; z < ksplit; ++z) fc += slabs[((size_t)z * M + i) * k.dim + d];
       float nz = 1.0f;
-      if (inst && k.has_mask) nz = noise_at(bits, inst[i].mask_off, inst[i].pos * k.dim + d, k.scale);
-      const float dr = (inst && k.has_mask) ? fc * nz : fc;
+      if (mb && k.has_mask) nz = noise_at(bits, mb[i].hid, d, k.scale);
+      const float dr = (mb && k.has_mask) ? fc * nz : fc;
       v = fmaxf(dr * a3[d] + b3[d], 0.f);
     }
     Q[(size_t)i * k.dp + d] = v;
@@ -186,7 +204,7 @@ __global__ __launch_bounds__(256) void kp_cv_dx(int M, CvConst k, const CvInst* 
       if (d < k.dim) dx += corr * E[(size_t)e * k.dp + d];
     }
     if (d < k.dim) {
-      const float nz = k.has_mask ? noise_at(bits, I.mask_off, I.pos * k.dim + d, k.scale) : 1.0f;
+      const float nz = k.has_mask ? noise_at(bits, I.mb.hid, d, k.scale) : 1.0f;
       const float relu = xi[d] > 0.f ? 1.0f : 0.0f;
       const float v = dx * relu * a3[d] * nz;
       dfc[(size_t)i * k.dim + d] = v;
@@ -208,10 +226,14 @@ __global__ __launch_bounds__(256) void kp_cv_dx(int M, CvConst k, const CvInst* 
 }
 
 // dL/dflat -> ReLU / BN2 -> transposed 3x3 conv -> BN1 -> the lhs half of the image
+// (feature-map dropout: flat holds the dropped map, so flat > 0 is the ReLU mask of a
+// kept channel, and a kept channel's gradient carries its 1/(1-p); input dropout: the
+// image gradient times the input mask)
 __global__ __launch_bounds__(256) void kp_cv_conv_bwd(int M, CvConst k, const float* __restrict__ dflat,
                                                       const float* __restrict__ flat,
                                                       const float* __restrict__ cw, const float* __restrict__ bna,
-                                                      float* __restrict__ dl) {
+                                                      const CvBits* __restrict__ mb,
+                                                      const int32_t* __restrict__ bits, float* __restrict__ dl) {
   extern __shared__ __attribute__((aligned(16))) float dc[];  // [32][20][W2]
   __shared__ float w[288];
   const int i = blockIdx.x;
@@ -224,7 +246,8 @@ __global__ __launch_bounds__(256) void kp_cv_conv_bwd(int M, CvConst k, const fl
     const int c = j / (20 * W2), rem = j - c * 20 * W2;
     const int o = c * per_c + rem;  // rows 0..19 of channel c
     const float f = flat[(size_t)i * k.hid + o];
-    dc[j] = (f > 0.f) ? dflat[(size_t)i * k.hid + o] * bna[1 + c] : 0.f;
+    const float g = dflat[(size_t)i * k.hid + o];
+    dc[j] = (f > 0.f) ? (k.has_fm ? g * k.scale_fm : g) * bna[1 + c] : 0.f;
   }
   __syncthreads();
   const float a1 = bna[0];
@@ -244,6 +267,7 @@ __global__ __launch_bounds__(256) void kp_cv_conv_bwd(int M, CvConst k, const fl
         }
       }
     }
+    if (k.has_in) acc *= noise_at(bits, mb[i].in, j, k.scale_in);
     dl[(size_t)i * k.dp + j] = acc * a1;
   }
 }
@@ -324,10 +348,14 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
       const int d = lane + 64 * u;
       v[u] = 0.f;
       if (d < k.dim) {
-        const float fc = fcf[(size_t)F.fp * k.dim + d];
-        const float nz = k.has_mask ? noise_at(bits, F.mask_off, F.pos * k.dim + d, k.scale) : 1.0f;
-        const float dr = k.has_mask ? fc * nz : fc;
-        v[u] = fmaxf(dr * a3[d] + b3[d], 0.f);
+        if (k.fr_step) {  // encoded this step with its own masks (kp_cv_post_fc)
+          v[u] = fcf[(size_t)F.fp * k.dp + d];
+        } else {
+          const float fc = fcf[(size_t)F.fp * k.dim + d];
+          const float nz = k.has_mask ? noise_at(bits, F.mb.hid, d, k.scale) : 1.0f;
+          const float dr = k.has_mask ? fc * nz : fc;
+          v[u] = fmaxf(dr * a3[d] + b3[d], 0.f);
+        }
         part += v[u] * xs[d];
       }
     }
@@ -365,6 +393,37 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
   }
 }
 
+// fp64 ranking queries (launch_rank_f64, act 1): the encoder output of the post-trained
+// row (fp32, eval mode) widened to fp64; its logit against the target and against the
+// kelpie row as one sequential fp64 FMA chain over d (exact products of fp32 operands),
+// the order kp_rank_f64_count scores every entity in.  At the reference init the sigmoid
+// scores of ~10^5 entities lie within ~0.005 of 0.5, a few per fp32 ulp there, so fp32
+// scores tie and their rounding moves the rank; the logits order them as a fp64 run does.
+__global__ void kp_cv_rankq64(const float* __restrict__ Qr, const float* __restrict__ X,
+                              const float* __restrict__ E, int n_ent, int dp, const int32_t* __restrict__ po,
+                              int n_slots, double* __restrict__ Q, double* __restrict__ t64,
+                              double* __restrict__ kcol64) {
+  const int s = blockIdx.x;
+  if (s >= n_slots) return;
+  double* q = Q + (size_t)s * dp;
+  for (int d = threadIdx.x; d < dp; d += blockDim.x) q[d] = (double)Qr[(size_t)s * dp + d];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float* x = X + (size_t)s * dp;
+    const int o = po[s];
+    double z = 0.0, t = 0.0;
+    for (int d = 0; d < dp; ++d) z = __fma_rn(q[d], (double)x[d], z);
+    if (o < n_ent) {
+      const float* eo = E + (size_t)o * dp;
+      for (int d = 0; d < dp; ++d) t = __fma_rn(q[d], (double)eo[d], t);
+    } else {
+      t = z;  // the kelpie entity is its own object
+    }
+    kcol64[s] = z;
+    t64[s] = t;
+  }
+}
+
 // kelpie column of the rank scores: sigmoid(q_s . x_s)
 __global__ void kp_cv_kcol(int n, CvConst k, const float* __restrict__ Q, const float* __restrict__ X,
                            float* __restrict__ scores, int ld) {
@@ -383,9 +442,18 @@ CvConst make_const(kp_ctx* c, const kp_hp* hp) {
   k.dp = c->dp;
   k.H = c->dim / 20;
   k.hid = c->hidden;
+  // ATen's noise value: 1 / (1 - p) in float32 (the dropout's div_ of the bernoulli mask);
+  // p == 1 ships zero keep bits, so its infinite scale is never selected
+  auto scale_of = [](double p) { return (p > 0.0 && p < 1.0) ? (1.0f / (float)(1.0 - p)) : 1.0f; };
   const double p = hp ? hp->hidden_dropout : 0.0;
   k.has_mask = (p > 0.0) ? 1 : 0;
-  k.scale = (p > 0.0) ? (1.0f / (float)(1.0 - p)) : 1.0f;
+  k.scale = scale_of(p);
+  const double pin = hp ? hp->input_dropout : 0.0, pfm = hp ? hp->fmap_dropout : 0.0;
+  k.has_in = (pin > 0.0) ? 1 : 0;
+  k.has_fm = (pfm > 0.0) ? 1 : 0;
+  k.scale_in = scale_of(pin);
+  k.scale_fm = scale_of(pfm);
+  k.fr_step = (k.has_in || k.has_fm) ? 1 : 0;
   const double ls = hp ? hp->label_smoothing : 0.0;
   if (ls != 0.0) {
     const float inv_n = (float)(1.0 / (double)(c->n_ent + 1));
@@ -405,7 +473,7 @@ void encode_eval(kp_ctx* c, int n, const int2* dsrc, const float* dX, float* dQ)
   float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)n * c->hidden));
   float* dfc = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * (size_t)n * c->dim));
   KP_CONV_FWD(dim3(n), dim3(256), 0, c->stream, n, dsrc, c->dE, dX, c->dR, k, c->d_conv_w,
-                     c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
+                     c->d_conv_b, c->d_bn_a, c->d_bn_b, nullptr, nullptr, dflat);
   KP_HIP(hipGetLastError());
   launch_gemm_abt(c, dflat, c->hidden, n, c->d_fc_w, c->hidden, c->dim, c->hidden, dfc, c->dim, c->d_fc_b, 0, 1);
   hipLaunchKernelGGL(kp_cv_post_fc, dim3(n), dim3(256), 0, c->stream, n, dfc, 1, k, nullptr, nullptr, c->d_bn_a,
@@ -493,27 +561,44 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
         }
       }
   }
-  // mask word offsets: per slot, steps in order, ceil(b*dim/32) words each
-  std::vector<std::vector<long long>> moff(ns);
+  // keep-bit offsets: per slot, steps in order; per step one word-aligned run per drawn
+  // dropout, in the forward's order (input b x 2d, feature map b x 32, hidden b x d)
+  struct StepBits {
+    long long in, fm, hid;  // word offsets (-1: not drawn)
+  };
+  std::vector<std::vector<StepBits>> moff(ns);
   for (int s = 0; s < ns; ++s) {
     const int nb = plan[s].nb;
     const int P = (int)plan[s].pairs.size();
     long long off = bt->rng_off[s];
     for (int t = 0; t < E_ * nb; ++t) {
       const int j = t % nb;
-      const int b = std::min(hp->batch_size, P - j * hp->batch_size);
-      moff[s].push_back(kc.has_mask ? off : -1);
-      off += ((long long)b * c->dim + 31) / 32;
+      const long long b = std::min(hp->batch_size, P - j * hp->batch_size);
+      StepBits sb{-1, -1, -1};
+      if (kc.has_in) { sb.in = off; off += (b * 2 * c->dim + 31) / 32; }
+      if (kc.has_fm) { sb.fm = off; off += (b * 32 + 31) / 32; }
+      if (kc.has_mask) { sb.hid = off; off += (b * c->dim + 31) / 32; }
+      moff[s].push_back(sb);
     }
-    if (kc.has_mask) KP_REQUIRE(off <= bt->rng_off[s + 1], "ConvE: missing hidden-dropout keep bits");
+    KP_REQUIRE(off <= bt->rng_off[s + 1], "ConvE: missing dropout keep bits");
   }
-  // per-step instance lists
-  std::vector<int> kin_off(T + 1, 0), fin_off(T + 1, 0), act_o(T + 1, 0);
-  int max_k = 0;
+  auto pair_bits = [&](const StepBits& sb, int pos) {
+    return CvBits{sb.in < 0 ? -1 : 32 * sb.in + (long long)pos * 2 * c->dim,
+                  sb.fm < 0 ? -1 : 32 * sb.fm + (long long)pos * 32,
+                  sb.hid < 0 ? -1 : 32 * sb.hid + (long long)pos * c->dim};
+  };
+  // per-step instance lists; the step's encoder rows (kelpie pairs, then with fr_step the
+  // frozen-head pairs) with their keep-bit offsets
+  std::vector<int> kin_off(T + 1, 0), fin_off(T + 1, 0), act_o(T + 1, 0), enc_off(T + 1, 0);
+  std::vector<int2> enc_src;
+  std::vector<CvBits> enc_bits;
+  int max_k = 0, max_enc = 0;
   for (int t = 0; t < T; ++t) {
     kin_off[t] = (int)kinst.size();
     fin_off[t] = (int)finst.size();
     act_o[t] = (int)acts.size();
+    enc_off[t] = (int)enc_src.size();
+    std::vector<int2> fr_hr;  // the step's frozen-head (h, r), with fr_step
     int local_k = 0;
     for (int s = 0; s < ns; ++s) {
       const int nb = plan[s].nb;
@@ -534,7 +619,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
           I.rel = pr.r;
           I.b = b;
           I.pos = q - p0;
-          I.mask_off = moff[s][t];
+          I.mb = pair_bits(moff[s][t], I.pos);
           I.tail_begin = (int)tails.size();
           std::vector<int> uniq;
           for (int tt : pr.tails)
@@ -546,19 +631,32 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
         } else {
           CvFInst F{};
           F.slot = s;
-          F.fp = fp_id.at((long long)pr.h * c->n_rel2 + pr.r);
+          F.fp = kc.fr_step ? (int)finst.size() - fin_off[t] : fp_id.at((long long)pr.h * c->n_rel2 + pr.r);
           F.b = b;
           F.pos = q - p0;
-          F.mask_off = moff[s][t];
+          F.mb = pair_bits(moff[s][t], F.pos);
           finst.push_back(F);
+          if (kc.fr_step) fr_hr.push_back(make_int2(pr.h, pr.r));
         }
       }
       A.k_count = local_k - A.k_begin;
       A.f_count = (int)finst.size() - fin_off[t] - A.f_begin;
       acts.push_back(A);
     }
+    for (int i = kin_off[t]; i < (int)kinst.size(); ++i) {
+      enc_src.push_back(make_int2(-kinst[i].slot - 1, kinst[i].rel));
+      enc_bits.push_back(kinst[i].mb);
+    }
+    if (kc.fr_step)
+      for (int i = fin_off[t]; i < (int)finst.size(); ++i) {
+        finst[i].fp += local_k;  // its row in the step's encoder output, after the kelpie pairs
+        enc_src.push_back(fr_hr[i - fin_off[t]]);
+        enc_bits.push_back(finst[i].mb);
+      }
     max_k = std::max(max_k, local_k);
+    max_enc = std::max(max_enc, (int)enc_src.size() - enc_off[t]);
   }
+  enc_off[T] = (int)enc_src.size();
   kin_off[T] = (int)kinst.size();
   fin_off[T] = (int)finst.size();
   act_o[T] = (int)acts.size();
@@ -576,17 +674,23 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   CvAct* dAct = upload(c, c->ws[5], acts.data(), std::max<size_t>(1, acts.size()));
   int32_t* dTails = upload(c, c->ws[6], tails.data(), std::max<size_t>(1, tails.size()));
   const int64_t nbits = bt->rng_off[ns];
-  int32_t* dBits = upload(c, c->ws[7], bt->rng, (size_t)std::max<int64_t>(1, nbits));
-  const int nfp = (int)fpairs.size();
+  // the keep bits, plus one zero guard word (kp_cv_fwd_fused reads a row's input bits as
+  // a 64-bit window)
+  int32_t* dBits = reinterpret_cast<int32_t*>(c->ws[7].ensure(sizeof(int32_t) * (size_t)(nbits + 2)));
+  if (nbits > 0)
+    KP_HIP(hipMemcpyAsync(dBits, bt->rng, sizeof(int32_t) * (size_t)nbits, hipMemcpyHostToDevice, c->stream));
+  KP_HIP(hipMemsetAsync(dBits + nbits, 0, 2 * sizeof(int32_t), c->stream));
+  const int nfp = kc.fr_step ? 0 : (int)fpairs.size();
 
   KP_HIP(hipEventRecord(c->ev0, c->stream));
-  // frozen-head pairs: FC output (pre-dropout) once per batch
+  // frozen-head pairs without an input / feature-map dropout: FC output (pre-dropout)
+  // once per batch
   float* dFcf = reinterpret_cast<float*>(c->ws[8].ensure(sizeof(float) * (size_t)std::max(1, nfp) * c->dim));
   if (nfp > 0) {
     int2* dFp = upload(c, c->ws[9], fpairs.data(), fpairs.size());
     float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)nfp * c->hidden));
     KP_CONV_FWD(dim3(nfp), dim3(256), 0, c->stream, nfp, dFp, c->dE, dX, c->dR, kc,
-                       c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
+                       c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, nullptr, nullptr, dflat);
     KP_HIP(hipGetLastError());
     launch_gemm_abt(c, dflat, c->hidden, nfp, c->d_fc_w, c->hidden, c->dim, c->hidden, dFcf, c->dim, c->d_fc_b, 0, 1);
   }
@@ -595,32 +699,28 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   const bool fused = c->cv_fused && c->dim == 200 && c->hidden == kpcvf::HID;
   const int KS = fused ? kpcvf::NSPLIT : 8;  // split-K of the FC forward
   const int mk = std::max(1, max_k);
-  float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)std::max(fused ? 1 : mk, nfp) * c->hidden));
-  float* dslab = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * (size_t)KS * mk * c->dim));
+  const int me = std::max(1, max_enc);  // encoder rows per step (kelpie pairs + per-step frozen pairs)
+  float* dflat = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)std::max(fused ? 1 : me, nfp) * c->hidden));
+  float* dslab = reinterpret_cast<float*>(c->ws[13].ensure(sizeof(float) * (size_t)KS * me * c->dim));
   const __bf16* cvf_fw = nullptr;
   const __bf16* cvf_bw = nullptr;
   uint8_t* dRelu = nullptr;
   __bf16* dG3 = nullptr;
   if (fused) {
     conve_fused_images(c, &cvf_fw, &cvf_bw);
-    dRelu = reinterpret_cast<uint8_t*>(c->ws[24].ensure((size_t)mk * kpcvf::MASK_B));
+    dRelu = reinterpret_cast<uint8_t*>(c->ws[24].ensure((size_t)me * kpcvf::MASK_B));
     dG3 = reinterpret_cast<__bf16*>(c->ws[25].ensure(3 * sizeof(__bf16) * (size_t)mk * kpcvf::KB));
   }
   const int n_dl = fused ? kpcvf::NSPLIT : 1;  // lhs image-gradient slabs per pair (kp_cv_bwd_fused, reduced in slab 0)
-  float* dQ = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)mk * DP));
-  int2* dSrc = reinterpret_cast<int2*>(c->ws[15].ensure(sizeof(int2) * (size_t)std::max<size_t>(1, kinst.size())));
+  float* dQ = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)me * DP));
+  int2* dSrc = upload(c, c->ws[15], enc_src.data(), std::max<size_t>(1, enc_src.size()));
+  CvBits* dEncBits = upload(c, c->ws[26], enc_bits.data(), std::max<size_t>(1, enc_bits.size()));
   float* dgs = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)std::max<size_t>(1, kinst.size())));
   {
-    std::vector<int2> src(kinst.size());
     std::vector<float> gsv(kinst.size());
-    for (size_t i = 0; i < kinst.size(); ++i) {
-      src[i] = make_int2(-kinst[i].slot - 1, kinst[i].rel);
-      gsv[i] = 1.0f / (float)((long long)kinst[i].b * (long long)(K + 1));
-    }
-    if (!src.empty()) {
-      KP_HIP(hipMemcpyAsync(dSrc, src.data(), sizeof(int2) * src.size(), hipMemcpyHostToDevice, c->stream));
+    for (size_t i = 0; i < kinst.size(); ++i) gsv[i] = 1.0f / (float)((long long)kinst[i].b * (long long)(K + 1));
+    if (!gsv.empty())
       KP_HIP(hipMemcpyAsync(dgs, gsv.data(), sizeof(float) * gsv.size(), hipMemcpyHostToDevice, c->stream));
-    }
   }
   int attn_slots = c->n_cu * (DBV <= 13 ? 2 : 1);  // co-resident attention workgroups
   if (c->attn_mode == 1) {
@@ -649,6 +749,8 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   // kp_gemm3_abt stages 8-value chunks: other widths (d = 60 in the goldens) stay on fp32
   const int fcm = (c->dim % 8 == 0 && c->hidden % 8 == 0) ? c->fc_mode : 0;
   uint16_t* ddfc3 = reinterpret_cast<uint16_t*>(c->ws[27].ensure(3 * sizeof(uint16_t) * (size_t)mk * c->dim));
+  // the masks' multipliers as the fused kernels take them (1: not drawn)
+  const float s_in = kc.has_in ? kc.scale_in : 1.0f, s_fm = kc.has_fm ? kc.scale_fm : 1.0f;
 
   CvOpt opt{};
   opt.lr = hp->lr;
@@ -665,30 +767,40 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   const size_t shm_cbwd = sizeof(float) * 32 * 20 * (c->dim / 20 - 2);
   for (int t = 0; t < T; ++t) {
     const int nk = kin_off[t + 1] - kin_off[t];
+    const int ne = enc_off[t + 1] - enc_off[t];  // nk kelpie rows first
     const int na = act_o[t + 1] - act_o[t];
     const CvInst* KI = dKI + kin_off[t];
-    if (nk > 0) {
-      const int n_split = step_plan[t].wk.n_parts;
-      const int cvf_grid = kpcvf::NSPLIT * ((nk + kpcvf::MT - 1) / kpcvf::MT);
+    const int2* ES = dSrc + enc_off[t];
+    const CvBits* EB = dEncBits + enc_off[t];
+    if (ne > 0) {  // encoder forward (conve.py:133-153, train-mode dropouts)
       if (fused) {
-        hipLaunchKernelGGL(kpcvf::kp_cv_fwd_fused, dim3(cvf_grid), dim3(512), kpcvf::FWD_LDS, c->stream, nk,
-                           dSrc + kin_off[t], c->dE, dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b,
-                           cvf_fw, c->d_fc_b, c->dim, dslab, dRelu);
+        const int fgrid = kpcvf::NSPLIT * ((ne + kpcvf::MT - 1) / kpcvf::MT);
+        if (kc.fr_step)
+          hipLaunchKernelGGL(kpcvf::kp_cv_fwd_fused<true>, dim3(fgrid), dim3(512), kpcvf::FWD_LDS, c->stream, ne, ES,
+                             c->dE, dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, cvf_fw, c->d_fc_b,
+                             c->dim, EB, dBits, s_in, s_fm, dslab, dRelu);
+        else
+          hipLaunchKernelGGL(kpcvf::kp_cv_fwd_fused<false>, dim3(fgrid), dim3(512), kpcvf::FWD_LDS, c->stream, ne, ES,
+                             c->dE, dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, cvf_fw, c->d_fc_b,
+                             c->dim, EB, dBits, s_in, s_fm, dslab, dRelu);
         KP_HIP(hipGetLastError());
       } else {
-        KP_CONV_FWD(dim3(nk), dim3(256), 0, c->stream, nk, dSrc + kin_off[t], c->dE, dX, c->dR,
-                    kc, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dflat);
+        KP_CONV_FWD(dim3(ne), dim3(256), 0, c->stream, ne, ES, c->dE, dX, c->dR, kc, c->d_conv_w, c->d_conv_b,
+                    c->d_bn_a, c->d_bn_b, EB, dBits, dflat);
         KP_HIP(hipGetLastError());
         if (fcm & 1)
-          launch_gemm3_abt(c, dflat, true, c->hidden, nk, conve_fc3(c, false), c->hidden, c->dim, c->hidden, dslab,
+          launch_gemm3_abt(c, dflat, true, c->hidden, ne, conve_fc3(c, false), c->hidden, c->dim, c->hidden, dslab,
                            c->dim, c->d_fc_b, 0, KS);
         else
-          launch_gemm_abt(c, dflat, c->hidden, nk, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b,
+          launch_gemm_abt(c, dflat, c->hidden, ne, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b,
                           0, KS);
       }
-      hipLaunchKernelGGL(kp_cv_post_fc, dim3(nk), dim3(256), 0, c->stream, nk, dslab, KS, kc, KI, dBits, c->d_bn_a,
+      hipLaunchKernelGGL(kp_cv_post_fc, dim3(ne), dim3(256), 0, c->stream, ne, dslab, KS, kc, EB, dBits, c->d_bn_a,
                          c->d_bn_b, dQ);
       KP_HIP(hipGetLastError());
+    }
+    if (nk > 0) {
+      const int n_split = step_plan[t].wk.n_parts;
       hipEvent_t ea = nullptr, eb = nullptr;
       if (c->time_hot) {
         ea = c->event(2 * launches);
@@ -722,12 +834,13 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
                          dBits, c->d_bn_a, ddfc, dgk, dG3);
       KP_HIP(hipGetLastError());
       if (fused) {
-        hipLaunchKernelGGL(kpcvf::kp_cv_bwd_fused, dim3(cvf_grid), dim3(512), kpcvf::BWD_LDS, c->stream, nk, dG3,
-                           cvf_bw, dRelu, c->d_conv_w, c->d_bn_a, DP, ddl);
+        const int bgrid = kpcvf::NSPLIT * ((nk + kpcvf::MT - 1) / kpcvf::MT);
+        hipLaunchKernelGGL(kpcvf::kp_cv_bwd_fused, dim3(bgrid), dim3(512), kpcvf::BWD_LDS, c->stream, nk, dG3,
+                           cvf_bw, dRelu, c->d_conv_w, c->d_bn_a, s_fm, DP, ddl);
         KP_HIP(hipGetLastError());
         const long long nr = (long long)nk * kpcvf::LR * kpcvf::IW;
         hipLaunchKernelGGL(kpcvf::kp_cv_dl_reduce, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, c->stream, nk, DP,
-                           ddl);
+                           kc.has_in ? EB : nullptr, dBits, s_in, ddl);
         KP_HIP(hipGetLastError());
       } else if (fcm & 2) {
         split3_rows(c, ddfc, nk, c->dim, c->dim, ddfc3);
@@ -738,7 +851,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       }
       if (!fused) {
         hipLaunchKernelGGL(kp_cv_conv_bwd, dim3(nk), dim3(256), shm_cbwd, c->stream, nk, kc, ddflat, dflat, c->d_conv_w,
-                           c->d_bn_a, ddl);
+                           c->d_bn_a, EB, dBits, ddl);
         KP_HIP(hipGetLastError());
       }
     }
@@ -746,16 +859,15 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     opt.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, step)));
     opt.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)hp->beta2, step));
     if (na > 0) {
-      // dAct entries index kinst/finst relative to this step's lists
+      // dAct entries index kinst/finst relative to this step's lists; the frozen-head pairs
+      // read their encodings from dQ (fr_step) or the batch's FC rows
       hipLaunchKernelGGL(kp_cv_update, dim3(na), dim3(256), 0, c->stream, kc, dAct + act_o[t], KI, dFI + fin_off[t], dQ,
-                         dgk, ddl, dFcf, dBits, c->d_bn_a, c->d_bn_b, dX, dS1, dS2, opt);
+                         dgk, ddl, kc.fr_step ? dQ : dFcf, dBits, c->d_bn_a, c->d_bn_b, dX, dS1, dS2, opt);
       KP_HIP(hipGetLastError());
     }
   }
 
   // ---------------- rank: sigmoid(enc(x, R_p) . E_e), kelpie column, maximizer
-  const int ld = round_up(K + 1, 4);
-  float* dScores = reinterpret_cast<float*>(c->ws[10].ensure(sizeof(float) * (size_t)ns * ld));
   std::vector<int2> rsrc(ns);
   std::vector<int32_t> po(ns);
   for (int s = 0; s < ns; ++s) {
@@ -768,16 +880,27 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   int2* dRsrc = upload(c, c->ws[11], rsrc.data(), rsrc.size());
   float* dQr = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)std::max(ns, mk) * DP));
   encode_eval(c, ns, dRsrc, dX, dQr);
-  launch_score_gemm(c, dQr, ns, dScores, ld, 1);
-  hipLaunchKernelGGL(kp_cv_kcol, dim3(ns), dim3(64), 0, c->stream, ns, kc, dQr, dX, dScores, ld);
-  KP_HIP(hipGetLastError());
   int32_t* dPo = upload(c, c->ws[22], po.data(), po.size());
   int32_t* dFo = upload(c, c->ws[23], bt->filt_off, (size_t)ns + 1);
   DevBuf bF, bT, bR;
   int32_t* dF = upload(c, bF, bt->filt, (size_t)std::max(1, bt->filt_off[ns]));
   float* dTarget = reinterpret_cast<float*>(bT.ensure(sizeof(float) * ns));
   int64_t* dRank = reinterpret_cast<int64_t*>(bR.ensure(sizeof(int64_t) * ns));
-  launch_rank_count(c, ns, dScores, ld, K + 1, dPo, dFo, dF, 0, dTarget, dRank);
+  if (c->cv_rank64) {
+    double* dQ64 = reinterpret_cast<double*>(c->ws[29].ensure(sizeof(double) * (size_t)ns * DP));
+    double* dT64 = reinterpret_cast<double*>(c->ws[30].ensure(sizeof(double) * 2 * (size_t)ns));
+    hipLaunchKernelGGL(kp_cv_rankq64, dim3(ns), dim3(64), 0, c->stream, dQr, dX, c->dE, K, DP, dPo, ns, dQ64, dT64,
+                       dT64 + ns);
+    KP_HIP(hipGetLastError());
+    launch_rank_f64(c, ns, dQ64, dT64, dT64 + ns, dPo, dFo, dF, dTarget, dRank, RANK64_SIGMOID);
+  } else {
+    const int ld = round_up(K + 1, 4);
+    float* dScores = reinterpret_cast<float*>(c->ws[10].ensure(sizeof(float) * (size_t)ns * ld));
+    launch_score_gemm(c, dQr, ns, dScores, ld, 1);
+    hipLaunchKernelGGL(kp_cv_kcol, dim3(ns), dim3(64), 0, c->stream, ns, kc, dQr, dX, dScores, ld);
+    KP_HIP(hipGetLastError());
+    launch_rank_count(c, ns, dScores, ld, K + 1, dPo, dFo, dF, 0, dTarget, dRank);
+  }
   KP_HIP(hipEventRecord(c->ev1, c->stream));
   if (bt->out_x) KP_HIP(hipMemcpyAsync(xp.data(), dX, sizeof(float) * xp.size(), hipMemcpyDeviceToHost, c->stream));
   KP_HIP(hipMemcpyAsync(bt->out_score, dTarget, sizeof(float) * ns, hipMemcpyDeviceToHost, c->stream));

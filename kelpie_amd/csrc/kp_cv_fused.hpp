@@ -27,6 +27,13 @@
 // 3x3 convolution into per-thread accumulators of the 20 x 10 lhs image gradient.
 // Output: one partial image gradient per channel group (16 slabs), summed by kp_cv_update.
 //
+// Train-mode dropouts (conve.py:142,147; the masks are host-drawn keep bits, a pair's
+// CvBits row gives the bit offsets, -1 = not drawn): the input mask multiplies each
+// image row as it enters the window (after BN1); the feature-map mask multiplies the
+// ReLU output of a dropped-or-kept channel, and a dropped channel's ReLU bits are stored
+// as 0, so the backward's mask covers both and it only applies the kept scale; the input
+// mask of the lhs half is applied to the reduced image gradient (kp_cv_dl_reduce).
+//
 // XCD-aware: blockIdx b runs on XCD b % 8; both kernels give XCD x the bands / channel
 // groups x and x + 8, so each XCD's 4 MB L2 holds only its slices of the weight images
 // (forward ~1.5 MB of 12 MB, backward ~0.9 MB of 6.9 MB).
@@ -38,6 +45,13 @@
 namespace kpcvf {
 
 using kpattn::bf16x8;
+
+// bit offsets of one pair's dropout keep bits in a batch's draws (-1: that dropout is
+// not drawn): input image (2 d bits, row-major 40 x d/20), feature-map channels (32),
+// hidden units (d)
+struct CvBits {
+  long long in, fm, hid;
+};
 
 constexpr int CH = 32;                // conv channels
 constexpr int IW = 10;                // image width (d = 200: 20 x 10 per half)
@@ -108,13 +122,17 @@ __global__ void kp_cv_bwd_image(const float* __restrict__ W, int dim, __bf16* __
 
 // forward: out[z][i][n] = sum over band z of map_i[k] W[n][k] (+ fc bias in band 0);
 // relu[i][20 ch + y] = ReLU signs of row y < 20 of channel ch
+// DROP: the input / feature-map dropout code is compiled in (the model has one of them)
+template <bool DROP>
 __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __restrict__ src,
                                                        const float* __restrict__ E, const float* __restrict__ X,
                                                        const float* __restrict__ R, int dp,
                                                        const float* __restrict__ cw, const float* __restrict__ cb,
                                                        const float* __restrict__ bna, const float* __restrict__ bnb,
                                                        const __bf16* __restrict__ W3, const float* __restrict__ fcb,
-                                                       int dim, float* __restrict__ out, uint8_t* __restrict__ relu) {
+                                                       int dim, const CvBits* __restrict__ mb,
+                                                       const int32_t* __restrict__ bits, float s_in, float s_fm,
+                                                       float* __restrict__ out, uint8_t* __restrict__ relu) {
   extern __shared__ __attribute__((aligned(16))) __bf16 bsh[];  // [stage][piece][NR][RS]
   __shared__ float sw[CH * 9], sc[CH], sa[CH], sbb[CH];
   const int tid = threadIdx.x;
@@ -137,6 +155,25 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
   const float* lhs = s.x >= 0 ? E + (size_t)s.x * dp : X + (size_t)(-s.x - 1) * dp;
   const float* rel = R + (size_t)s.y * dp;
   const float a1 = bna[0], b1 = bnb[0];
+  // the pair's dropout keep bits: the input image (bit 10 r + x of row r) and the 32
+  // feature-map channels (one word: its run starts on a multiple of 32)
+  const CvBits pb = DROP ? mb[ok ? i : M - 1] : CvBits{-1, -1, -1};
+  const uint32_t fm_keep = DROP && pb.fm >= 0 ? (uint32_t)bits[pb.fm >> 5] : 0xffffffffu;
+  const bool fm_on = DROP && pb.fm >= 0;
+  // BN1 then the input dropout of image row r (conve.py:141-142), in place
+  auto bn1_row = [&](int r, float (&o)[IW]) __attribute__((always_inline)) {
+    uint32_t kb = 0x3ffu;
+    if (DROP && pb.in >= 0) {
+      const long long b0 = pb.in + (long long)r * IW;
+      const uint64_t w = (uint64_t)(uint32_t)bits[b0 >> 5] | ((uint64_t)(uint32_t)bits[(b0 >> 5) + 1] << 32);
+      kb = (uint32_t)(w >> (b0 & 31)) & 0x3ffu;
+    }
+#pragma unroll
+    for (int xx = 0; xx < IW; ++xx) {
+      o[xx] = o[xx] * a1 + b1;
+      if (DROP && pb.in >= 0) o[xx] *= ((kb >> xx) & 1u) ? s_in : 0.f;
+    }
+  };
   const int y0 = band_y0(z), y1 = band_y0(z + 1);
   const int nst = (y1 - y0) * 8;
 
@@ -191,8 +228,7 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky) {
     img_row(y0 + ky, im[ky]);
-#pragma unroll
-    for (int xx = 0; xx < IW; ++xx) im[ky][xx] = im[ky][xx] * a1 + b1;
+    bn1_row(y0 + ky, im[ky]);
   }
   img_row(min(y0 + 3, FR + 1), nx);
 
@@ -203,33 +239,37 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
   do {                                                                                         \
     const int y = y0 + ((Q) >> 3), cg = (Q) & 7;                                               \
     if (cg == 0 && (Q) > 0) {                                                                  \
+      bn1_row(y + 2, nx);                                                                      \
       _Pragma("unroll") for (int xx = 0; xx < IW; ++xx) {                                      \
         im[0][xx] = im[1][xx];                                                                 \
         im[1][xx] = im[2][xx];                                                                 \
-        im[2][xx] = nx[xx] * a1 + b1;                                                          \
+        im[2][xx] = nx[xx];                                                                    \
       }                                                                                        \
       img_row(min(y + 3, FR + 1), nx);                                                         \
     }                                                                                          \
     const int ch = 4 * cg + g;                                                                 \
+    const bool kept = ((fm_keep >> ch) & 1u) != 0;                                             \
     float wv[9];                                                                               \
     _Pragma("unroll") for (int t = 0; t < 9; ++t) wv[t] = sw[ch * 9 + t];                      \
     const float cbias = sc[ch], ca = sa[ch], cbb = sbb[ch];                                    \
     bf16x8 a[3];                                                                               \
-    unsigned bits = 0;                                                                         \
+    unsigned rb = 0;                                                                           \
     _Pragma("unroll") for (int x = 0; x < FW; ++x) {                                           \
       float v = 0.f;                                                                           \
       _Pragma("unroll") for (int ky = 0; ky < 3; ++ky)                                         \
         _Pragma("unroll") for (int kx = 0; kx < 3; ++kx) v += wv[ky * 3 + kx] * im[ky][x + kx]; \
       v += cbias;                                                                              \
       v = v * ca + cbb;                                                                        \
-      bits |= (v > 0.f ? 1u : 0u) << x;                                                        \
+      rb |= (v > 0.f && kept ? 1u : 0u) << x;                                                  \
+      float f = fmaxf(v, 0.f);                                                                 \
+      if (fm_on) f *= kept ? s_fm : 0.f;                                                       \
       __bf16 h, m, l;                                                                          \
-      kpattn::split3(fmaxf(v, 0.f), h, m, l);                                                  \
+      kpattn::split3(f, h, m, l);                                                              \
       a[0][x] = h;                                                                             \
       a[1][x] = m;                                                                             \
       a[2][x] = l;                                                                             \
     }                                                                                          \
-    if (y < LR && ok) relu[(size_t)i * MASK_B + ch * LR + y] = (uint8_t)bits;                  \
+    if (y < LR && ok) relu[(size_t)i * MASK_B + ch * LR + y] = (uint8_t)rb;                    \
     const __bf16* sb = bsh + (ST) * (3 * NR * RS);                                             \
     _Pragma("unroll") for (int n = 0; n < NBF; ++n) {                                          \
       bf16x8 b[3];                                                                             \
@@ -279,7 +319,7 @@ __global__ __launch_bounds__(512) void kp_cv_bwd_fused(int M, const __bf16* __re
                                                        const __bf16* __restrict__ WT3,
                                                        const uint8_t* __restrict__ relu,
                                                        const float* __restrict__ cw, const float* __restrict__ bna,
-                                                       int dp, float* __restrict__ dl) {
+                                                       float s_fm, int dp, float* __restrict__ dl) {
   extern __shared__ __attribute__((aligned(16))) __bf16 bsh[];  // [stage][piece][160][RS]; then dmap [MT][DCS] fp32
   __shared__ uint8_t rls[CGRP][MT * LR];                        // the tile's ReLU sign bytes
   constexpr int BR = LR * FW;                                   // 160 weight rows per channel
@@ -389,7 +429,9 @@ __global__ __launch_bounds__(512) void kp_cv_bwd_fused(int M, const __bf16* __re
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int pl = 16 * w + 4 * g + r;
-        dms[pl * DCS + col] = ((rls[cc][pl * LR + y] >> x) & 1u) ? acc[n][r] * a2 : 0.f;
+        // (feature-map dropout: the stored bits are 0 for a dropped channel; a kept one
+        // carries 1/(1-p), s_fm = 1 without that dropout)
+        dms[pl * DCS + col] = ((rls[cc][pl * LR + y] >> x) & 1u) ? (acc[n][r] * s_fm) * a2 : 0.f;
       }
     }
     __syncthreads();
@@ -430,8 +472,10 @@ __global__ __launch_bounds__(512) void kp_cv_bwd_fused(int M, const __bf16* __re
   }
 }
 
-// dl[0][i][j] = sum over the channel-group slabs (in slab order), in place in slab 0
-__global__ void kp_cv_dl_reduce(int M, int dp, float* __restrict__ dl) {
+// dl[0][i][j] = sum over the channel-group slabs (in slab order), in place in slab 0,
+// times the pair's input-dropout multiplier of lhs image element j (mb: with that dropout)
+__global__ void kp_cv_dl_reduce(int M, int dp, const CvBits* __restrict__ mb, const int32_t* __restrict__ bits,
+                                float s_in, float* __restrict__ dl) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int jn = LR * IW;
   if (t >= (long long)M * jn) return;
@@ -440,6 +484,10 @@ __global__ void kp_cv_dl_reduce(int M, int dp, float* __restrict__ dl) {
   float v = dl[o];
 #pragma unroll
   for (int zz = 1; zz < NSPLIT; ++zz) v += dl[zz * zs + o];
+  if (mb) {
+    const long long b = mb[i].in + j;
+    v *= (((uint32_t)bits[b >> 5] >> (b & 31)) & 1u) ? s_in : 0.f;
+  }
   dl[o] = v;
 }
 

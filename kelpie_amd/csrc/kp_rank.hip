@@ -209,16 +209,27 @@ __global__ __launch_bounds__(256) void kp_rank_filter_bits(int n_slots, int nwor
 
 // kelpie column and target: one thread per slot (counts the kelpie column, writes the
 // fp32 target score)
+// act RANK64_DOT: the scores are the fp64 values (ComplEx); RANK64_SIGMOID: the scores
+// are sigmoid(logit) and the rank compares the monotone logits (ConvE); RANK64_DIST: a
+// minimizer whose scores are L2 distances and the rank compares their squares (TransE:
+// get_triple_results' minimizer branch, the target counting itself even when filtered)
 __global__ void kp_rank_f64_kelpie(int n_slots, int n_ent, int nwords, const uint32_t* __restrict__ bits,
-                                   const double* __restrict__ t64, const double* __restrict__ kcol64,
-                                   float* __restrict__ target_out, unsigned long long* __restrict__ rank) {
+                                   const int32_t* __restrict__ pred_o, const double* __restrict__ t64,
+                                   const double* __restrict__ kcol64, int act, float* __restrict__ target_out,
+                                   unsigned long long* __restrict__ rank) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_slots) return;
   const bool filtered = (bits[(size_t)s * nwords + (n_ent >> 5)] >> (n_ent & 31)) & 1u;
-  rank[s] = (!filtered && kcol64[s] >= t64[s]) ? 1ull : 0ull;
-  target_out[s] = (float)t64[s];
+  if (act == RANK64_DIST)
+    rank[s] = (pred_o[s] == n_ent || (!filtered && kcol64[s] <= t64[s])) ? 1ull : 0ull;
+  else
+    rank[s] = (!filtered && kcol64[s] >= t64[s]) ? 1ull : 0ull;
+  target_out[s] = act == RANK64_SIGMOID ? (float)(1.0 / (1.0 + exp(-t64[s])))
+                  : act == RANK64_DIST  ? (float)sqrt(t64[s])
+                                        : (float)t64[s];
 }
 
+template <bool DIST>
 __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent, int dp, const double* __restrict__ Q,
                                                          const double* __restrict__ t64,
                                                          const int32_t* __restrict__ pred_o, const float* __restrict__ ET,
@@ -237,7 +248,14 @@ __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent,
     const double v = (double)ET[(size_t)d * ldt + e];
 #pragma unroll
     for (int j = 0; j < RQ; ++j)
-      if (j < ns) acc[j] = __fma_rn(q[(size_t)j * dp + d], v, acc[j]);
+      if (j < ns) {
+        if constexpr (DIST) {
+          const double df = q[(size_t)j * dp + d] - v;  // exact: fp32 operands, fp64 difference
+          acc[j] = __fma_rn(df, df, acc[j]);
+        } else {
+          acc[j] = __fma_rn(q[(size_t)j * dp + d], v, acc[j]);
+        }
+      }
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -246,8 +264,12 @@ __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent,
     if (j < ns && e < n_ent) {
       const int s = s0 + j;
       const bool filtered = (bits[(size_t)s * nwords + (e >> 5)] >> (e & 31)) & 1u;
-      // the target counts itself (unless filtered) whatever the rounding of its own score
-      hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s]);
+      // the target counts itself whatever the rounding of its own score (a maximizer's
+      // only if unfiltered: its filtered score is set back after the count)
+      if constexpr (DIST)
+        hit = e == pred_o[s] || (!filtered && acc[j] <= t64[s]);
+      else
+        hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s]);
     }
     for (int o = 32; o > 0; o >>= 1) hit += __shfl_xor(hit, o, 64);
     if (lane == 0) part[w][j] = hit;
@@ -262,7 +284,7 @@ __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent,
 
 void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* d_t64, const double* d_kcol64,
                      const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt, float* d_target,
-                     int64_t* d_rank) {
+                     int64_t* d_rank, int act) {
   if (n_slots <= 0) return;
   const int ldt = (c->n_ent + 255) / 256 * 256;
   if (!c->eT_ready) {
@@ -280,10 +302,14 @@ void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* 
                      n_cols, bits);
   KP_HIP(hipGetLastError());
   hipLaunchKernelGGL(kp_rank_f64_kelpie, dim3((n_slots + 63) / 64), dim3(64), 0, c->stream, n_slots, c->n_ent, nwords,
-                     bits, d_t64, d_kcol64, d_target, rank);
+                     bits, d_pred_o, d_t64, d_kcol64, act, d_target, rank);
   KP_HIP(hipGetLastError());
-  hipLaunchKernelGGL(kp_rank_f64_count, dim3(ldt / 256, (n_slots + RQ - 1) / RQ), dim3(256), 0, c->stream, n_slots,
-                     c->n_ent, c->dp, d_q64, d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
+  if (act == RANK64_DIST)
+    hipLaunchKernelGGL(kp_rank_f64_count<true>, dim3(ldt / 256, (n_slots + RQ - 1) / RQ), dim3(256), 0, c->stream,
+                       n_slots, c->n_ent, c->dp, d_q64, d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
+  else
+    hipLaunchKernelGGL(kp_rank_f64_count<false>, dim3(ldt / 256, (n_slots + RQ - 1) / RQ), dim3(256), 0, c->stream,
+                       n_slots, c->n_ent, c->dp, d_q64, d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
   KP_HIP(hipGetLastError());
 }
 

@@ -803,6 +803,7 @@ class TorchWalker {
     }
     const int rc = fail_rc_;
     fail_rc_ = KP_OK;
+    if (rc != KP_OK) carried_ = false;  // a failed walk leaves a partial stream: nothing continues it
     return rc;
   }
   int wait() { return take(nullptr, nullptr); }
@@ -1002,12 +1003,15 @@ int kp_rng_transe_calls_async(const uint8_t* ts, size_t tlen, uint32_t* np_key, 
                                wv.empty() ? nullptr : wv.data(), epochs, ratio, nent, x_base, x_pt, out);
     };
     if (!TorchWalker::get().submit(ts, task)) {
-      // no walker thread: walk here (the caller's state is current: nothing is carried)
+      // no walker thread (nothing is carried then: a failed start drops the carried
+      // state): walk here on the caller's state and say so, so that the caller keeps the
+      // stream itself instead of expecting a walk to carry it
       TorchMt mt;
       mt.load(ts);
       const int r2 = task(mt);
       if (r2 != KP_OK) return r2;
       mt.store(const_cast<uint8_t*>(ts));
+      return KP_INLINE;
     }
   } catch (...) {
     return KP_ENOMEM;
@@ -1020,32 +1024,59 @@ int kp_rng_torch_take(uint8_t* ts, size_t tlen, int32_t* taken) {
   return TorchWalker::get().take(ts, taken);
 }
 
-int kp_rng_conve_masks_enqueue(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim,
-                               double keep, uint32_t* out) {
-  if (!ts || tlen < 24 + kN * 8 || n_steps < 0 || dim <= 0 || (n_steps > 0 && (!rows || !out))) return KP_EINVAL;
+// the word layout of kp_rng_conve_masks: per step, one word-aligned run per segment
+static int conve_mask_plan(int32_t n_steps, const int32_t* rows, int32_t n_seg, const int32_t* seg_elems,
+                           const double* seg_keep, uint64_t* draws) {
+  if (n_steps < 0 || n_seg < 0 || n_seg > 8 || (n_steps > 0 && !rows) || (n_seg > 0 && (!seg_elems || !seg_keep)))
+    return KP_EINVAL;
+  uint64_t total = 0;
+  for (int j = 0; j < n_seg; ++j)
+    if (seg_elems[j] <= 0 || !(seg_keep[j] >= 0.0 && seg_keep[j] <= 1.0)) return KP_EINVAL;
+  for (int st = 0; st < n_steps; ++st) {
+    if (rows[st] < 0) return KP_EINVAL;
+    for (int j = 0; j < n_seg; ++j)
+      if (seg_keep[j] > 0.0) total += (uint64_t)rows[st] * (uint64_t)seg_elems[j];
+  }
+  *draws = total;
+  return KP_OK;
+}
+
+static void conve_mask_fill(TorchMt& m, int32_t n_steps, const int32_t* rows, int32_t n_seg,
+                            const int32_t* seg_elems, const double* seg_keep, uint32_t* out,
+                            std::vector<uint32_t>& buf) {
+  size_t w0 = 0;
+  for (int st = 0; st < n_steps; ++st)
+    for (int j = 0; j < n_seg; ++j) {
+      const uint64_t n = (uint64_t)rows[st] * (uint64_t)seg_elems[j];
+      const size_t nw = (size_t)((n + 31) / 32);
+      if (seg_keep[j] > 0.0)
+        bernoulli_words(m, n, seg_keep[j], out + w0, buf);  // one random64 (two outputs) per element
+      else
+        std::memset(out + w0, 0, sizeof(uint32_t) * nw);  // rate 1: zeros, nothing drawn
+      w0 += nw;
+    }
+}
+
+int kp_rng_conve_masks_enqueue(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t n_seg,
+                               const int32_t* seg_elems, const double* seg_keep, uint32_t* out) {
+  if (!ts || tlen < 24 + kN * 8 || (n_steps > 0 && n_seg > 0 && !out)) return KP_EINVAL;
+  uint64_t total = 0;
+  int rc = conve_mask_plan(n_steps, rows, n_seg, seg_elems, seg_keep, &total);
+  if (rc != KP_OK) return rc;
   try {
     TorchMt mt;
     mt.load(ts);
     std::vector<int32_t> rv(rows, rows + n_steps);
-    uint64_t total = 0;
-    for (int st = 0; st < n_steps; ++st) {
-      if (rv[st] < 0) return KP_EINVAL;
-      total += (uint64_t)rv[st] * (uint64_t)dim;
-    }
-    if (total == 0) return KP_OK;
+    std::vector<int32_t> ev(seg_elems, seg_elems + n_seg);
+    std::vector<double> kv(seg_keep, seg_keep + n_seg);
     TorchMt adv = mt;
-    adv.skip(2 * total);  // bernoulli_: one random64 (two outputs) per element
+    adv.skip(2 * total);
     Task fill = [=](Scratch& sc) {
       TorchMt m = mt;
-      size_t w0 = 0;
-      for (int st = 0; st < n_steps; ++st) {
-        const uint64_t n = (uint64_t)rv[st] * (uint64_t)dim;
-        bernoulli_words(m, n, keep, out + w0, sc.draw);
-        w0 += (size_t)((n + 31) / 32);
-      }
+      conve_mask_fill(m, n_steps, rv.data(), n_seg, ev.data(), kv.data(), out, sc.draw);
     };
     if (!DrawQueue::get().enqueue(Task(), fill)) {
-      const int rc = DrawQueue::get().wait();
+      rc = DrawQueue::get().wait();
       if (rc != KP_OK) return rc;
       Scratch sc;
       fill(sc);
@@ -1066,19 +1097,17 @@ int kp_rng_wait(void) {
   return rw != KP_OK ? rw : rd;
 }
 
-int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t dim, double keep,
-                       uint32_t* out) {
-  if (!ts || tlen < 24 + kN * 8 || n_steps < 0 || dim <= 0 || (n_steps > 0 && (!rows || !out))) return KP_EINVAL;
+int kp_rng_conve_masks(uint8_t* ts, size_t tlen, int32_t n_steps, const int32_t* rows, int32_t n_seg,
+                       const int32_t* seg_elems, const double* seg_keep, uint32_t* out) {
+  if (!ts || tlen < 24 + kN * 8 || (n_steps > 0 && n_seg > 0 && !out)) return KP_EINVAL;
+  uint64_t total = 0;
+  const int rc = conve_mask_plan(n_steps, rows, n_seg, seg_elems, seg_keep, &total);
+  if (rc != KP_OK) return rc;
   try {
     TorchMt mt;
     mt.load(ts);
     std::vector<uint32_t> buf;
-    size_t w0 = 0;
-    for (int st = 0; st < n_steps; ++st) {
-      const uint64_t n = (uint64_t)rows[st] * (uint64_t)dim;
-      bernoulli_words(mt, n, keep, out + w0, buf);  // each step's mask starts on a word
-      w0 += (size_t)((n + 31) / 32);
-    }
+    conve_mask_fill(mt, n_steps, rows, n_seg, seg_elems, seg_keep, out, buf);
     mt.store(ts);
   } catch (...) {
     return KP_ENOMEM;

@@ -462,6 +462,43 @@ void launch_te_scores(kp_ctx* c, int nq, const int32_t* dh, const int32_t* dr, c
   KP_HIP(hipGetLastError());
 }
 
+// fp64 ranking queries (launch_rank_f64, RANK64_DIST): the translation q = x + R_p of
+// the post-trained row in fp64 (exact: two fp32 operands), its squared distance to the
+// target and to the kelpie row as one sequential fp64 FMA chain over d, the order
+// kp_rank_f64_count scores every entity in.  An fp32 norm over 200 terms is ~1e-7
+// relative off, enough to swap near-tied entities (FB15k-237 necessary fixtures).
+__global__ void kp_te_rankq64(const float* __restrict__ X, const float* __restrict__ R,
+                              const float* __restrict__ E, int n_ent, int dp, const int32_t* __restrict__ pred,
+                              int n_slots, double* __restrict__ Q, double* __restrict__ t64,
+                              double* __restrict__ kcol64) {
+  const int s = blockIdx.x;
+  if (s >= n_slots) return;
+  const float* x = X + (size_t)s * dp;
+  const float* r = R + (size_t)pred[3 * s + 1] * dp;
+  double* q = Q + (size_t)s * dp;
+  for (int d = threadIdx.x; d < dp; d += blockDim.x) q[d] = (double)x[d] + (double)r[d];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int o = pred[3 * s + 2];
+    double z = 0.0, t = 0.0;
+    for (int d = 0; d < dp; ++d) {
+      const double df = q[d] - (double)x[d];
+      z = __fma_rn(df, df, z);
+    }
+    if (o < n_ent) {
+      const float* eo = E + (size_t)o * dp;
+      for (int d = 0; d < dp; ++d) {
+        const double df = q[d] - (double)eo[d];
+        t = __fma_rn(df, df, t);
+      }
+    } else {
+      t = z;  // the kelpie entity is its own object
+    }
+    kcol64[s] = z;
+    t64[s] = t;
+  }
+}
+
 }  // namespace
 
 void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
@@ -557,11 +594,21 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   int32_t* dPo = upload(c, c->ws[6], po.data(), po.size());
   int32_t* dFo = upload(c, c->ws[7], bt->filt_off, (size_t)ns + 1);
   int32_t* dF = upload(c, c->ws[8], bt->filt, (size_t)std::max(1, bt->filt_off[ns]));
-  float* dScores = reinterpret_cast<float*>(c->ws[9].ensure(sizeof(float) * (size_t)ns * ld));
   float* dTarget = reinterpret_cast<float*>(c->ws[10].ensure(sizeof(float) * ns));
   int64_t* dRank = reinterpret_cast<int64_t*>(c->ws[11].ensure(sizeof(int64_t) * ns));
-  launch_te_scores(c, ns, dH, dRl, dX, dScores, ld, c->n_ent);
-  launch_rank_count(c, ns, dScores, ld, c->n_ent + 1, dPo, dFo, dF, 1, dTarget, dRank);
+  if (c->te_rank64) {
+    int32_t* dPred = upload(c, c->ws[13], bt->pred, (size_t)ns * 3);
+    double* dQ64 = reinterpret_cast<double*>(c->ws[29].ensure(sizeof(double) * (size_t)ns * DP));
+    double* dT64 = reinterpret_cast<double*>(c->ws[30].ensure(sizeof(double) * 2 * (size_t)ns));
+    hipLaunchKernelGGL(kp_te_rankq64, dim3(ns), dim3(64), 0, c->stream, dX, c->dR, c->dE, c->n_ent, DP, dPred, ns,
+                       dQ64, dT64, dT64 + ns);
+    KP_HIP(hipGetLastError());
+    launch_rank_f64(c, ns, dQ64, dT64, dT64 + ns, dPo, dFo, dF, dTarget, dRank, RANK64_DIST);
+  } else {
+    float* dScores = reinterpret_cast<float*>(c->ws[9].ensure(sizeof(float) * (size_t)ns * ld));
+    launch_te_scores(c, ns, dH, dRl, dX, dScores, ld, c->n_ent);
+    launch_rank_count(c, ns, dScores, ld, c->n_ent + 1, dPo, dFo, dF, 1, dTarget, dRank);
+  }
   KP_HIP(hipEventRecord(c->ev1, c->stream));
   if (bt->out_x) {
     KP_HIP(hipMemcpyAsync(xp.data(), dX, sizeof(float) * xp.size(), hipMemcpyDeviceToHost, c->stream));

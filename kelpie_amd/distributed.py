@@ -17,7 +17,9 @@ slots, the numpy one by simulating the TransE shuffles, whose consumption is
 data-dependent).  Claims are made while scheduling, in slot order, by the same
 greedy rule on every rank: a slot goes to the rank with the least claimed row count so
 far (ties to the lowest rank).  One all-gather of fixed-size (slot, score, rank)
-records per batch (RCCL over xGMI with the ``nccl`` backend, ``gloo`` on CPU) gives
+records per batch (RCCL over xGMI with the ``nccl`` backend, ``gloo`` on CPU; every
+rank sends a block of the same size, known from the claims, so it is a single
+collective with no count exchange) gives
 every rank every result, so the builder's accept / early-exit / ``random.random()``
 replay runs identically on all ranks; each rank's record set carries a status row, so
 a rank whose device work failed makes every rank raise instead of leaving the others
@@ -112,33 +114,48 @@ class SlotSharding:
         self.world = dist.get_world_size() if world is None and init else (world or 1)
         self.device = device
         self.gathers = 0
+        self.collectives = 0  # collective calls issued (the slot gather: one per batch)
         self.loads = [0] * self.world
 
     def begin_batch(self):
         """Start claiming the slots of a new engine batch."""
         self.loads = [0] * self.world
 
-    def claim(self, cost) -> bool:
+    def claim_owner(self, cost) -> int:
         """Assign the next slot of the batch (in scheduling order) to the rank with the
-        least claimed cost so far, ties to the lowest rank; True if that is this rank.
-        Every rank makes the same calls in the same order, so all agree."""
+        least claimed cost so far, ties to the lowest rank, and return that rank.  Every
+        rank makes the same calls in the same order, so all agree on every owner."""
         loads = self.loads
         r = loads.index(min(loads))  # the first (lowest) rank among the least loaded
         loads[r] += int(cost)
-        return r == self.rank
+        return r
 
-    def gather_slots(self, idx, score, rank, n, failed=False):
+    def claim(self, cost) -> bool:
+        """:meth:`claim_owner`, True if the slot is this rank's."""
+        return self.claim_owner(cost) == self.rank
+
+    def gather_slots(self, idx, score, rank, n, failed=False, counts=None):
         """Every rank's (slot index, score, rank) records -> full [n] score / rank arrays.
-        Each rank adds a status record (index -1, its failure flag); if any rank failed,
-        every rank raises after the gather."""
-        recs = np.zeros((len(idx) + 1, 3), np.float64)
+
+        ``counts[r]``: the slots rank r owns (every rank knows them from the claims), so
+        every rank sends the same fixed-size block -- its records, padding rows (index
+        -2) and a status row (index -1, its failure flag) -- in ONE all-gather, with no
+        count exchange.  A rank whose device work failed sends only padding and its
+        status; if any rank failed, every rank raises after the gather."""
+        if counts is None:  # a caller without the owners: exchange the counts first
+            counts = self._gather_counts(len(idx))
+        m = int(max(counts)) + 1 if len(counts) else 1
+        if len(idx) > m - 1:
+            raise RuntimeError("slot sharding: more records than the slots this rank owns")
+        recs = np.zeros((m, 3), np.float64)
+        recs[:, 0] = -2.0
         if len(idx):
-            recs[:-1, 0] = idx
-            recs[:-1, 1] = np.asarray(score, np.float64)
-            recs[:-1, 2] = np.asarray(rank, np.float64)
+            recs[:len(idx), 0] = idx
+            recs[:len(idx), 1] = np.asarray(score, np.float64)
+            recs[:len(idx), 2] = np.asarray(rank, np.float64)
         recs[-1] = (-1.0, 1.0 if failed else 0.0, float(self.rank))
-        allr = self._gather(recs, 3)
-        bad = [int(rk) for i, st, rk in allr if i < 0 and st != 0]
+        allr = self._gather_fixed(recs)
+        bad = [int(rk) for i, st, rk in allr if i == -1 and st != 0]
         if bad:
             raise RuntimeError(f"slot sharding: the device work of rank(s) {bad} failed")
         out_s = np.zeros(n, np.float32)
@@ -156,28 +173,38 @@ class SlotSharding:
 
     def gather_mask(self, lo, hi, keep, n):
         """Keep flags of the entity range [lo, hi) from every rank -> the full [n] mask."""
-        recs = np.zeros((hi - lo, 2), np.float64)
-        recs[:, 0] = np.arange(lo, hi)
-        recs[:, 1] = np.asarray(keep, np.float64)
-        allr = self._gather(recs, 2)
+        # every rank's range is [n r / w, n (r + 1) / w): fixed-size blocks, one collective
+        m = max(1, max((n * (r + 1)) // self.world - (n * r) // self.world for r in range(self.world)))
+        recs = np.zeros((m, 2), np.float64)
+        recs[:, 0] = -1.0
+        recs[:hi - lo, 0] = np.arange(lo, hi)
+        recs[:hi - lo, 1] = np.asarray(keep, np.float64)
+        allr = self._gather_fixed(recs)
+        allr = allr[allr[:, 0] >= 0]
         out = np.zeros(n, bool)
         out[allr[:, 0].astype(np.int64)] = allr[:, 1] != 0
         return out
 
-    def _gather(self, recs, width):
+    def _gather_fixed(self, recs):
+        """All-gather one [m, width] float64 block per rank (the same m on every rank):
+        one collective, no host synchronisation before it."""
         self.gathers += 1
+        self.collectives += 1
         if self.world == 1 or not dist.is_initialized():
             return recs
         device = self.device or _device()
-        cnt = torch.tensor([recs.shape[0]], dtype=torch.int64, device=device)
+        buf = torch.from_numpy(np.ascontiguousarray(recs)).to(device)
+        out = torch.empty((self.world * recs.shape[0], recs.shape[1]), dtype=torch.float64, device=device)
+        dist.all_gather_into_tensor(out, buf)
+        return out.cpu().numpy()
+
+    def _gather_counts(self, n):
+        self.collectives += 1
+        if self.world == 1 or not dist.is_initialized():
+            return [n]
+        device = self.device or _device()
+        cnt = torch.tensor([n], dtype=torch.int64, device=device)
         counts = [torch.zeros_like(cnt) for _ in range(self.world)]
         dist.all_gather(counts, cnt)
-        counts = [int(c.item()) for c in counts]
-        m = max(counts)
-        buf = torch.zeros((max(m, 1), width), dtype=torch.float64, device=device)
-        if recs.shape[0]:
-            buf[:recs.shape[0]] = torch.from_numpy(recs).to(device)
-        out = torch.zeros((self.world * max(m, 1), width), dtype=torch.float64, device=device)
-        dist.all_gather_into_tensor(out, buf)
-        out = out.cpu().numpy().reshape(self.world, max(m, 1), width)
-        return np.concatenate([out[r, :counts[r]] for r in range(self.world)])
+        return [int(c.item()) for c in counts]
+

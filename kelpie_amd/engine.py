@@ -42,6 +42,9 @@ class _Slot:
     # False: another rank post-trains this slot (kelpie_amd.distributed); only the
     # generators were advanced past its draws, and x0 / rows / rng / filt may be None
     own: bool = True
+    # the rank that post-trains it (sharded batches; every rank records every owner, so
+    # each knows every rank's record count in the gather)
+    owner: int = 0
     # rows and filter held by the library's host scheduler instead of rows / filt:
     # (SchedBatch, its slot index, row count, filter length) (kelpie_amd/_lib.py)
     native: tuple = None
@@ -62,19 +65,20 @@ def _contiguous_draws(slots, total, ctx=None):
     arrays = [s.rng.reshape(-1) for s in slots]
     from . import _lib
     live = [a for a in arrays if a.size]
-    if live and _lib.is_pinned(live[0]):
+    lease = _lib.arena_of(live[0]) if live else None
+    if lease is not None:
         # the draws were written back to back into one page-locked arena in slot order
-        # (the usual case): hand the library that span, which it uploads by DMA
-        base = live[0].base if isinstance(live[0].base, np.ndarray) else live[0]
+        # (the usual case): hand the library that span (a view of the lease, which keeps
+        # the arena busy while the library reads it), uploaded by DMA
         start = live[0].__array_interface__["data"][0]
         pos = start
         for a in live:
-            if a.base is not base or a.__array_interface__["data"][0] != pos or a.dtype.itemsize != 4:
+            if _lib.arena_of(a) is not lease or a.__array_interface__["data"][0] != pos or a.dtype.itemsize != 4:
                 break
             pos += 4 * a.size
         else:
-            off = (start - base.__array_interface__["data"][0]) // 4
-            return base[off:off + total]
+            off = (start - lease.__array_interface__["data"][0]) // 4
+            return lease[off:off + total]
     if ctx is None or any(a.dtype.itemsize != 4 for a in arrays):
         return np.concatenate(arrays).astype(np.int32, copy=False)
     buf = getattr(ctx, "_draw_buf", None)
@@ -224,14 +228,16 @@ class PostTrainingEngine(RelevanceEngine):
         m, rng, sh = self.model, self.rng, self.sharding
         kp = view.as_kelpie_triple(pred)
         need_base = pred not in self.base_pt_results and pred not in pending_base
-        own_base = need_base and sh.claim(max(1, len(view.base_rows)))
+        base_owner = sh.claim_owner(max(1, len(view.base_rows))) if need_base else -1
+        own_base = base_owner == sh.rank
         edit = view.removed if mode == "necessary" else view.added
         try:
             n_pt, _ = edit(triples, rows=False)  # the reference raises after the draws below
             err = None
         except Exception as e:  # noqa: BLE001 -- re-raised at the reference's point
             err, n_pt = e, 0
-        own_pt = err is None and sh.claim(max(1, n_pt))
+        pt_owner = sh.claim_owner(max(1, n_pt)) if err is None else -1
+        own_pt = pt_owner == sh.rank
         if own_base or own_pt:
             init = rng.rand_init(m.dimension)
         else:
@@ -245,6 +251,7 @@ class PostTrainingEngine(RelevanceEngine):
                 slots.append(self._slot(x_base, view.base_rows, kp, view.filter_for(kp[1])))
             else:
                 slots.append(self._skip_slot(kp, view.base_rows, len(view.base_rows)))
+            slots[-1].owner = base_owner
         x_pt = m.kelpie_init(init, rng) if own_pt else m.kelpie_skip(rng)
         if err is not None:
             raise err
@@ -254,6 +261,7 @@ class PostTrainingEngine(RelevanceEngine):
             slots.append(self._slot(x_pt, rows, kp, view.filter_for(kp[1], delta.get(kp[1]))))
         else:
             slots.append(self._skip_slot(kp, rows if m.skip_needs_rows else None, n_pt))
+        slots[-1].owner = pt_owner
         return len(slots) - 1, pred
 
     def _schedule_fused(self, pred, view, triples, mode, slots, pending_base):
@@ -267,20 +275,24 @@ class PostTrainingEngine(RelevanceEngine):
         need_base = pred not in self.base_pt_results and pred not in pending_base
         sharded = self._sharded()
         nb = view.n_base_rows
-        own_base = need_base and (not sharded or self.sharding.claim(max(1, nb)))
+        base_owner = pt_owner = 0
+        if sharded and need_base:
+            base_owner = self.sharding.claim_owner(max(1, nb))
+        own_base = need_base and (not sharded or base_owner == self.sharding.rank)
         if sharded:
             # owners from row counts known before the edit: the base rows +- the rule's
             # rows (kelpie_amd.distributed); every rank still runs every edit's checks
             est = nb + 2 * len(triples) if mode == "sufficient" else nb - 2 * len(triples)
-            own_pt = self.sharding.claim(max(1, est))
+            pt_owner = self.sharding.claim_owner(max(1, est))
+            own_pt = pt_owner == self.sharding.rank
         else:
             own_pt = True
         base = None
         if need_base:
             pending_base[pred] = len(slots)
-            base = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_base)
+            base = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_base, owner=base_owner)
             slots.append(base)
-        pt = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_pt)
+        pt = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_pt, owner=pt_owner)
         slots.append(pt)
         self._fused.append({"view": view, "kp": kp, "triples": [(int(a), int(b), int(c)) for a, b, c in triples],
                             "flags": (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
@@ -369,7 +381,8 @@ class PostTrainingEngine(RelevanceEngine):
                     score, rank = stats.pop("_score"), stats.pop("_rank")
                 except Exception as e:  # noqa: BLE001 -- raised on every rank by _collect
                     err, mine = e, []
-            stats["_local"] = (mine, score, rank, len(slots), err)
+            counts = np.bincount([s.owner for s in slots], minlength=self.sharding.world)
+            stats["_local"] = (mine, score, rank, len(slots), err, counts)
             self.last_batch_stats = stats
             return stats
         return self._run_slots(slots, ctx, fill=True)
@@ -379,10 +392,10 @@ class PostTrainingEngine(RelevanceEngine):
         local = stats.pop("_local", None) if stats else None
         if local is None:
             return
-        mine, score, rank, n, err = local
+        mine, score, rank, n, err, counts = local
         t0 = time.perf_counter()
         try:
-            all_s, all_r = self.sharding.gather_slots(mine, score, rank, n, failed=err is not None)
+            all_s, all_r = self.sharding.gather_slots(mine, score, rank, n, failed=err is not None, counts=counts)
         except Exception:
             if err is not None:
                 raise err
@@ -512,7 +525,12 @@ class PostTrainingEngine(RelevanceEngine):
                 slots, _, _ = self._schedule_all(items, None)
             self._deferred_error = None
             for ctx in ctxs[1:]:
-                self._run(slots, ctx=ctx)
+                st = self._run(slots, ctx=ctx)
+                # a warm-up has no gather (_collect), so a sharded run's captured device
+                # error is raised here (each rank warms the slots it owns)
+                local = st.get("_local") if st else None
+                if local is not None and local[4] is not None:
+                    raise local[4]
         finally:
             cp.restore()
             self.set_cache()

@@ -195,13 +195,17 @@ class ConvE(FrozenModel):
         d = self.dimension
         if d % 20 or d // 20 < 3:
             raise ValueError("ConvE dimension must be 20*h with h >= 3")
-        if input_dropout_rate or feature_map_dropout_rate:
-            raise NotImplementedError("ConvE input / feature-map dropout > 0 during post-training")
+        for rate in (input_dropout_rate, feature_map_dropout_rate, hidden_dropout_rate):
+            if not 0.0 <= float(rate) <= 1.0:
+                raise ValueError(f"dropout probability has to be between 0 and 1, but got {rate}")
         self.hidden_layer_size = 32 * 38 * (d // 20 - 2)
         self.conv_weight = np.asarray(conv_weight, np.float32).reshape(32, 3, 3)
         self.conv_bias = np.asarray(conv_bias, np.float32).reshape(32)
         self.fc_weight = np.asarray(fc_weight, np.float32).reshape(d, self.hidden_layer_size)
         self.fc_bias = np.asarray(fc_bias, np.float32).reshape(d)
+        # the three dropouts stay in train mode during post-training (model.py:114-125)
+        self.input_dropout_rate = float(input_dropout_rate)
+        self.feature_map_dropout_rate = float(feature_map_dropout_rate)
         self.hidden_dropout_rate = float(hidden_dropout_rate)
         alpha, beta = [], []
         for i, c in ((1, 1), (2, 32), (3, d)):
@@ -229,7 +233,8 @@ class ConvE(FrozenModel):
     def kp_hp(self, hp):
         return _lib.HP(optimizer=_lib.KP_OPT["Adam"], epochs=int(hp["epochs"]), batch_size=int(hp["batch_size"]),
                        lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, label_smoothing=float(hp["label_smoothing"]),
-                       hidden_dropout=self.hidden_dropout_rate)
+                       hidden_dropout=self.hidden_dropout_rate, input_dropout=self.input_dropout_rate,
+                       fmap_dropout=self.feature_map_dropout_rate)
 
     def er_vocab_sizes(self, rows: np.ndarray, batch_size: int, epochs: int):
         pairs = {}
@@ -239,17 +244,26 @@ class ConvE(FrozenModel):
         per_epoch = [min(batch_size, P - s) for s in range(0, P, batch_size)]
         return per_epoch * epochs
 
+    def dropout_segments(self):
+        """(elements per pair, rate) of each dropout in the forward's draw order: the
+        input dropout over the stacked 40 x (d/20) image, the feature-map Dropout2d over
+        the 32 channels, the hidden dropout over d (conve.py:142,147,151)."""
+        return [(2 * self.dimension, self.input_dropout_rate), (32, self.feature_map_dropout_rate),
+                (self.dimension, self.hidden_dropout_rate)]
+
     def posttrain_draws(self, rows, hp, rng):
         steps = self.er_vocab_sizes(rows, int(hp["batch_size"]), int(hp["epochs"]))
-        return rng.conve_masks(steps, self.dimension, self.hidden_dropout_rate)
+        return rng.conve_masks(steps, self.dropout_segments())
 
     def kelpie_skip(self, rng):
         rng.conve_construction(self.hidden_layer_size, self.dimension)
 
     def posttrain_skip(self, rows, n_rows, hp, rng):
-        if self.hidden_dropout_rate > 0.0:
+        # bernoulli_: one random64 (two outputs) per element; rate 0 and rate 1 draw nothing
+        per_pair = sum(n for n, p in self.dropout_segments() if 0.0 < p < 1.0)
+        if per_pair:
             steps = self.er_vocab_sizes(rows, int(hp["batch_size"]), int(hp["epochs"]))
-            rng.discard(2 * self.dimension * int(sum(steps)))  # bernoulli_: one random64 per element
+            rng.discard(2 * per_pair * int(sum(steps)))
 
 
 MODEL_REGISTRY = {"ComplEx": ComplEx, "TransE": TransE, "ConvE": ConvE}

@@ -112,10 +112,19 @@ def _flush_skip():
 def sync():
     """Wait for every queued TransE draw (the numpy global state is then current) and
     apply any pending torch-generator advance."""
-    global _outstanding
+    global _outstanding, _torch_async, _skip
     if _outstanding:
         _outstanding = False
-        _lib.rng_wait()
+        try:
+            _lib.rng_wait()
+        except Exception:
+            # a failed walk or draw task: the stream it carried is partial, so drop the
+            # asynchronous state and the pending advance instead of installing either
+            # on a later draw, then report the failure
+            _torch_async = False
+            _skip = 0
+            _inflight.clear()
+            raise
     _inflight.clear()
     _flush_skip()  # also takes the torch stream back from an asynchronous walk
 
@@ -146,7 +155,11 @@ class ReferenceRNG:
     # The deferred draws of one block are laid out back to back in an arena, so the
     # engine ships a batch's draws without concatenating them (engine._run).  A fresh
     # arena per block: the arrays of an earlier batch may still be in flight.
-    _ARENA = 1 << 24  # int32 words (64 MiB of address space; untouched pages cost nothing)
+    # int32 words of a fresh arena: one TransE FB15k-237 batch's draws (~6 M words) fit, so
+    # they stay one contiguous span.  A pooled page-locked arena (_lib.pinned_i32) is
+    # committed and locked when allocated: the pool holds at most KP_PINNED_ARENAS (4) of
+    # them, 256 MiB per process; a pageable one commits only the pages written.
+    _ARENA = 1 << 24
 
     def _take(self, n: int) -> np.ndarray:
         if self._arena is None or self._arena_pos + n > self._arena.size:
@@ -248,10 +261,13 @@ class ReferenceRNG:
             else:
                 st = _state_shape()
             out = self._take(total) if total else None
-            xb, xp = _lib.transe_calls_async(st, addr, addr + 4 * 624, _lib.normal_cap(), D, d, std, R_base, R_pt,
-                                             epochs, ratio, n_entities, out, wa)
+            xb, xp, queued = _lib.transe_calls_async(st, addr, addr + 4 * 624, _lib.normal_cap(), D, d, std, R_base,
+                                                     R_pt, epochs, ratio, n_entities, out, wa)
             _inflight.extend((xb, xp))  # the walk writes them until sync(), wanted or not
-            _torch_async = True
+            if queued:
+                _torch_async = True
+            else:  # walked inline (no walker thread): st is the advanced stream, nothing carried
+                _set_state(st)
             _outstanding = True
         else:
             _flush_skip()
@@ -271,19 +287,24 @@ class ReferenceRNG:
             off += a + b
         return xb, xp, draws
 
-    def conve_masks(self, n_rows_per_step, dim: int, p_drop: float) -> np.ndarray:
-        """Hidden-dropout keep bits for every step, packed per step in uint32 words."""
-        if p_drop <= 0.0 or len(n_rows_per_step) == 0:
+    def conve_masks(self, n_rows_per_step, segs) -> np.ndarray:
+        """ConvE dropout keep bits for every step, packed per step and dropout in uint32
+        words.  ``segs`` = [(elements per pair, rate)] of the dropouts with a non-zero
+        rate, in the forward's order (input image, feature-map channels, hidden;
+        conve.py:142,147,151)."""
+        segs = [(int(n), float(p)) for n, p in segs if p > 0.0]
+        if not segs or len(n_rows_per_step) == 0:
             return np.zeros(0, np.int32)
+        keep = [(n, 1.0 - p) for n, p in segs]
         global _outstanding
         _flush_skip()
         st = _get_state()
         if self._defer_depth:
-            words = _lib.conve_masks_enqueue(st, n_rows_per_step, dim, 1.0 - p_drop,
-                                             self._take(_lib.mask_words(n_rows_per_step, dim)))
+            words = _lib.conve_masks_enqueue(st, n_rows_per_step, keep,
+                                             self._take(_lib.mask_words(n_rows_per_step, [n for n, _ in keep])))
             _outstanding = True
         else:
-            words = _lib.conve_masks(st, n_rows_per_step, dim, 1.0 - p_drop)
+            words = _lib.conve_masks(st, n_rows_per_step, keep)
         _set_state(st)
         return words.view(np.int32)
 

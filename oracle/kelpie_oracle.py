@@ -223,13 +223,19 @@ class OracleModel:
         c, dd = rel[..., :d], rel[..., d:]
         return np.concatenate([a * c - b * dd, a * dd + b * c], axis=-1).astype(F32)
 
-    def conve_encode(self, lhs, rel, hidden_mask=None):
-        """ConvE encoder (conve.py:133-153).  Returns (x, cache for backward)."""
+    def conve_encode(self, lhs, rel, hidden_mask=None, in_mask=None, fm_mask=None):
+        """ConvE encoder (conve.py:133-153).  Returns (x, cache for backward).
+
+        The three dropout multipliers (conve.py:142,147,151; ``None``: not drawn) are
+        ``in_mask`` (b, 40, eh) on the BN1 image, ``fm_mask`` (b, 32) per feature-map
+        channel after the ReLU and ``hidden_mask`` (b, d) on the FC output."""
         b = lhs.shape[0]
         d = self.dim
         img = np.concatenate([lhs.reshape(b, 20, self.eh), rel.reshape(b, 20, self.eh)], axis=1)  # (b,40,eh)
         a1, b1 = self.bn[1]
         img_bn = (img * a1[0] + b1[0]).astype(F32)
+        if in_mask is not None:
+            img_bn = (img_bn * in_mask.reshape(b, 40, self.eh)).astype(F32)
         W = self.w["conv_weight"][:, 0]  # (32,3,3)
         H, Wd = 38, self.eh - 2
         # per channel: the nine taps accumulated in (ky, kx) order on cache-sized arrays
@@ -247,6 +253,8 @@ class OracleModel:
         a2, b2 = self.bn[2]
         c_bn = (conv * a2[None, :, None, None] + b2[None, :, None, None]).astype(F32)
         c_relu = np.maximum(c_bn, 0).astype(F32)
+        if fm_mask is not None:
+            c_relu = (c_relu * fm_mask.reshape(b, 32, 1, 1)).astype(F32)
         flat = c_relu.reshape(b, -1)
         fc = (flat @ self.w["fc_weight"].T + self.w["fc_bias"]).astype(F32)
         if hidden_mask is not None:
@@ -256,11 +264,11 @@ class OracleModel:
         a3, b3 = self.bn[3]
         h_bn = (fc_d * a3 + b3).astype(F32)
         x = np.maximum(h_bn, 0).astype(F32)
-        return x, (c_bn, h_bn, hidden_mask)
+        return x, (c_bn, h_bn, hidden_mask, in_mask, fm_mask)
 
     def conve_backward_lhs(self, dx, cache):
         """d loss / d lhs-embedding through the frozen encoder (ConvE)."""
-        c_bn, h_bn, mask = cache
+        c_bn, h_bn, mask, in_mask, fm_mask = cache
         b = dx.shape[0]
         a3, _ = self.bn[3]
         g = dx * (h_bn > 0)
@@ -269,7 +277,10 @@ class OracleModel:
             g = g * mask
         dflat = (g @ self.w["fc_weight"]).astype(F32)  # (b, hidden)
         H, Wd = 38, self.eh - 2
-        dc = dflat.reshape(b, 32, H, Wd) * (c_bn > 0)
+        dc = dflat.reshape(b, 32, H, Wd)
+        if fm_mask is not None:
+            dc = dc * fm_mask.reshape(b, 32, 1, 1)
+        dc = dc * (c_bn > 0)
         a2, _ = self.bn[2]
         dc = dc * a2[None, :, None, None]
         W = self.w["conv_weight"][:, 0]
@@ -277,6 +288,8 @@ class OracleModel:
         for ky in range(3):
             for kx in range(3):
                 dimg[:, ky:ky + H, kx:kx + Wd] += np.einsum("bchw,c->bhw", dc, W[:, ky, kx])
+        if in_mask is not None:
+            dimg = dimg * in_mask.reshape(b, 40, self.eh)
         a1, _ = self.bn[1]
         dimg = dimg * a1[0]
         return dimg[:, :20, :].reshape(b, self.dim).astype(F32)
@@ -670,7 +683,7 @@ def posttrain_conve(model: OracleModel, ds, triples, x0, hp, rng):
     x = x0.astype(F32).copy()
     d = model.dimension
     opt = AdamState(d, 1e-3)
-    p_hid = model.hidden_dropout
+    p_hid, p_in, p_fm = model.hidden_dropout, model.input_dropout, model.fmap_dropout
     for _ in range(int(hp["epochs"])):
         start = 0
         while start < len(pairs):
@@ -684,9 +697,14 @@ def posttrain_conve(model: OracleModel, ds, triples, x0, hp, rng):
             if ls:
                 y = (F32(1.0 - ls) * y).astype(F32)
                 y = (y + F32(1.0 / N)).astype(F32)
+            # the forward's draw order: input dropout over the (b, 1, 40, eh) image, the
+            # feature-map Dropout2d over (b, 32), the hidden dropout over (b, d)
+            # (conve.py:142,147,151; nothing drawn at rate 0, ATen _dropout_impl)
+            m_in = rng.dropout_mask((b, 2 * d), p_in) if p_in > 0 else None
+            m_fm = rng.dropout_mask((b, 32), p_fm) if p_fm > 0 else None
             mask = rng.dropout_mask((b, d), p_hid) if p_hid > 0 else None
             E = np.vstack([model.E, x[None]])
-            enc, cache = model.conve_encode(E[hs], model.R[rs], mask)
+            enc, cache = model.conve_encode(E[hs], model.R[rs], mask, m_in, m_fm)
             s = (enc @ E.T).astype(F32)
             p = (1.0 / (1.0 + np.exp(-s.astype(np.float64)))).astype(F32)
             # BCELoss + sigmoid backward (torch): (p-y)/max(p(1-p),1e-12) * p(1-p) / (b*N)
@@ -696,7 +714,7 @@ def posttrain_conve(model: OracleModel, ds, triples, x0, hp, rng):
             hk = hs == k
             if hk.any():
                 denc = (G[hk] @ E.astype(np.float64)).astype(F32)
-                sub = (cache[0][hk], cache[1][hk], None if mask is None else mask[hk])
+                sub = tuple(None if a is None else a[hk] for a in cache)
                 g += model.conve_backward_lhs(denc, sub).sum(0)
             x = opt.step(x, g.astype(F32))
             start += bs
@@ -758,7 +776,10 @@ class TorchNumpyRNG:
         torch.nn.Linear(hidden, dim)
 
     def dropout_mask(self, shape, p):
-        # ATen CPU dropout: empty_like(x).bernoulli_(1-p).div_(1-p)
+        # ATen CPU dropout (_dropout_impl): zeros without a draw at p == 1, else
+        # empty_like(x).bernoulli_(1-p).div_(1-p)
+        if p == 1:
+            return np.zeros(shape, F32)
         m = torch.empty(shape).bernoulli_(1 - p)
         m.div_(1 - p)
         return m.numpy().astype(F32)

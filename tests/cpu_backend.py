@@ -59,11 +59,15 @@ class ReplayRNG:
         return rows[blk[0].astype(np.int64)], blk[1].astype(np.int64), blk[2].astype(np.int64)
 
     def dropout_mask(self, shape, p):
-        n = shape[0] * shape[1]
+        # the shipped layout: per step, one word-aligned run of keep bits per dropout
+        # (input, feature map, hidden: the forward's draw order)
+        n = int(np.prod(shape))
         words = (n + 31) // 32
         w = self.blob[self.off:self.off + words].view(np.uint32)
         self.off += words
         bits = np.unpackbits(w.view(np.uint8), bitorder="little")[:n].astype(np.float32)
+        if p == 1:  # zeros (the library ships zero words and draws nothing)
+            return np.zeros(shape, np.float32)
         scale = np.float32(1.0) / np.float32(1.0 - p)
         return (bits * scale).astype(np.float32).reshape(shape)
 
@@ -91,6 +95,8 @@ class OracleBackedContext:
                 w[f"bn{i}_weight"], w[f"bn{i}_bias"] = a, b
                 w[f"bn{i}_mean"], w[f"bn{i}_var"] = np.zeros(c, np.float32), np.ones(c, np.float32)
             params["hidden_dropout_rate"] = model.hidden_dropout_rate
+            params["input_dropout_rate"] = model.input_dropout_rate
+            params["feature_map_dropout_rate"] = model.feature_map_dropout_rate
         else:
             dim = model.dimension
         self.om = ko.OracleModel(name, w, dim, params)

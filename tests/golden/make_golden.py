@@ -83,6 +83,22 @@ CASES = {
                          hp={"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.995,
                              "epochs": 40},
                          xsi=5.0, suff_xsi=0.9, conve_random_bn=True),
+    # all three ConvE dropouts in train mode during post-training, at the rates of the
+    # reference's ConvE YAGO4-20 config (configs/ConvE_YAGO4-20_training.json: input 0.2,
+    # feature map 0.3, hidden 0.1, 150 epochs): d = 200 runs the fused encoder kernels,
+    # d = 60 the unfused ones
+    "conve_drop_tiny": dict(model="ConvE", shape="tiny", dim=200,
+                            model_params={"dimension": 200, "input_dropout_rate": 0.2, "hidden_dropout_rate": 0.1,
+                                          "feature_map_dropout_rate": 0.3, "hidden_layer_size": 9728},
+                            hp={"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0427, "decay": 0.995,
+                                "epochs": 150},
+                            xsi=5.0, suff_xsi=0.9, conve_random_bn=True, skip_builder=True),
+    "conve60_drop_tiny": dict(model="ConvE", shape="tiny", dim=60,
+                              model_params={"dimension": 60, "input_dropout_rate": 0.2, "hidden_dropout_rate": 0.1,
+                                            "feature_map_dropout_rate": 0.3, "hidden_layer_size": 1216},
+                              hp={"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0427, "decay": 0.995,
+                                  "epochs": 40},
+                              xsi=5.0, suff_xsi=0.9, conve_random_bn=True),
     # the production kernel instantiations (ComplEx D = 400 -> kp_attn3<25>, TransE d = 200),
     # pinned by reference vectors directly (2,000-entity graph; hub subject -> multi-step epochs)
     "complex200_small": dict(model="ComplEx", shape="small", dim=200,

@@ -89,6 +89,8 @@ int main(int argc, char** argv) {
   const int n_slots = 48;
   std::vector<size_t> off(n_slots + 1, 0);
   std::vector<int32_t> mask_rows = {7, 7, 3, 12};
+  const int32_t seg_elems = 200;  // one dropout of 200 units per pair, keep 0.8
+  const double seg_keep = 0.8;
   size_t mask_words = 0;
   for (int r : mask_rows) mask_words += ((size_t)r * 200 + 31) / 32;
   for (int i = 0; i < n_slots; ++i) off[i + 1] = off[i] + (size_t)3 * 3 * (10 + i) + (i % 4 == 3 ? mask_words : 0);
@@ -97,7 +99,7 @@ int main(int argc, char** argv) {
     ok(kp_rng_transe_enqueue(ts.data(), ts.size(), key.data(), &pos, 10 + i, 3, 5, 14542, arena.data() + off[i]),
        "transe_enqueue");
     if (i % 4 == 3)
-      ok(kp_rng_conve_masks_enqueue(ts.data(), ts.size(), (int)mask_rows.size(), mask_rows.data(), 200, 0.8,
+      ok(kp_rng_conve_masks_enqueue(ts.data(), ts.size(), (int)mask_rows.size(), mask_rows.data(), 1, &seg_elems, &seg_keep,
                                     reinterpret_cast<uint32_t*>(arena.data() + off[i] + (size_t)3 * 3 * (10 + i))),
          "conve_masks_enqueue");
   }
@@ -136,7 +138,7 @@ int main(int argc, char** argv) {
   put(xb);
   put(xp);
   std::vector<uint32_t> masks(mask_words);
-  ok(kp_rng_conve_masks(ts.data(), ts.size(), (int)mask_rows.size(), mask_rows.data(), 200, 0.8, masks.data()),
+  ok(kp_rng_conve_masks(ts.data(), ts.size(), (int)mask_rows.size(), mask_rows.data(), 1, &seg_elems, &seg_keep, masks.data()),
      "conve_masks");
   put(masks);
   put(ts);

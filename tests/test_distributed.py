@@ -103,6 +103,9 @@ def _engine_run(name, sharding, backend="cpu"):
         out["builder"] = [(r["rule_to_relevance"], r["#relevances"]) for r in res]
     out["gathers"] = sharding.gathers if sharding is not None else 0
     if sharding is not None:
+        # one collective per gather: every rank's block size is known from the claims
+        assert sharding.collectives == sharding.gathers, (sharding.collectives, sharding.gathers)
+    if sharding is not None:
         # the last batch: this rank scheduled in full only the slots it claimed
         eng.set_cache()
         with eng.rng.deferred():

@@ -10,7 +10,7 @@ import pytest
 from engine_cases import check_builder, check_necessary, check_pipeline, check_pipeline_explain, check_sufficient
 from golden_io import CASES
 
-FAST = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve60_tiny"]
+FAST = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve60_tiny", "conve60_drop_tiny"]
 
 
 @pytest.mark.parametrize("name", FAST)
@@ -24,7 +24,7 @@ def test_sufficient_host_protocol(name):
     check_sufficient(name, "cpu", batched=True)
 
 
-@pytest.mark.parametrize("name", ["transe_tiny", "complex_tiny", "conve60_tiny"])
+@pytest.mark.parametrize("name", ["transe_tiny", "complex_tiny", "conve60_tiny", "conve60_drop_tiny"])
 @pytest.mark.parametrize("window", [1, 4, 32])
 def test_builder_speculative_windows(name, window):
     check_builder(name, "cpu", window=window)

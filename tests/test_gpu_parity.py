@@ -13,7 +13,8 @@ import kelpie_amd as ka
 
 pytestmark = pytest.mark.gpu
 
-GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny", "conve60_tiny", "conve_tiny"]
+GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny", "conve60_tiny", "conve_tiny", "conve_drop_tiny",
+             "conve60_drop_tiny"]
 
 
 @pytest.mark.parametrize("name", GPU_CASES + ["complex200_small", "transe200_small"])
@@ -144,10 +145,14 @@ def test_transe_vs_oracle_full_width(dim):
 CV_HP = {"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0432, "decay": 0.995, "epochs": 25}
 
 
-@pytest.mark.parametrize("dim,p_drop,part", [(200, 0.2, "streamk"), (200, 0.2, "ranges"), (60, 0.0, "auto")])
+@pytest.mark.parametrize("dim,p_drop,part", [(200, 0.2, "streamk"), (200, 0.2, "ranges"), (60, 0.0, "auto"),
+                                              (200, (0.2, 0.3, 0.1), "ranges"), (60, (0.2, 0.3, 0.1), "auto"),
+                                              (200, (0.3, 0.0, 0.0), "auto"), (200, (0.0, 0.5, 0.0), "auto")])
 def test_conve_vs_oracle_full_width(dim, p_drop, part, monkeypatch):
     """d = 200 (the production 20x10 image, FC 9728 -> 200) on a 2,000-entity graph,
-    with the attention partition forced (KP_ATTN_PART)."""
+    with the attention partition forced (KP_ATTN_PART).  ``p_drop``: the hidden dropout
+    rate, or (input, feature map, hidden) rates (conve.py:142,147,151)."""
+    p_in, p_fm, p_hid = p_drop if isinstance(p_drop, tuple) else (0.0, 0.0, p_drop)
     from cpu_backend import OracleBackedContext
     monkeypatch.setenv("KP_ATTN_PART", part)
     from kelpie_amd import synth
@@ -163,7 +168,8 @@ def test_conve_vs_oracle_full_width(dim, p_drop, part, monkeypatch):
     out = {}
     for backend in ("gpu", "cpu"):
         model = ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
-                         w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn, hidden_dropout_rate=p_drop)
+                         w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn, hidden_dropout_rate=p_hid,
+                         input_dropout_rate=p_in, feature_map_dropout_rate=p_fm)
         if backend == "cpu":
             model._ctx = OracleBackedContext(model)
         seed_all(42)

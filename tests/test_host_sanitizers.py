@@ -68,7 +68,7 @@ def _expected(ts, key, pos, tri, n_ent, off, cls):
         n = 9 * (10 + i)
         _lib.transe_enqueue(st, ka, pa, 10 + i, 3, 5, 14542, out=arena[offs[i]:offs[i] + n])
         if i % 4 == 3:
-            _lib.conve_masks_enqueue(st, rows, 200, 0.8, arena[offs[i] + n:offs[i] + n + mw])
+            _lib.conve_masks_enqueue(st, rows, [(200, 0.8)], arena[offs[i] + n:offs[i] + n + mw])
     _lib.rng_wait()
     out += [arena.tobytes(), st.tobytes(), key.tobytes(), posa.tobytes()]
     rb = np.array([12, -1, -1, 30, -1, -1], np.int32)
@@ -84,7 +84,7 @@ def _expected(ts, key, pos, tri, n_ent, off, cls):
     xb, xp = _lib.transe_calls(st, ka, pa, 1, 32, 32, float(np.float32(0.2425)), rb, rp, 4, 5, 14542, calls2, want)
     _lib.rng_wait()
     out += [calls2[:tot2].tobytes(), xb.tobytes(), xp.tobytes()]
-    out.append(_lib.conve_masks(st, rows, 200, 0.8).tobytes())
+    out.append(_lib.conve_masks(st, rows, [(200, 0.8)]).tobytes())
     out += [st.tobytes(), key.tobytes(), posa.tobytes()]
     g = _lib.Graph(n_ent, tri)
     out.append(g.bfs(np.array([0, 1, 2, 3, 5, 8, 13, 21])).tobytes())

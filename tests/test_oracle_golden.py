@@ -45,10 +45,15 @@ def test_oracle_necessary(name):
     # the d = 200 cases: the first (moderate-degree) prediction only on the CPU; the hub
     # prediction after it is checked against the same goldens by the GPU tests
     blocks = rec["necessary"][:1] if name.endswith("_small") else rec["necessary"]
+    # conve_drop_tiny (d = 200, 150 epochs, three dropouts): the first prediction's first
+    # three calls on the CPU, every call on the GPU (tests/test_gpu_parity.py)
+    n_calls = 3 if name == "conve_drop_tiny" else None
+    if n_calls:
+        blocks = blocks[:1]
     for block in blocks:
         eng.set_cache()
         pred = tuple(block["pred"])
-        for ci, call in enumerate(block["calls"]):
+        for ci, call in enumerate(block["calls"][:n_calls]):
             rule = [tuple(t) for t in call["rule"]]
             rel, pt, base = eng.necessary_relevance(pred, rule)
             _check_results(pt, base, call["results"], ci == 0)

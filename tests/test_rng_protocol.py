@@ -86,7 +86,7 @@ def test_conve_masks_match_torch_dropout_sequence():
     rng = ReferenceRNG()
     steps = [3, 7, 1]
     torch.manual_seed(21)
-    words = rng.conve_masks(steps, 20, 0.2)
+    words = rng.conve_masks(steps, [(20, 0.2)])
     after = torch.rand(2)
     torch.manual_seed(21)
     off = 0
@@ -152,6 +152,45 @@ def test_deferred_transe_draws_match_reference_calls():
     assert np.array_equal(np.random.randint(0, 1 << 30, 8), np_after)
 
 
+def _unpack(words, off, n):
+    nw = (n + 31) // 32
+    return np.unpackbits(words[off:off + nw].view(np.uint32).view(np.uint8), bitorder="little")[:n], off + nw
+
+
+@pytest.mark.parametrize("deferred", [False, True])
+def test_conve_three_dropouts_match_torch_forward_sequence(deferred):
+    """The three ConvE dropouts of each step in the forward's order (conve.py:142,147,151):
+    input (b x 40 x h), feature-map Dropout2d (b x 32), hidden (b x d); a rate-1 dropout
+    ships zero words and draws nothing (ATen _dropout_impl), a rate-0 one is absent."""
+    rng = ReferenceRNG()
+    steps = [3, 5, 1]
+    d = 60
+    for rates in ((0.2, 0.3, 0.1), (0.2, 0.0, 0.1), (0.0, 1.0, 0.25), (0.5, 0.3, 0.0)):
+        segs = [(2 * d, rates[0]), (32, rates[1]), (d, rates[2])]
+        torch.manual_seed(31)
+        if deferred:
+            with rng.deferred():
+                words = rng.conve_masks(steps, segs)
+        else:
+            words = rng.conve_masks(steps, segs)
+        after = torch.rand(2)
+        torch.manual_seed(31)
+        off = 0
+        for b in steps:
+            for n, p in segs:
+                if p == 0:
+                    continue
+                if p == 1:
+                    got, off = _unpack(words, off, b * n)
+                    assert not got.any()
+                    continue
+                m = torch.empty(b, n).bernoulli_(1 - p).numpy().reshape(-1).astype(np.uint8)
+                got, off = _unpack(words, off, b * n)
+                assert np.array_equal(got, m), (rates, b, n)
+        assert off == words.size
+        assert torch.equal(torch.rand(2), after), rates
+
+
 def test_deferred_conve_masks_match_torch_dropout_sequence():
     """Deferred masks (kp_rng_conve_masks_enqueue) interleaved with other torch draws
     and a discard, as in a ConvE batch schedule: same bits, same final state."""
@@ -163,7 +202,7 @@ def test_deferred_conve_masks_match_torch_dropout_sequence():
         for steps in plans:
             inits.append(rng.rand_init(6))
             rng.conve_construction(4, 20)
-            got.append(rng.conve_masks(steps, 20, 0.2))
+            got.append(rng.conve_masks(steps, [(20, 0.2)]))
     after = torch.rand(2)
     torch.manual_seed(23)
     for steps, words, init in zip(plans, got, inits):

@@ -15,6 +15,10 @@
 #include <random>
 
 #include "kp_attn3.hpp"  // -I selects the source tree under test (tools/attn_micro.sh)
+#if __has_include("kp_attn5.hpp")
+#include "kp_attn5.hpp"
+#define KP_MICRO_HAS_ATTN5 1
+#endif
 #if __has_include("kp_attn4.hpp")
 #include "kp_attn4.hpp"
 #define KP_MICRO_HAS_ATTN4 1
@@ -144,7 +148,15 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
   KP_HIP(hipMalloc(&dqs, nq * 4));
   KP_HIP(hipMemcpy(dQ, Q.data(), Q.size() * 4, hipMemcpyHostToDevice));
   KP_HIP(hipMemcpy(dqs, qs.data(), nq * 4, hipMemcpyHostToDevice));
+  // KP_MICRO_ATTN5=1: the wave-pair kernel (kp_attn5.hpp) for the D = 400 softmax modes
+  bool use5 = std::getenv("KP_MICRO_ATTN5") && std::atoi(std::getenv("KP_MICRO_ATTN5")) == 1;
+#ifdef KP_MICRO_HAS_ATTN5
+  use5 = use5 && DB == 25 && MODE != ATT_BCE_O;
+  const int slots = c.n_cu * (use5 ? attn5_wpc(&c) : attn3_wpc<DB>(&c));
+#else
+  use5 = false;
   const int slots = c.n_cu * attn3_wpc<DB>(&c);
+#endif
   const AttnPlan plan = attn_plan_ctx(&c, nq, n_ent, slots);
   const int parts = plan.wk.n_parts;
   float *dm, *dl, *dO;
@@ -164,6 +176,14 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
     }
 #endif
     (void)use4;
+#ifdef KP_MICRO_HAS_ATTN5
+    if constexpr (DB == 25 && MODE != ATT_BCE_O) {
+      if (use5) {
+        launch_attn5<MODE>(&c, n_ent, dQ, nq, plan, dm, dl, dO);
+        return;
+      }
+    }
+#endif
     launch_attn3<DB, MODE>(&c, n_ent, dQ, nq, plan, dm, dl, dO, dqs, ylo);
   };
   if (std::getenv("KP_MICRO_RTCAL")) {
@@ -419,9 +439,9 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
            "\"warm_launches\": %d}\n", med, f.empty() ? 0.0 : f.front(), f.empty() ? 0.0 : f.back(), f.size(), warm);
   }
 #endif
-  printf("{\"DB\": %d, \"mode\": %d, \"n_ent\": %d, \"nq\": %d, \"parts\": %d, \"ranges\": %d, \"n_wg\": %d, "
+  printf("{\"kernel\": \"%s\", \"DB\": %d, \"mode\": %d, \"n_ent\": %d, \"nq\": %d, \"parts\": %d, \"ranges\": %d, \"n_wg\": %d, "
          "\"ms\": %.5f, \"tflops\": %.2f, \"frac_bf16x6\": %.4f, \"err_l\": %.3e, \"err_o\": %.3e, \"bits\": \"%016llx\"}\n",
-         DB, MODE, n_ent, nq, parts, plan.wk.ranges, plan.n_wg, ms, flops / ms / 1e9, flops / ms / 1e9 / 419.43,
+         use5 ? "kp_attn5" : "kp_attn3", DB, MODE, n_ent, nq, parts, plan.wk.ranges, plan.n_wg, ms, flops / ms / 1e9, flops / ms / 1e9 / 419.43,
          err_l, err_o, bits);
   return 0;
 }
