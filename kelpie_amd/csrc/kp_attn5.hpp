@@ -43,7 +43,7 @@ constexpr size_t attn5_lds_bytes() { return (size_t)A5_XS_OFF + 8 * 32 * sizeof(
 static_assert(attn5_lds_bytes() <= 160 * 1024, "kp_attn5: LDS over the 160 KiB of a CU");
 static_assert(split3_tile_bytes(A5_DP) == A5_BUF_B, "kp_attn5: a tile is a whole number of DMA pieces");
 
-template <int H, int MODE>
+template <int H, int G, int MODE>
 __device__ __forceinline__ void attn5_half(const uint8_t* __restrict__ E3, int n_ent, const float* __restrict__ Qpre,
                                            int nq, const AttnWork& wk, float* __restrict__ out_m,
                                            float* __restrict__ out_l, float* __restrict__ out_O,
@@ -61,8 +61,8 @@ __device__ __forceinline__ void attn5_half(const uint8_t* __restrict__ E3, int n
   constexpr uint32_t SUB_B = 16u * ROW_B;           // the second sub-tile's rows
   static_assert(SUB_B + 3 * PART_B + 64 * NK < 65536, "LDS read offsets exceed the 16-bit offset field");
   const int g = lane >> 4, c = lane & 15;
-  const int pr = w & 3;  // the pair: queries 16 pr .. 16 pr + 15 of the query tile
-  const int wp = w ^ 4;  // the partner wave (the other half)
+  const int pr = w >> 1;   // the pair: queries 16 pr .. 16 pr + 15 of the query tile
+  const int wp = w ^ 1;    // the partner wave (the other half)
   // exchange slots (floats): slot[w] = lanes x 4; column scalars xs[w][32]
   float* my_slot = xf + w * 256 + 4 * lane;
   float* pa_slot = xf + wp * 256 + 4 * lane;
@@ -162,13 +162,24 @@ __device__ __forceinline__ void attn5_half(const uint8_t* __restrict__ E3, int n
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
 
-      for (int t = 0; t < ntiles; ++t) {
-        const int k0 = key_begin + t * KT;
-        const int tn = t + 1 < ntiles ? t + 1 : t;  // the last tile re-reads its own rows (no branch)
-        const uint32_t tb = lds0 + (uint32_t)((t & 1) * BUF_B);
-        // ---- S: partial S^T of both sub-tiles over this half's dimensions
-        f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
-        const uint32_t rb = tb + (uint32_t)(c * ROW_B + 16 * g);
+      // per-tile state carried from one phase (interval) to the next
+      f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+      bf16x8 pb[3];
+      bf16x4 ol[3][3], oh[3][3];
+      auto tile_base = [&](int t) { return lds0 + (uint32_t)((t & 1) * BUF_B); };
+      auto o_base = [&](int t) { return tile_base(t) + (uint32_t)((4 * g + (c >> 2)) * ROW_B + 8 * (c & 3)); };
+      auto read_o = [&](uint32_t ob, int m, int k) {  // read k of local block m (piece k / 2, rows 4g / 16 + 4g)
+        const int mm = MB0 + m, pp = k >> 1;
+        if (k & 1)
+          oh[m % 3][pp] = lds_rd_tr<true>(ob, 16 * ROW_B + pp * PART_B + 32 * mm);
+        else
+          ol[m % 3][pp] = lds_rd_tr<true>(ob, pp * PART_B + 32 * mm);
+      };
+      // ---- S: partial S^T of both sub-tiles over this half's dimensions, then the
+      // partial of the sub-tile the partner keeps into this wave's slot
+      auto phase_s = [&](int t) {
+        sc[0] = sc[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const uint32_t rb = tile_base(t) + (uint32_t)(c * ROW_B + 16 * g);
         const uint32_t rbt = rb - 8u * g;  // tail reads: 8 bytes per lane group
         bf16x8 ra[3][2][3];
         bf16x4 rt[2][3];
@@ -208,36 +219,21 @@ __device__ __forceinline__ void attn5_half(const uint8_t* __restrict__ E3, int n
             }
           }
         }
-        // ---- exchange the partial scores: this half keeps sub-tile H
         *reinterpret_cast<f32x4*>(my_slot) = sc[1 - H];
-        __syncthreads();
+      };
+      // ---- softmax of sub-tile H (this half's): the partner's partial added, the next
+      // tile's LDS-DMA issued (its buffer was released by the lagging group's O phase of
+      // tile t - 1, the interval before), the weights into the partner's slot, and the O
+      // phase's first two blocks read ahead.  The first tile of a pass exchanges the
+      // column max and min (a barrier inside the interval; the other group meets it)
+      auto phase_soft = [&](int t) {
         f32x4 S = sc[H];
         {
           const f32x4 v = *reinterpret_cast<const f32x4*>(pa_slot);
           S += v;
         }
-        if (!WITH_O) {
-          // statistics only: the next tile's copy in one burst (no O phase to spread it over)
-          issue(tn, (t + 1) & 1);
-        }
-        // O-phase operands: blocks 0 and 1 of this half, issued before the softmax
-        const uint32_t ob = tb + (uint32_t)((4 * g + (c >> 2)) * ROW_B + 8 * (c & 3));
-        bf16x4 ol[3][3], oh[3][3];
-        auto read_o = [&](int m, int k) {  // read k of local block m (piece k / 2, rows 4g / 16 + 4g)
-          const int mm = MB0 + m, pp = k >> 1;
-          if (k & 1)
-            oh[m % 3][pp] = lds_rd_tr<true>(ob, 16 * ROW_B + pp * PART_B + 32 * mm);
-          else
-            ol[m % 3][pp] = lds_rd_tr<true>(ob, pp * PART_B + 32 * mm);
-        };
-        if (WITH_O) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) read_o(0, k);
-#pragma unroll
-          for (int k = 0; k < 6; ++k) read_o(1, k);
-        }
-        // ---- softmax of sub-tile H: entity k0 + 16 H + 4 g + r for query c
-        const int e0 = k0 + 16 * H + 4 * g;
+        if (t + 1 < ntiles) issue(t + 1, (t + 1) & 1);
+        const int e0 = key_begin + t * KT + 16 * H + 4 * g;  // entity e0 + r for query c
         float v[4];
         float tmax = kNegInf, tmin = kPosInf;
 #pragma unroll
@@ -249,8 +245,8 @@ __device__ __forceinline__ void attn5_half(const uint8_t* __restrict__ E3, int n
         }
         m_seen = fmaxf(m_seen, tmax);
         if (t == 0) {
-          // the tile's column max and min over both sub-tiles: the pass's reference max
-          // (pass 0) and its centring shift, the smallest weight e^{min - m_ref}
+          // the pass's reference max (pass 0) and its centring shift, the smallest weight
+          // e^{min - m_ref}, over both sub-tiles of the first tile
           float mq = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
           mq = fmaxf(mq, __shfl_xor(mq, 32, 64));
           float mn = fminf(tmin, __shfl_xor(tmin, 16, 64));
@@ -266,65 +262,95 @@ __device__ __forceinline__ void attn5_half(const uint8_t* __restrict__ E3, int n
           csh = (mn < kPosInf) ? __expf(mn - m_ref) : 0.f;
         }
         float pw[4];
-        {
-          float lt = 0.f;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) pw[r] = (e0 + r < key_end) ? __fsub_rn(__expf(v[r] - m_ref), csh) : 0.f;
-          lt = (pw[0] + pw[1]) + (pw[2] + pw[3]);
-          l_run += lt;
-        }
+        for (int r = 0; r < 4; ++r) pw[r] = (e0 + r < key_end) ? __fsub_rn(__expf(v[r] - m_ref), csh) : 0.f;
+        l_run += (pw[0] + pw[1]) + (pw[2] + pw[3]);
         if (WITH_O) {
-          // ---- exchange the weights: this half's into the partner's slot (read above),
-          // the partner's from this half's slot
           *reinterpret_cast<f32x4*>(pa_slot) = (f32x4){pw[0], pw[1], pw[2], pw[3]};
-          __syncthreads();
-          const f32x4 pv = *reinterpret_cast<const f32x4*>(my_slot);
-          // P pieces in the B layout: element j of lane group g = entity 4 g + j (j < 4,
-          // sub-tile 0) or 16 + 4 g + j - 4 (sub-tile 1)
-          float p8[8];
+          // P pieces of this half's sub-tile in the B layout (element j of lane group g:
+          // entity 4 g + j of sub-tile 0 for j < 4, 4 g + j - 4 of sub-tile 1)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            p8[r] = H == 0 ? pw[r] : pv[r];
-            p8[4 + r] = H == 0 ? pv[r] : pw[r];
-          }
-          bf16x8 pb[3];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
             __bf16 h, m, l;
-            split3(p8[j], h, m, l);
-            pb[0][j] = h;
-            pb[1][j] = m;
-            pb[2][j] = l;
+            split3(pw[r], h, m, l);
+            pb[0][4 * H + r] = h;
+            pb[1][4 * H + r] = m;
+            pb[2][4 * H + r] = l;
           }
-          // ---- O^T += E^T . P over this half's blocks, one DMA piece of the next tile per
-          // block; block m + 2's reads ride in block m's MFMA issue gaps
+          const uint32_t ob = o_base(t);
 #pragma unroll
-          for (int m = 0; m < NB; ++m) {
-            if (m + 1 < NB)
-              lgkm_wait<6>();
-            else
-              lgkm_wait<0>();
-            __builtin_amdgcn_sched_barrier(0);
-            if (m < npw) {
-              bdma(tn, (t + 1) & 1, m);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-            bf16x8 a[3];
+          for (int k = 0; k < 6; ++k) read_o(ob, 0, k);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
-              const bf16x4 x = ol[m % 3][p], y = oh[m % 3][p];
-              a[p] = (bf16x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-            }
+          for (int k = 0; k < 6; ++k) read_o(ob, 1, k);
+        }
+      };
+      // ---- the partner's weights, then O^T += E^T . P over this half's blocks; block
+      // m + 2's reads ride in block m's MFMA issue gaps
+      auto phase_o = [&](int t) {
+        if (!WITH_O) return;
+        {
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(my_slot);
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-              O[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kPA[k]], pb[kPB[k]], O[m], 0, 0, 0);
-              if (m + 2 < NB) read_o(m + 2, k);
-              __builtin_amdgcn_sched_barrier(0);
-            }
+          for (int r = 0; r < 4; ++r) {
+            __bf16 h, m, l;
+            split3(pv[r], h, m, l);
+            pb[0][4 * (1 - H) + r] = h;
+            pb[1][4 * (1 - H) + r] = m;
+            pb[2][4 * (1 - H) + r] = l;
           }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        const uint32_t ob = o_base(t);
+#pragma unroll
+        for (int m = 0; m < NB; ++m) {
+          if (m + 1 < NB)
+            lgkm_wait<6>();
+          else
+            lgkm_wait<0>();
+          __builtin_amdgcn_sched_barrier(0);
+          bf16x8 a[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const bf16x4 x = ol[m % 3][p], y = oh[m % 3][p];
+            a[p] = (bf16x8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+          }
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            O[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kPA[k]], pb[kPB[k]], O[m], 0, 0, 0);
+            if (m + 2 < NB) read_o(ob, m + 2, k);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      };
+      // Intervals between workgroup barriers, 3 per tile: group 0 runs S_t | softmax_t |
+      // O_t, group 1 one interval later (O_{t-1} | S_t | softmax_t), so on every SIMD one
+      // wave's softmax sits beside the other's MFMAs.  Both groups pass the same barriers:
+      // 3 per tile, 2 more on the first tile (the max / min exchange), 1 for the lag.
+      // The next tile's copies, issued in the softmax intervals, land before the barrier
+      // that closes each tile's third interval.
+      if (G == 0) {
+        for (int t = 0; t < ntiles; ++t) {
+          phase_s(t);
+          __syncthreads();
+          phase_soft(t);
+          __syncthreads();
+          if (t == 0) __syncthreads();  // group 1's max / min exchange
+          phase_o(t);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+        }
+        __syncthreads();  // group 1's last O phase
+      } else {
+        __syncthreads();  // group 0's first S phase
+        for (int t = 0; t < ntiles; ++t) {
+          if (t == 0) __syncthreads();  // group 0's max / min exchange
+          phase_s(t);
+          __syncthreads();
+          phase_soft(t);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          phase_o(t);
+          __syncthreads();
+        }
       }
       float mq = fmaxf(m_seen, __shfl_xor(m_seen, 16, 64));
       mq = fmaxf(mq, __shfl_xor(mq, 32, 64));
@@ -395,7 +421,8 @@ __device__ __forceinline__ void attn5_half(const uint8_t* __restrict__ E3, int n
   }
 }
 
-// 8 waves: w < 4 the first half of the dimensions, w >= 4 the second (pairs w, w ^ 4)
+// 8 waves: pairs (w, w ^ 1), even w the first half of the dimensions; waves 4..7 (the
+// second group, sharing the SIMDs of waves 0..3) one interval behind
 template <int MODE>
 __global__ __launch_bounds__(512, 1) void kp_attn5(const uint8_t* __restrict__ E3, int n_ent,
                                                    const float* __restrict__ Qpre, int nq, AttnWork wk,
@@ -406,10 +433,12 @@ __global__ __launch_bounds__(512, 1) void kp_attn5(const uint8_t* __restrict__ E
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds5;
   float* xf = reinterpret_cast<float*>(lds5 + A5_X_OFF);
-  if (w >= 4)
-    attn5_half<1, MODE>(E3, n_ent, Qpre, nq, wk, out_m, out_l, out_O, colpre, w, lane, lds0, xf);
-  else
-    attn5_half<0, MODE>(E3, n_ent, Qpre, nq, wk, out_m, out_l, out_O, colpre, w, lane, lds0, xf);
+  switch ((w & 1) | (w >> 2) << 1) {  // (half, group)
+    case 0: attn5_half<0, 0, MODE>(E3, n_ent, Qpre, nq, wk, out_m, out_l, out_O, colpre, w, lane, lds0, xf); break;
+    case 1: attn5_half<1, 0, MODE>(E3, n_ent, Qpre, nq, wk, out_m, out_l, out_O, colpre, w, lane, lds0, xf); break;
+    case 2: attn5_half<0, 1, MODE>(E3, n_ent, Qpre, nq, wk, out_m, out_l, out_O, colpre, w, lane, lds0, xf); break;
+    default: attn5_half<1, 1, MODE>(E3, n_ent, Qpre, nq, wk, out_m, out_l, out_O, colpre, w, lane, lds0, xf); break;
+  }
 }
 
 // Host: co-resident kp_attn5 workgroups per CU (one: the LDS), cached per context.

@@ -315,10 +315,11 @@ def test_complex_db100k_sufficient_batch_equals_sequential(db100k):
 
 @pytest.mark.parametrize("model_name", ["ComplEx", "ConvE"])
 def test_attention_contractions_agree(model_name, monkeypatch):
-    """kp_attn3 (bf16 MFMA, exact three-piece operand splits, the default) against
-    kp_attn (fp32 MFMA, KP_ATTN=f32) on the same post-trainings at the production
-    widths (ComplEx D = 400, ConvE d = 200): target scores within 1e-5 relative, ranks
-    equal.  Both differ from the fp32 FMA chain only in accumulation order."""
+    """kp_attn3 (bf16 MFMA, exact three-piece operand splits) and, for ComplEx, the
+    wave-pair kp_attn5 against kp_attn (fp32 MFMA, KP_ATTN=f32) on the same
+    post-trainings at the production widths (ComplEx D = 400, ConvE d = 200): target
+    scores within 1e-5 relative, ranks equal.  They differ from the fp32 FMA chain only
+    in accumulation order."""
     from kelpie_amd import synth
     g = synth.make_graph("small", seed=5)
     ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
@@ -339,8 +340,10 @@ def test_attention_contractions_agree(model_name, monkeypatch):
                                 bn=bn, hidden_dropout_rate=0.2)
         hp = CV_HP
     out = {}
-    for mode in ("f32", "bf16x3"):
-        monkeypatch.setenv("KP_ATTN", mode)
+    # ComplEx also runs the wave-pair kernel (kp_attn5, KP_ATTN_PAIR=1) on bf16x3
+    for mode in ("f32", "bf16x3", "pair") if model_name == "ComplEx" else ("f32", "bf16x3"):
+        monkeypatch.setenv("KP_ATTN", "f32" if mode == "f32" else "bf16x3")
+        monkeypatch.setenv("KP_ATTN_PAIR", "1" if mode == "pair" else "0")
         model = make()
         seed_all(42)
         eng = ka.NecessaryPostTrainingEngine(model, ds, hp)
@@ -353,10 +356,13 @@ def test_attention_contractions_agree(model_name, monkeypatch):
                     for pt, b in eng.last_results]
         model.close() if hasattr(model, "close") else None
         out[mode] = res
-    for a, b in zip(out["bf16x3"], out["f32"]):
-        assert abs(a[1] - b[1]) <= 1e-5 * max(1e-3, abs(b[1])), (a, b)
-        assert abs(a[3] - b[3]) <= 1e-5 * max(1e-3, abs(b[3])), (a, b)
-        assert a[0] == b[0] and a[2] == b[2], (a, b)
+    for mode in out:
+        if mode == "f32":
+            continue
+        for a, b in zip(out[mode], out["f32"]):
+            assert abs(a[1] - b[1]) <= 1e-5 * max(1e-3, abs(b[1])), (mode, a, b)
+            assert abs(a[3] - b[3]) <= 1e-5 * max(1e-3, abs(b[3])), (mode, a, b)
+            assert a[0] == b[0] and a[2] == b[2], (mode, a, b)
 
 
 def test_conve_fused_encoder_agrees(monkeypatch):
