@@ -31,7 +31,7 @@ def _sigmoid(x):
     return 1 / (1 + math.exp(-x))
 
 
-@dataclass
+@dataclass(slots=True)
 class _Slot:
     x0: np.ndarray
     rows: np.ndarray
@@ -303,6 +303,49 @@ class PostTrainingEngine(RelevanceEngine):
             # the sequential numpy chain starts right away)
             self._flush_fused()
         return len(slots) - 1, pred
+
+    def _schedule_fused_pred(self, pred, rules, mode, slots, pending_base):
+        """:meth:`_schedule_fused` for every rule of one prediction (no checkpoints, no
+        empty rule): the same slots, claims and queued calls in the same order, with the
+        prediction's view, kelpie triple and row count looked up once.  Returns the
+        prediction's [(pt slot index, base key)]."""
+        pred = tuple(int(v) for v in pred)
+        view = self._get_kelpie_dataset(pred[0])
+        kp = view.as_kelpie_triple(pred)
+        sharded = self._sharded()
+        sh = self.sharding
+        nb = view.n_base_rows
+        sufficient = mode == "sufficient"
+        fused, flush_at = self._fused, self._FUSED_FLUSH if self._sched is not None else self._FUSED_FIRST
+        out = []
+        for rule in rules:
+            triples = [(int(a), int(b), int(c)) for a, b, c in rule]
+            need_base = pred not in self.base_pt_results and pred not in pending_base
+            base_owner = pt_owner = 0
+            if sharded and need_base:
+                base_owner = sh.claim_owner(max(1, nb))
+            own_base = need_base and (not sharded or base_owner == sh.rank)
+            if sharded:
+                est = nb + 2 * len(triples) if sufficient else nb - 2 * len(triples)
+                pt_owner = sh.claim_owner(max(1, est))
+                own_pt = pt_owner == sh.rank
+            else:
+                own_pt = True
+            base = None
+            if need_base:
+                pending_base[pred] = len(slots)
+                base = _Slot(None, None, None, kp, None, None, own_base, base_owner)
+                slots.append(base)
+            pt = _Slot(None, None, None, kp, None, None, own_pt, pt_owner)
+            slots.append(pt)
+            fused.append({"view": view, "kp": kp, "triples": triples,
+                          "flags": (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
+                          | (8 if sufficient else 0), "base": base, "pt": pt})
+            out.append((len(slots) - 1, pred))
+            if len(fused) >= flush_at:
+                self._flush_fused()
+                fused, flush_at = self._fused, self._FUSED_FLUSH
+        return out
 
     _FUSED_FLUSH = 24  # queued TransE calls per library call
     _FUSED_FIRST = 4  # ... for a batch's first one
@@ -631,7 +674,11 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
 
     def _schedule_multi(self, items, checkpoints):
         slots, pending, jobs = [], {}, []
+        fast = checkpoints is None and getattr(self.model, "fused_call_draws", False)
         for pred, rules in items:
+            if fast and all(len(r) for r in rules):
+                jobs.append(self._schedule_fused_pred(pred, rules, "necessary", slots, pending))
+                continue
             pj = []
             for rule in rules:
                 rule = [tuple(t) for t in rule]

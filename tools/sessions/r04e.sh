@@ -8,7 +8,7 @@ set -o pipefail
 O=gpurun_out/r04e; mkdir -p $O
 for rep in 1 2; do
   for k in 0 1; do
-    for args in "25 0 14541 3100 30" "25 0 99604 1800 10" "25 1 14541 3100 30"; do
+    for args in "25 0 14541 3100 30" "25 0 99604 1800 10"; do
       KP_MICRO_ATTN5=$k timeout -k 10 120 variants/attn_micro_cur $args 0.05 >> $O/micro.jsonl || { echo "micro failed k=$k $args"; exit 1; }
     done
   done
