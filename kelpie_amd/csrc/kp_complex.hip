@@ -107,10 +107,10 @@ struct CxOpt {
 // (measured ~-4e-6 against the fp64 reference, tools/headline_probe.py).
 //
 // The scalar part of that work (the row's logit z, the split statistics' merge, the
-// log-sum-exp with the kelpie column and the per-split weights) is split out of the
-// per-row merge so that the fp64 transcendentals run once per row on one LANE
-// (kp_cx_prep) instead of once per row on a whole wave: as wave-uniform code in the
-// merge kernel (round 3) they made it VALU-bound, 56 -> 106 us per launch.
+// log-sum-exp with the kelpie column and the per-split weights) runs on 16 lanes per row
+// (4 rows per wave) at the start of kp_cx_contrib, the logit in kp_cx_stepq, instead of
+// once per row on a whole wave: as wave-uniform code in every row's wave (round 3) the
+// fp64 transcendentals made the merge VALU-bound, 56 -> 106 us per launch.
 
 // z of every step row (fp32, the lane order and wave reduction the merge used):
 // queries q . x with q = x o r (the row of kp_cx_stepq), frozen-head rows q_pair . x
@@ -147,16 +147,25 @@ __device__ __forceinline__ double cx_butterfly(const float* __restrict__ att_m, 
   return v[0];
 }
 
-// one thread per step row (queries first, then the frozen-head rows):
-//   query:  pk = p(kelpie column) and the split weights wv[sp][item] = e^{m_sp - lse}
-//   frozen: coef = c (p_k - 1)
+// One wave per (query or frozen-head row) of this step: its contribution to the
+// kelpie row's gradient (un-normalised by the batch size).
+//   query (kelpie-head rows sharing relation r, count c, kelpie targets ck):
+//     J_r^T (c <E> - Tsum - ck x) + (c p_k - ck) q,   <E> = softmax-weighted entity
+//     (frozen part sum_sp w_sp O_sp merged with the kelpie column p_k x)
+//   frozen-head row pair (count c, target = kelpie):  c (p_k - 1) q_pair
+// pk / coef and the split weights: computed at the start (below).
+//
+// The scalars of the workgroup's four rows first, in wave 0 with 16 lanes per row (lane
+// 16 r + sp: split sp of row r): the split statistics' exp and fp64 butterfly sum (the
+// 16-lane xor butterfly is the 64-lane one of one split per lane: lanes at or above the
+// next power of two above n_split only ever add zeros), then one lane per row the
+// log-sum-exp with the kelpie column, then each split's weight -- into LDS for the
+// merge.  n_split > 16: one lane per row (cx_row_scalars).
 template <int NS>
-__global__ __launch_bounds__(256) void kp_cx_prep(int nq, int nt, const int4* __restrict__ stept,
-                                                  const float* __restrict__ zrow, const float* __restrict__ lsef,
-                                                  const float* __restrict__ att_m, const float* __restrict__ att_l,
-                                                  int n_split, double* __restrict__ wv, double* __restrict__ coef) {
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
-  if (item >= nq + nt) return;
+__device__ __forceinline__ void cx_row_scalars(int item, int nq, const int4* __restrict__ stept,
+                                               const float* __restrict__ zrow, const float* __restrict__ lsef,
+                                               const float* __restrict__ att_m, const float* __restrict__ att_l,
+                                               int n_split, double* w_out, double* c_out) {
   const double z = (double)zrow[item];
   if (item < nq) {
     float mm = kNegInf;
@@ -165,37 +174,64 @@ __global__ __launch_bounds__(256) void kp_cx_prep(int nq, int nt, const int4* __
     const double lse_f = (double)mm + log(e);
     const double hi = fmax(lse_f, z), lo = fmin(lse_f, z);
     const double lse = hi + log1p(exp(lo - hi));
-    coef[item] = exp(z - lse);
+    *c_out = exp(z - lse);
     for (int sp = 0; sp < n_split; ++sp) {
       const float ms = att_m[(size_t)sp * nq + item];
-      wv[(size_t)sp * nq + item] = (ms == kNegInf) ? 0.0 : exp((double)ms - lse);
+      w_out[sp] = (ms == kNegInf) ? 0.0 : exp((double)ms - lse);
     }
   } else {
     const int4 st = stept[item - nq];  // slot, pair, count
     const double lf = lsef[st.y];
     const double hi = fmax(lf, z), lo = fmin(lf, z);
     const double lse = hi + log1p(exp(lo - hi));
-    coef[item] = (double)st.z * (exp(z - lse) - 1.0);
+    *c_out = (double)st.z * (exp(z - lse) - 1.0);
   }
 }
 
-// One wave per (query or frozen-head row) of this step: its contribution to the
-// kelpie row's gradient (un-normalised by the batch size).
-//   query (kelpie-head rows sharing relation r, count c, kelpie targets ck):
-//     J_r^T (c <E> - Tsum - ck x) + (c p_k - ck) q,   <E> = softmax-weighted entity
-//     (frozen part sum_sp w_sp O_sp merged with the kelpie column p_k x)
-//   frozen-head row pair (count c, target = kelpie):  c (p_k - 1) q_pair
-// pk / coef and the split weights come from kp_cx_prep.
 template <int DP>
 __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __restrict__ stepq, int nq,
                                                      const int4* __restrict__ stept, int nt,
                                                      const CxQuery* __restrict__ pq, const float* __restrict__ X,
                                                      const float* __restrict__ R, const float* __restrict__ Tsum,
-                                                     const float* __restrict__ Qpair, const double* __restrict__ wv,
-                                                     const double* __restrict__ coef, const float* __restrict__ att_O,
+                                                     const float* __restrict__ Qpair, const float* __restrict__ zrow,
+                                                     const float* __restrict__ lsef, const float* __restrict__ att_m,
+                                                     const float* __restrict__ att_l, const float* __restrict__ att_O,
                                                      int n_split, float* __restrict__ contrib) {
+  __shared__ double s_w[4][64];  // per row: the split weights
+  __shared__ double s_c[4];      // per row: pk (query) or coef (frozen-head row)
   const int lane = threadIdx.x & 63;
-  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
+  const int wv_ = threadIdx.x >> 6;
+  const int item0 = blockIdx.x * 4;
+  if (wv_ == 0) {
+    const int r = lane >> 4, sp = lane & 15, item = item0 + r;
+    if (n_split <= 16) {
+      const bool row = item < nq + nt;
+      const bool q = row && item < nq;
+      const float ms = (q && sp < n_split) ? att_m[(size_t)sp * nq + item] : kNegInf;
+      const float ls = (q && sp < n_split) ? att_l[(size_t)sp * nq + item] : 0.f;
+      float mm = ms;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) mm = fmaxf(mm, __shfl_xor(mm, o, 64));
+      double e = (ms == kNegInf) ? 0.0 : (double)ls * exp((double)ms - (double)mm);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+      double lse = 0.0;
+      if (row && sp == 0) {
+        const double z = (double)zrow[item];
+        const double lf = q ? (double)mm + log(e) : (double)lsef[stept[item - nq].y];
+        const double hi = fmax(lf, z), lo = fmin(lf, z);
+        lse = hi + log1p(exp(lo - hi));
+        s_c[r] = q ? exp(z - lse) : (double)stept[item - nq].z * (exp(z - lse) - 1.0);
+      }
+      lse = __shfl(lse, lane & ~15, 64);
+      if (q && sp < n_split) s_w[r][sp] = (ms == kNegInf) ? 0.0 : exp((double)ms - lse);
+    } else if (lane < 4 && item0 + lane < nq + nt) {
+      if (n_split <= 64)
+        cx_row_scalars<64>(item0 + lane, nq, stept, zrow, lsef, att_m, att_l, n_split, s_w[lane], &s_c[lane]);
+    }
+  }
+  __syncthreads();
+  const int item = __builtin_amdgcn_readfirstlane(item0 + wv_);  // wave-uniform
   if (item >= nq + nt) return;
   float* out = contrib + (size_t)item * DP;
   if (item < nq) {
@@ -203,7 +239,7 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
     const float* x = X + (size_t)sq.x * DP;
     const float* rel = R + (size_t)sq.y * DP;
     const CxQuery Q = pq[sq.z];
-    const double pk = coef[item];
+    const double pk = s_c[wv_];
     // merge the partials split by split (increasing split order, the sum's order), four
     // splits' loads in flight together
     constexpr int NI = (DP / 2 + 63) / 64;
@@ -217,7 +253,7 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
 #pragma unroll
       for (int j = 0; j < SU; ++j) {
         const bool v = sp + j < n_split;
-        w[j] = v ? wv[(size_t)(sp + j) * nq + item] : 0.0;
+        w[j] = v ? s_w[wv_][sp + j] : 0.0;
         const float* Oj = att_O + ((size_t)(v ? sp + j : sp) * nq + item) * DP;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
@@ -256,7 +292,7 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
   } else {
     const int4 st = stept[item - nq];  // slot, pair, count
     const float* qp = Qpair + (size_t)st.y * DP;
-    const double cf = coef[item];
+    const double cf = s_c[wv_];
     for (int d = lane; d < 2 * half; d += 64) out[d] = (float)(cf * (double)qp[d]);
   }
 }
@@ -481,20 +517,13 @@ template <int DB>
 void launch_update(kp_ctx* c, int n_act, const int4* act, const CxPlan* plans, const CxQuery* pq,
                    const int4* stepq, int nq, const int4* stept, int nt, const float* tsum, const float* qpair,
                    const float* lsef, const float* zrow, const float* am, const float* al, const float* aO,
-                   int n_split, double* wv, double* coef, float* contrib, float* X, float* S1, float* S2,
-                   const CxOpt& opt) {
+                   int n_split, float* contrib, float* X, float* S1, float* S2, const CxOpt& opt) {
   if (n_act <= 0) return;
   const int half = c->dim / 2;
   KP_REQUIRE(n_split >= 1 && n_split <= 64, "cx contrib: at most 64 attention splits");
   if (nq + nt > 0) {
-    const dim3 pg((nq + nt + 255) / 256), pb(256);
-    if (n_split <= 16)
-      hipLaunchKernelGGL((kp_cx_prep<16>), pg, pb, 0, c->stream, nq, nt, stept, zrow, lsef, am, al, n_split, wv, coef);
-    else
-      hipLaunchKernelGGL((kp_cx_prep<64>), pg, pb, 0, c->stream, nq, nt, stept, zrow, lsef, am, al, n_split, wv, coef);
-    KP_HIP(hipGetLastError());
     hipLaunchKernelGGL((kp_cx_contrib<16 * DB>), dim3((nq + nt + 3) / 4), dim3(256), 0, c->stream, half, stepq, nq,
-                       stept, nt, pq, X, c->dR, tsum, qpair, wv, coef, aO, n_split, contrib);
+                       stept, nt, pq, X, c->dR, tsum, qpair, zrow, lsef, am, al, aO, n_split, contrib);
     KP_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL((kp_cx_update<16 * DB>), dim3(n_act), dim3(256), 0, c->stream, half, act, plans, nq, contrib, X,
@@ -747,10 +776,8 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float* dAl = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * att_rows));
   float* dAO = reinterpret_cast<float*>(c->ws[15].ensure(sizeof(float) * att_rows * DP));
   float* dQs = reinterpret_cast<float*>(c->ws[26].ensure(sizeof(float) * (size_t)std::max(max_nq, 1) * DP));
-  // per step row: its logit (kp_cx_stepq), the split weights and pk / coef (kp_cx_prep)
+  // per step row: its logit (kp_cx_stepq)
   float* dZrow = reinterpret_cast<float*>(c->ws[5].ensure(sizeof(float) * (size_t)std::max(1, max_items)));
-  double* dWv = reinterpret_cast<double*>(c->ws[27].ensure(sizeof(double) * att_rows));
-  double* dCoef = reinterpret_cast<double*>(c->ws[31].ensure(sizeof(double) * (size_t)std::max(1, max_items)));
   if (npairs > 0) {
     hipLaunchKernelGGL(kp_cx_qpair, dim3(npairs), dim3(128), 0, c->stream, c->dE, c->dR, DP, half, dPairs, npairs,
                        dQpair);
@@ -811,8 +838,8 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     opt.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, step)));
     opt.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)hp->beta2, step));
     CX_DISPATCH(DBV, launch_update<DB>(c, na, dActs + act_off[t], dPlans, dPq, dStepQ + q_off[t], nq,
-                                       dStepT + t_off[t], nt, dTsum, dQpair, dLsef, dZrow, dAm, dAl, dAO, sp, dWv,
-                                       dCoef, dContrib, dX, dS1, dS2, opt));
+                                       dStepT + t_off[t], nt, dTsum, dQpair, dLsef, dZrow, dAm, dAl, dAO, sp,
+                                       dContrib, dX, dS1, dS2, opt));
   }
   KP_HIP(hipEventRecord(h1, c->stream));
 
