@@ -99,53 +99,7 @@ struct CxOpt {
   float reg_w;
 };
 
-// The softmax normalisation of every step row in fp64 with correctly rounded exp / log.
-// <E> (kp_cx_contrib) is ~5e-4 per coordinate at the reference init and the row
-// contributions cancel to a gradient up to ~100x smaller on the coordinates Adagrad has
-// not saturated, so a one-sided ulp error of a fast exp / log here (every row, every
-// step, the same sign) became a one-sided drift of those coordinates of the kelpie row
-// (measured ~-4e-6 against the fp64 reference, tools/headline_probe.py).
-//
-// The scalar part of that work (the row's logit z, the split statistics' merge, the
-// log-sum-exp with the kelpie column and the per-split weights) runs on 16 lanes per row
-// (4 rows per wave) at the start of kp_cx_contrib, the logit in kp_cx_stepq, instead of
-// once per row on a whole wave: as wave-uniform code in every row's wave (round 3) the
-// fp64 transcendentals made the merge VALU-bound, 56 -> 106 us per launch.
-
-// z of every step row (fp32, the lane order and wave reduction the merge used):
-// queries q . x with q = x o r (the row of kp_cx_stepq), frozen-head rows q_pair . x
-template <int DP>
-__device__ __forceinline__ float cx_row_z(int lane, int half, const float* __restrict__ a,
-                                          const float* __restrict__ rel, const float* __restrict__ x) {
-  float z = 0.f;
-  if (rel)
-    for (int d = lane; d < 2 * half; d += 64) z += cx_q(a, rel, d, half) * x[d];
-  else
-    for (int d = lane; d < 2 * half; d += 64) z += a[d] * x[d];
-  return wave_sum(z);
-}
-
-// Per row, one lane: the 64-lane xor butterfly of the merge (split sp on lane sp, zeros
-// above n_split) restated on NS <= 64 registers: lanes >= the next power of two above
-// n_split only ever add zeros to lanes below it, so the first NS entries reproduce the
-// wave's sum bit for bit
-template <int NS>
-__device__ __forceinline__ double cx_butterfly(const float* __restrict__ att_m, const float* __restrict__ att_l,
-                                               size_t stride, int item, int n_split, float mm) {
-  double v[NS];
-#pragma unroll
-  for (int l = 0; l < NS; ++l) {
-    const float ms = l < n_split ? att_m[(size_t)l * stride + item] : kNegInf;
-    const float ls = l < n_split ? att_l[(size_t)l * stride + item] : 0.f;
-    v[l] = (ms == kNegInf) ? 0.0 : (double)ls * exp((double)ms - (double)mm);
-  }
-#pragma unroll
-  for (int o = NS / 2; o > 0; o >>= 1)
-#pragma unroll
-    for (int l = 0; l < NS; ++l)
-      if (!(l & o)) v[l] = v[l ^ o] = v[l] + v[l ^ o];  // both lanes of a pair get the same sum
-  return v[0];
-}
+#define UPD_MAXSPLIT 16
 
 // One wave per (query or frozen-head row) of this step: its contribution to the
 // kelpie row's gradient (un-normalised by the batch size).
@@ -153,85 +107,17 @@ __device__ __forceinline__ double cx_butterfly(const float* __restrict__ att_m, 
 //     J_r^T (c <E> - Tsum - ck x) + (c p_k - ck) q,   <E> = softmax-weighted entity
 //     (frozen part sum_sp w_sp O_sp merged with the kelpie column p_k x)
 //   frozen-head row pair (count c, target = kelpie):  c (p_k - 1) q_pair
-// pk / coef and the split weights: computed at the start (below).
-//
-// The scalars of the workgroup's four rows first, in wave 0 with 16 lanes per row (lane
-// 16 r + sp: split sp of row r): the split statistics' exp and fp64 butterfly sum (the
-// 16-lane xor butterfly is the 64-lane one of one split per lane: lanes at or above the
-// next power of two above n_split only ever add zeros), then one lane per row the
-// log-sum-exp with the kelpie column, then each split's weight -- into LDS for the
-// merge.  n_split > 16: one lane per row (cx_row_scalars).
-template <int NS>
-__device__ __forceinline__ void cx_row_scalars(int item, int nq, const int4* __restrict__ stept,
-                                               const float* __restrict__ zrow, const float* __restrict__ lsef,
-                                               const float* __restrict__ att_m, const float* __restrict__ att_l,
-                                               int n_split, double* w_out, double* c_out) {
-  const double z = (double)zrow[item];
-  if (item < nq) {
-    float mm = kNegInf;
-    for (int sp = 0; sp < n_split; ++sp) mm = fmaxf(mm, att_m[(size_t)sp * nq + item]);
-    const double e = cx_butterfly<NS>(att_m, att_l, (size_t)nq, item, n_split, mm);
-    const double lse_f = (double)mm + log(e);
-    const double hi = fmax(lse_f, z), lo = fmin(lse_f, z);
-    const double lse = hi + log1p(exp(lo - hi));
-    *c_out = exp(z - lse);
-    for (int sp = 0; sp < n_split; ++sp) {
-      const float ms = att_m[(size_t)sp * nq + item];
-      w_out[sp] = (ms == kNegInf) ? 0.0 : exp((double)ms - lse);
-    }
-  } else {
-    const int4 st = stept[item - nq];  // slot, pair, count
-    const double lf = lsef[st.y];
-    const double hi = fmax(lf, z), lo = fmin(lf, z);
-    const double lse = hi + log1p(exp(lo - hi));
-    *c_out = (double)st.z * (exp(z - lse) - 1.0);
-  }
-}
-
 template <int DP>
 __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __restrict__ stepq, int nq,
                                                      const int4* __restrict__ stept, int nt,
                                                      const CxQuery* __restrict__ pq, const float* __restrict__ X,
                                                      const float* __restrict__ R, const float* __restrict__ Tsum,
-                                                     const float* __restrict__ Qpair, const float* __restrict__ zrow,
-                                                     const float* __restrict__ lsef, const float* __restrict__ att_m,
-                                                     const float* __restrict__ att_l, const float* __restrict__ att_O,
-                                                     int n_split, float* __restrict__ contrib) {
-  __shared__ double s_w[4][64];  // per row: the split weights
-  __shared__ double s_c[4];      // per row: pk (query) or coef (frozen-head row)
+                                                     const float* __restrict__ Qpair, const float* __restrict__ lsef,
+                                                     const float* __restrict__ att_m, const float* __restrict__ att_l,
+                                                     const float* __restrict__ att_O, int n_split,
+                                                     float* __restrict__ contrib) {
   const int lane = threadIdx.x & 63;
-  const int wv_ = threadIdx.x >> 6;
-  const int item0 = blockIdx.x * 4;
-  if (wv_ == 0) {
-    const int r = lane >> 4, sp = lane & 15, item = item0 + r;
-    if (n_split <= 16) {
-      const bool row = item < nq + nt;
-      const bool q = row && item < nq;
-      const float ms = (q && sp < n_split) ? att_m[(size_t)sp * nq + item] : kNegInf;
-      const float ls = (q && sp < n_split) ? att_l[(size_t)sp * nq + item] : 0.f;
-      float mm = ms;
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) mm = fmaxf(mm, __shfl_xor(mm, o, 64));
-      double e = (ms == kNegInf) ? 0.0 : (double)ls * exp((double)ms - (double)mm);
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
-      double lse = 0.0;
-      if (row && sp == 0) {
-        const double z = (double)zrow[item];
-        const double lf = q ? (double)mm + log(e) : (double)lsef[stept[item - nq].y];
-        const double hi = fmax(lf, z), lo = fmin(lf, z);
-        lse = hi + log1p(exp(lo - hi));
-        s_c[r] = q ? exp(z - lse) : (double)stept[item - nq].z * (exp(z - lse) - 1.0);
-      }
-      lse = __shfl(lse, lane & ~15, 64);
-      if (q && sp < n_split) s_w[r][sp] = (ms == kNegInf) ? 0.0 : exp((double)ms - lse);
-    } else if (lane < 4 && item0 + lane < nq + nt) {
-      if (n_split <= 64)
-        cx_row_scalars<64>(item0 + lane, nq, stept, zrow, lsef, att_m, att_l, n_split, s_w[lane], &s_c[lane]);
-    }
-  }
-  __syncthreads();
-  const int item = __builtin_amdgcn_readfirstlane(item0 + wv_);  // wave-uniform
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= nq + nt) return;
   float* out = contrib + (size_t)item * DP;
   if (item < nq) {
@@ -239,38 +125,49 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
     const float* x = X + (size_t)sq.x * DP;
     const float* rel = R + (size_t)sq.y * DP;
     const CxQuery Q = pq[sq.z];
-    const double pk = s_c[wv_];
-    // merge the partials split by split (increasing split order, the sum's order), four
-    // splits' loads in flight together
+    float z = 0.f;
+    for (int d = lane; d < 2 * half; d += 64) z += cx_q(x, rel, d, half) * x[d];
+    z = wave_sum(z);
+    // The softmax normalisation in fp64 with correctly rounded exp / log.  <E> below is
+    // ~5e-4 per coordinate at the reference init and the row contributions cancel to a
+    // gradient up to ~100x smaller on the coordinates Adagrad has not saturated, so a
+    // one-sided ulp error of a fast exp / log here (every row, every step, the same
+    // sign) became a one-sided drift of those coordinates of the kelpie row (measured
+    // ~-4e-6 against the fp64 reference, tools/headline_probe.py).
+    // The split statistics one split per lane (n_split <= 64): the max, the fp64 sum of
+    // the rescaled l's (a butterfly, deterministic) and each split's weight, so a wave
+    // makes two fp64 exp per lane instead of 2 n_split in sequence on every lane.
+    const bool has = lane < n_split;
+    const float ms_l = has ? att_m[(size_t)lane * nq + item] : kNegInf;
+    const float ls_l = has ? att_l[(size_t)lane * nq + item] : 0.f;
+    const float mm = wave_max(ms_l);
+    double e_l = (ms_l == kNegInf) ? 0.0 : (double)ls_l * exp((double)ms_l - (double)mm);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) e_l += __shfl_xor(e_l, o, 64);
+    const double lse_f = (double)mm + log(e_l);
+    const double hi = fmax(lse_f, (double)z), lo = fmin(lse_f, (double)z);
+    const double lse = hi + log1p(exp(lo - hi));
+    const double pk = exp((double)z - lse);
+    const double wv_l = (ms_l == kNegInf) ? 0.0 : exp((double)ms_l - lse);
+    // merge the partials split by split (increasing split order), one split at a time:
+    // 64 registers, so that a wave fits beside a resident kp_attn3 wave on its SIMD (that
+    // one leaves 104 of the 512 registers per lane free; with two splits' loads in flight
+    // this kernel took 94 and still fitted, the round-4 forms with 150 did not and ran
+    // only on the CUs no attention workgroup held: 92 -> 192 us per launch under overlap)
     constexpr int NI = (DP / 2 + 63) / 64;
-    constexpr int SU = 4;
     double ore_k[NI], oim_k[NI];
 #pragma unroll
     for (int k = 0; k < NI; ++k) ore_k[k] = oim_k[k] = 0.0;
-    for (int sp = 0; sp < n_split; sp += SU) {
-      float a[SU][NI], b[SU][NI];
-      double w[SU];
+    for (int sp = 0; sp < n_split; ++sp) {
+      const double w0 = __shfl(wv_l, sp, 64);
+      const float* O0 = att_O + ((size_t)sp * nq + item) * DP;
 #pragma unroll
-      for (int j = 0; j < SU; ++j) {
-        const bool v = sp + j < n_split;
-        w[j] = v ? s_w[wv_][sp + j] : 0.0;
-        const float* Oj = att_O + ((size_t)(v ? sp + j : sp) * nq + item) * DP;
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-          const int i = lane + 64 * k;
-          const bool in = v && i < half;
-          a[j][k] = in ? Oj[i] : 0.f;
-          b[j][k] = in ? Oj[i + half] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < SU; ++j) {
-        if (sp + j >= n_split) break;
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-          ore_k[k] += w[j] * (double)a[j][k];
-          oim_k[k] += w[j] * (double)b[j][k];
-        }
+      for (int k = 0; k < NI; ++k) {
+        const int i = lane + 64 * k;
+        const bool in = i < half;
+        const float a0 = in ? O0[i] : 0.f, b0 = in ? O0[i + half] : 0.f;
+        ore_k[k] += w0 * (double)a0;
+        oim_k[k] += w0 * (double)b0;
       }
     }
     const double fc = (double)Q.c, fck = (double)Q.ck;
@@ -291,9 +188,16 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
     }
   } else {
     const int4 st = stept[item - nq];  // slot, pair, count
+    const float* x = X + (size_t)st.x * DP;
     const float* qp = Qpair + (size_t)st.y * DP;
-    const double cf = s_c[wv_];
-    for (int d = lane; d < 2 * half; d += 64) out[d] = (float)(cf * (double)qp[d]);
+    float z = 0.f;
+    for (int d = lane; d < 2 * half; d += 64) z += qp[d] * x[d];
+    z = wave_sum(z);
+    const double lf = lsef[st.y];
+    const double hi = fmax(lf, (double)z), lo = fmin(lf, (double)z);
+    const double lse = hi + log1p(exp(lo - hi));
+    const double coef = (double)st.z * (exp((double)z - lse) - 1.0);
+    for (int d = lane; d < 2 * half; d += 64) out[d] = (float)(coef * (double)qp[d]);
   }
 }
 
@@ -441,37 +345,22 @@ __global__ void kp_cx_scoreq(const float* __restrict__ E, const float* __restric
 // ----------------------------------------------------------------------------
 // host side
 // ----------------------------------------------------------------------------
-// step queries q_j = x_slot o R_rel (complex.py:65-72), one row per step query, and the
-// logit z of every step row (queries, then the frozen-head rows): one wave per row
+// step queries q_j = x_slot o R_rel (complex.py:65-72), one row per step query
 template <int DP>
-__global__ __launch_bounds__(64) void kp_cx_stepq(const float* __restrict__ X, const float* __restrict__ R,
-                                                  int half, const int4* __restrict__ stepq, int nq,
-                                                  const int4* __restrict__ stept, int nt,
-                                                  const float* __restrict__ Qpair, float* __restrict__ Q,
-                                                  float* __restrict__ zrow) {
+__global__ void kp_cx_stepq(const float* __restrict__ X, const float* __restrict__ R, int half,
+                            const int4* __restrict__ stepq, int nq, float* __restrict__ Q) {
   const int j = blockIdx.x;
-  if (j >= nq + nt) return;
-  const int lane = threadIdx.x;
-  float z;
-  if (j < nq) {
-    const int4 sq = stepq[j];
-    const float* x = X + (size_t)sq.x * DP;
-    const float* rel = R + (size_t)sq.y * DP;
-    for (int d = lane; d < DP; d += 64) Q[(size_t)j * DP + d] = cx_q(x, rel, d, half);
-    z = cx_row_z<DP>(lane, half, x, rel, x);
-  } else {
-    const int4 st = stept[j - nq];
-    z = cx_row_z<DP>(lane, half, Qpair + (size_t)st.y * DP, nullptr, X + (size_t)st.x * DP);
-  }
-  if (lane == 0) zrow[j] = z;
+  if (j >= nq) return;
+  const int4 sq = stepq[j];
+  const float* x = X + (size_t)sq.x * DP;
+  const float* rel = R + (size_t)sq.y * DP;
+  for (int d = threadIdx.x; d < DP; d += blockDim.x) Q[(size_t)j * DP + d] = cx_q(x, rel, d, half);
 }
 
 template <int DB>
-void launch_stepq(kp_ctx* c, const int4* stepq, int nq, const int4* stept, int nt, const float* X,
-                  const float* qpair, float* Q, float* zrow) {
-  if (nq + nt <= 0) return;
-  hipLaunchKernelGGL((kp_cx_stepq<16 * DB>), dim3(nq + nt), dim3(64), 0, c->stream, X, c->dR, c->dim / 2, stepq, nq,
-                     stept, nt, qpair, Q, zrow);
+void launch_stepq(kp_ctx* c, const int4* stepq, const float* X, int nq, float* Q) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL((kp_cx_stepq<16 * DB>), dim3(nq), dim3(64), 0, c->stream, X, c->dR, c->dim / 2, stepq, nq, Q);
   KP_HIP(hipGetLastError());
 }
 
@@ -516,14 +405,14 @@ void launch_attn(kp_ctx* c, bool with_o, const float* Q, int nq, const AttnPlan&
 template <int DB>
 void launch_update(kp_ctx* c, int n_act, const int4* act, const CxPlan* plans, const CxQuery* pq,
                    const int4* stepq, int nq, const int4* stept, int nt, const float* tsum, const float* qpair,
-                   const float* lsef, const float* zrow, const float* am, const float* al, const float* aO,
-                   int n_split, float* contrib, float* X, float* S1, float* S2, const CxOpt& opt) {
+                   const float* lsef, const float* am, const float* al, const float* aO, int n_split, float* contrib,
+                   float* X, float* S1, float* S2, const CxOpt& opt) {
   if (n_act <= 0) return;
   const int half = c->dim / 2;
-  KP_REQUIRE(n_split >= 1 && n_split <= 64, "cx contrib: at most 64 attention splits");
+  KP_REQUIRE(n_split >= 1 && n_split <= 64, "cx contrib: one attention split per lane");
   if (nq + nt > 0) {
     hipLaunchKernelGGL((kp_cx_contrib<16 * DB>), dim3((nq + nt + 3) / 4), dim3(256), 0, c->stream, half, stepq, nq,
-                       stept, nt, pq, X, c->dR, tsum, qpair, zrow, lsef, am, al, aO, n_split, contrib);
+                       stept, nt, pq, X, c->dR, tsum, qpair, lsef, am, al, aO, n_split, contrib);
     KP_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL((kp_cx_update<16 * DB>), dim3(n_act), dim3(256), 0, c->stream, half, act, plans, nq, contrib, X,
@@ -776,8 +665,6 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float* dAl = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * att_rows));
   float* dAO = reinterpret_cast<float*>(c->ws[15].ensure(sizeof(float) * att_rows * DP));
   float* dQs = reinterpret_cast<float*>(c->ws[26].ensure(sizeof(float) * (size_t)std::max(max_nq, 1) * DP));
-  // per step row: its logit (kp_cx_stepq)
-  float* dZrow = reinterpret_cast<float*>(c->ws[5].ensure(sizeof(float) * (size_t)std::max(1, max_items)));
   if (npairs > 0) {
     hipLaunchKernelGGL(kp_cx_qpair, dim3(npairs), dim3(128), 0, c->stream, c->dE, c->dR, DP, half, dPairs, npairs,
                        dQpair);
@@ -823,8 +710,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       ea = c->event(2 * hot_launches);
       eb = c->event(2 * hot_launches + 1);
     }
-    const int nt = t_off[t + 1] - t_off[t];
-    CX_DISPATCH(DBV, launch_stepq<DB>(c, dStepQ + q_off[t], nq, dStepT + t_off[t], nt, dX, dQpair, dQs, dZrow));
+    CX_DISPATCH(DBV, launch_stepq<DB>(c, dStepQ + q_off[t], dX, nq, dQs));
     if (nq > 0 && c->time_hot) KP_HIP(hipEventRecord(ea, c->stream));
     CX_DISPATCH(DBV, launch_attn<DB>(c, true, dQs, nq, step_plan[t], dAm, dAl, dAO));
     if (nq > 0) {
@@ -838,8 +724,8 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     opt.step_size = (float)((double)hp->lr / (1.0 - std::pow((double)hp->beta1, step)));
     opt.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)hp->beta2, step));
     CX_DISPATCH(DBV, launch_update<DB>(c, na, dActs + act_off[t], dPlans, dPq, dStepQ + q_off[t], nq,
-                                       dStepT + t_off[t], nt, dTsum, dQpair, dLsef, dZrow, dAm, dAl, dAO, sp,
-                                       dContrib, dX, dS1, dS2, opt));
+                                       dStepT + t_off[t], t_off[t + 1] - t_off[t], dTsum, dQpair, dLsef, dAm, dAl, dAO,
+                                       sp, dContrib, dX, dS1, dS2, opt));
   }
   KP_HIP(hipEventRecord(h1, c->stream));
 
