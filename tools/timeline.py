@@ -58,17 +58,23 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--kernel", default="kp_attn3<25, 0>")
     ap.add_argument("--window", type=float, default=0.4, help="seconds at the end of the trace")
+    ap.add_argument("--skip-end", type=float, default=0.0, help="seconds cut off the end (the pipeline's drain)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end from kernels").fetchall()
-    t1 = max(e for _, _, e in rows)
+    t1 = max(e for _, _, e in rows) - a.skip_end * 1e9
     t0 = t1 - a.window * 1e9
-    rows = [(n, max(s, t0), e) for n, s, e in rows if e > t0]
+    rows = [(n, max(s, t0), min(e, t1)) for n, s, e in rows if e > t0 and s < t1]
     busy = union([(s, e) for _, s, e in rows])
     hot = union([(s, e) for n, s, e in rows if a.kernel in n])
     span = t1 - t0
     print(f"window {span / 1e6:.1f} ms: busy {sum(e - s for s, e in busy) / span:.3f}, "
           f"{a.kernel} active {sum(e - s for s, e in hot) / span:.3f}")
+    # idle gaps between busy intervals, by length
+    gaps = [b[0] - a_[1] for a_, b in zip(busy, busy[1:])]
+    for lo, hi in ((0, 1e4), (1e4, 1e5), (1e5, 1e6), (1e6, 1e12)):
+        g = [x for x in gaps if lo <= x < hi]
+        print(f"  idle gaps {lo / 1e3:g}-{hi / 1e3:g} us: {len(g)} gaps, {sum(g) / span:.3f} of the window")
     per = defaultdict(list)
     for n, s, e in rows:
         per[short_name(n)].append((s, e))
