@@ -339,10 +339,10 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
   float gw[10];
 #pragma unroll
   for (int u = 0; u < 10; ++u) gw[u] = 0.f;
-  for (int j = wave; j < A.f_count; j += 4) {
-    const CvFInst F = fi[A.f_begin + j];
-    float v[10];
-    float part = 0.f;
+  // a wave's pairs two at a time: both pairs' rows are loaded before either reduction, so
+  // a hub slot's long pair list waits on one load latency per two pairs (the sum order,
+  // pair after pair, is unchanged)
+  auto load_pair = [&](const CvFInst& F, float (&v)[10]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 10; ++u) {
       const int d = lane + 64 * u;
@@ -356,14 +356,36 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
           const float dr = k.has_mask ? fc * nz : fc;
           v[u] = fmaxf(dr * a3[d] + b3[d], 0.f);
         }
-        part += v[u] * xs[d];
       }
+    }
+  };
+  auto add_pair = [&](const CvFInst& F, const float (&v)[10]) __attribute__((always_inline)) {
+    float part = 0.f;
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int d = lane + 64 * u;
+      if (d < k.dim) part += v[u] * xs[d];
     }
     const float s = wave_sum(part);
     const float gs = 1.0f / (float)((long long)F.b * (long long)(k.n_ent + 1));
     const float G = bce_g(s, k.yhi, gs);
 #pragma unroll
     for (int u = 0; u < 10; ++u) gw[u] += G * v[u];
+  };
+  int j = wave;
+  for (; j + 4 < A.f_count; j += 8) {
+    const CvFInst F0 = fi[A.f_begin + j], F1 = fi[A.f_begin + j + 4];
+    float v0[10], v1[10];
+    load_pair(F0, v0);
+    load_pair(F1, v1);
+    add_pair(F0, v0);
+    add_pair(F1, v1);
+  }
+  if (j < A.f_count) {
+    const CvFInst F0 = fi[A.f_begin + j];
+    float v0[10];
+    load_pair(F0, v0);
+    add_pair(F0, v0);
   }
 #pragma unroll
   for (int u = 0; u < 10; ++u) {
