@@ -372,7 +372,10 @@ def test_conve_fused_encoder_agrees(monkeypatch):
     post-trainings (several 128-pair tiles per step, a partial last tile): kelpie rows within
     2e-5 of their scale, target scores within 1e-5 relative, ranks equal.  The two differ in
     the FC products (bf16x3 against fp32 MFMA, both exact to fp32 rounding) and in summation
-    order only."""
+    order only.  The shared-encoder split of the fused path (the default without input or
+    feature-map dropout: map rows 0-17 once per kelpie row, rows 18-19 per pair, rows 20-37
+    once per relation) is held to the same bounds against the separate kernels, and so is
+    the fused path with the whole map per pair (KP_CV_SHARED=0)."""
     from kelpie_amd import synth
     g = synth.make_graph("small", seed=5)
     ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
@@ -384,8 +387,9 @@ def test_conve_fused_encoder_agrees(monkeypatch):
     bn = {i: {"weight": w[f"bn{i}_weight"], "bias": w[f"bn{i}_bias"], "running_mean": w[f"bn{i}_mean"],
               "running_var": w[f"bn{i}_var"]} for i in (1, 2, 3)}
     out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("KP_CV_FUSED", mode)
+    for mode in ("0", "1", "shared"):
+        monkeypatch.setenv("KP_CV_FUSED", "0" if mode == "0" else "1")
+        monkeypatch.setenv("KP_CV_SHARED", "1" if mode == "shared" else "0")
         model = ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
                          w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn, hidden_dropout_rate=0.2)
         seed_all(42)
@@ -407,13 +411,15 @@ def test_conve_fused_encoder_agrees(monkeypatch):
             res += [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
                     for pt, b in eng.last_results]
         out[mode] = (res, np.concatenate(xs))
-    x0, x1 = out["0"][1], out["1"][1]
-    assert x0.shape == x1.shape and x0.shape[0] >= 16
-    assert np.max(np.abs(x1 - x0)) <= 2e-5 * np.max(np.abs(x0)), np.max(np.abs(x1 - x0))
-    for a, b in zip(out["1"][0], out["0"][0]):
-        assert abs(a[1] - b[1]) <= 1e-5 * max(1e-3, abs(b[1])), (a, b)
-        assert abs(a[3] - b[3]) <= 1e-5 * max(1e-3, abs(b[3])), (a, b)
-        assert a[0] == b[0] and a[2] == b[2], (a, b)
+    x0 = out["0"][1]
+    for mode in ("1", "shared"):
+        x1 = out[mode][1]
+        assert x0.shape == x1.shape and x0.shape[0] >= 16
+        assert np.max(np.abs(x1 - x0)) <= 2e-5 * np.max(np.abs(x0)), (mode, np.max(np.abs(x1 - x0)))
+        for a, b in zip(out[mode][0], out["0"][0]):
+            assert abs(a[1] - b[1]) <= 1e-5 * max(1e-3, abs(b[1])), (mode, a, b)
+            assert abs(a[3] - b[3]) <= 1e-5 * max(1e-3, abs(b[3])), (mode, a, b)
+            assert a[0] == b[0] and a[2] == b[2], (mode, a, b)
 
 
 @pytest.mark.parametrize("part", PARTS)
