@@ -107,6 +107,10 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     // (kp_cv_fused.hpp) by default; KP_CV_FUSED=0 selects the separate kernels (A/B)
     c->cv_fused = 1;
     if (const char* a = std::getenv("KP_CV_FUSED")) c->cv_fused = std::atoi(a) != 0;
+    // on the fused path without input / feature-map dropout: the encoder split into kelpie
+    // row, pair and relation terms (kp_cv_fused.hpp); KP_CV_SHARED=0 runs the whole map per pair
+    c->cv_shared = 1;
+    if (const char* a = std::getenv("KP_CV_SHARED")) c->cv_shared = std::atoi(a) != 0;
     // ConvE rank of the post-trained row on fp64 logits (sigmoid is monotone), as a fp64
     // reference ranks; KP_CV_RANK=f32 ranks the fp32 sigmoid scores (A/B)
     if (const char* a = std::getenv("KP_CV_RANK")) c->cv_rank64 = std::strcmp(a, "f32") != 0;

@@ -115,6 +115,12 @@ struct kp_ctx {
   int te_rank64 = 1;       // TransE post-training rank on fp64 squared distances (KP_TE_RANK=f32: fp32 norms)
   DevBuf cvf_fw3, cvf_bw3;  // their permuted split images of the FC weight (built once)
   bool cvf_ready = false;
+  int cv_shared = 1;        // ConvE fused path: the shared-encoder split (kp_cv_fused.hpp), KP_CV_SHARED
+  DevBuf cv_wtm, cv_trel;   // its map-row-18-19 FC columns and the relations' FC terms (built once)
+  DevBuf cv_wtl, cv_wfm;    // the kelpie rows' FC columns and the mid columns, transposed (built once)
+  DevBuf cv_wlc;            // the kelpie rows' FC columns [dim][4608] (built once)
+  bool cv_shared_ready = false;
+  DevBuf cvs[10];           // its per-batch workspaces (kp_conve.hip)
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
   kp_cv_train* cvtrain = nullptr;   // kp_conve_train_*'s state (freed with the context)

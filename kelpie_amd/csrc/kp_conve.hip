@@ -149,6 +149,34 @@ __global__ void kp_cv_post_fc(int M, const float* __restrict__ slabs, int ksplit
   }
 }
 
+// the shared-encoder path (kp_cv_fused.hpp): fc_i = (the kelpie row's band slabs, FC bias
+// in band 0) + (the pair's map-row-18-19 slabs) + trel[relation], then as kp_cv_post_fc
+__global__ void kp_cv_post_fc3(int M, const float* __restrict__ sl, int nzl, int nl, const float* __restrict__ sm,
+                               int nzm, const float* __restrict__ trel, const int2* __restrict__ src,
+                               const int2* __restrict__ psr, CvConst k, const CvBits* __restrict__ mb,
+                               const int32_t* __restrict__ bits, const float* __restrict__ bna,
+                               const float* __restrict__ bnb, float* __restrict__ Q) {
+  const int i = blockIdx.x;
+  if (i >= M) return;
+  const int kr = psr[i].x, rel = src[i].y;
+  const float* a3 = bna + 33;
+  const float* b3 = bnb + 33;
+  for (int d = threadIdx.x; d < k.dp; d += blockDim.x) {
+    float v = 0.f;
+    if (d < k.dim) {
+      float fl = 0.f, fm = 0.f;
+      for (int z = 0; z < nzl; ++z) fl += sl[((size_t)z * nl + kr) * k.dim + d];
+      for (int z = 0; z < nzm; ++z) fm += sm[((size_t)z * M + i) * k.dim + d];
+      const float fc = (fl + fm) + trel[(size_t)rel * k.dim + d];
+      float nz = 1.0f;
+      if (mb && k.has_mask) nz = noise_at(bits, mb[i].hid, d, k.scale);
+      const float dr = (mb && k.has_mask) ? fc * nz : fc;
+      v = fmaxf(dr * a3[d] + b3[d], 0.f);
+    }
+    Q[(size_t)i * k.dp + d] = v;
+  }
+}
+
 // block-wide sum (256 threads)
 __device__ __forceinline__ float block_sum(float v, float* sh) {
   v = wave_sum(v);
@@ -285,16 +313,96 @@ struct CvOpt {
   float lr, b1, b2, eps, one_minus_b1, one_minus_b2, step_size, bc2_sqrt;
 };
 
-// gradient assembly + Adam, one workgroup per active slot
-__global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __restrict__ act,
-                                                    const CvInst* __restrict__ ki, const CvFInst* __restrict__ fi,
-                                                    const float* __restrict__ Q, const float* __restrict__ gk,
-                                                    const float* __restrict__ dl, const float* __restrict__ fcf,
-                                                    const int32_t* __restrict__ bits, const float* __restrict__ bna,
-                                                    const float* __restrict__ bnb, float* __restrict__ X,
-                                                    float* __restrict__ S1, float* __restrict__ S2, CvOpt opt) {
+// the frozen-head pairs' part of a slot's gradient (o, r_inv, kelpie): the kelpie
+// column's BCE gradient G * x_fc, in chunks of up to FCH pairs of one slot, one workgroup per
+// chunk (a hub slot's hundreds of pairs no longer run as one workgroup's serial loop);
+// ch = (slot's act index in the step, first pair, pair count); fpart[chunk][d]
+constexpr int FCH = 16;
+__global__ __launch_bounds__(256) void kp_cv_fgrad(CvConst k, const int4* __restrict__ chunks,
+                                                   const CvAct* __restrict__ act, const CvFInst* __restrict__ fi,
+                                                   const float* __restrict__ fcf, const int32_t* __restrict__ bits,
+                                                   const float* __restrict__ bna, const float* __restrict__ bnb,
+                                                   const float* __restrict__ X, float* __restrict__ fpart) {
   __shared__ float xs[640];
-  __shared__ float gw_s[4][640];  // per-wave partial gradients of the frozen-head pairs
+  __shared__ float gw_s[4][640];  // per-wave partial sums
+  const int4 ch = chunks[blockIdx.x];
+  const CvAct A = act[ch.x];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const float* x = X + (size_t)A.slot * k.dp;
+  for (int d = tid; d < k.dp; d += 256) xs[d] = x[d];
+  __syncthreads();
+  const float* a3 = bna + 33;
+  const float* b3 = bnb + 33;
+  float gw[10];
+#pragma unroll
+  for (int u = 0; u < 10; ++u) gw[u] = 0.f;
+  auto load_pair = [&](const CvFInst& F, float (&v)[10]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int d = lane + 64 * u;
+      v[u] = 0.f;
+      if (d < k.dim) {
+        if (k.fr_step) {  // encoded this step with its own masks (kp_cv_post_fc)
+          v[u] = fcf[(size_t)F.fp * k.dp + d];
+        } else {
+          const float fc = fcf[(size_t)F.fp * k.dim + d];
+          const float nz = k.has_mask ? noise_at(bits, F.mb.hid, d, k.scale) : 1.0f;
+          const float dr = k.has_mask ? fc * nz : fc;
+          v[u] = fmaxf(dr * a3[d] + b3[d], 0.f);
+        }
+      }
+    }
+  };
+  auto add_pair = [&](const CvFInst& F, const float (&v)[10]) __attribute__((always_inline)) {
+    float part = 0.f;
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int d = lane + 64 * u;
+      if (d < k.dim) part += v[u] * xs[d];
+    }
+    const float s = wave_sum(part);
+    const float gs = 1.0f / (float)((long long)F.b * (long long)(k.n_ent + 1));
+    const float G = bce_g(s, k.yhi, gs);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) gw[u] += G * v[u];
+  };
+  // a wave's pairs (wave, wave + 4, ...) two at a time: both rows loaded before either
+  // reduction
+  const int f0 = A.f_begin + ch.y;
+  int j = wave;
+  for (; j + 4 < ch.z; j += 8) {
+    const CvFInst F0 = fi[f0 + j], F1 = fi[f0 + j + 4];
+    float v0[10], v1[10];
+    load_pair(F0, v0);
+    load_pair(F1, v1);
+    add_pair(F0, v0);
+    add_pair(F1, v1);
+  }
+  if (j < ch.z) {
+    const CvFInst F0 = fi[f0 + j];
+    float v0[10];
+    load_pair(F0, v0);
+    add_pair(F0, v0);
+  }
+#pragma unroll
+  for (int u = 0; u < 10; ++u) {
+    const int d = lane + 64 * u;
+    if (d < k.dim) gw_s[wave][d] = gw[u];
+  }
+  __syncthreads();
+  for (int d = tid; d < k.dim; d += 256)
+    fpart[(size_t)blockIdx.x * k.dim + d] = (gw_s[0][d] + gw_s[1][d]) + (gw_s[2][d] + gw_s[3][d]);
+}
+
+// gradient assembly + Adam, one workgroup per active slot; its frozen-head pairs' part is
+// the sum of its kp_cv_fgrad chunks (A.pad0: first chunk of the step, A.pad1: count)
+__global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __restrict__ act,
+                                                    const float* __restrict__ Q, const float* __restrict__ gk,
+                                                    const float* __restrict__ dl, const float* __restrict__ fpart,
+                                                    float* __restrict__ X, float* __restrict__ S1,
+                                                    float* __restrict__ S2, CvOpt opt) {
+  __shared__ float xs[640];
   const CvAct A = act[blockIdx.x];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -332,72 +440,14 @@ __global__ __launch_bounds__(256) void kp_cv_update(CvConst k, const CvAct* __re
       }
     }
   }
-  // frozen-head pairs (o, r_inv, kelpie): the kelpie column's BCE gradient G * x_fc,
-  // one pair per wave at a time (wave reductions, no workgroup barrier per pair)
-  const float* a3 = bna + 33;
-  const float* b3 = bnb + 33;
-  float gw[10];
-#pragma unroll
-  for (int u = 0; u < 10; ++u) gw[u] = 0.f;
-  // a wave's pairs two at a time: both pairs' rows are loaded before either reduction, so
-  // a hub slot's long pair list waits on one load latency per two pairs (the sum order,
-  // pair after pair, is unchanged)
-  auto load_pair = [&](const CvFInst& F, float (&v)[10]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < 10; ++u) {
-      const int d = lane + 64 * u;
-      v[u] = 0.f;
-      if (d < k.dim) {
-        if (k.fr_step) {  // encoded this step with its own masks (kp_cv_post_fc)
-          v[u] = fcf[(size_t)F.fp * k.dp + d];
-        } else {
-          const float fc = fcf[(size_t)F.fp * k.dim + d];
-          const float nz = k.has_mask ? noise_at(bits, F.mb.hid, d, k.scale) : 1.0f;
-          const float dr = k.has_mask ? fc * nz : fc;
-          v[u] = fmaxf(dr * a3[d] + b3[d], 0.f);
-        }
-      }
-    }
-  };
-  auto add_pair = [&](const CvFInst& F, const float (&v)[10]) __attribute__((always_inline)) {
-    float part = 0.f;
-#pragma unroll
-    for (int u = 0; u < 10; ++u) {
-      const int d = lane + 64 * u;
-      if (d < k.dim) part += v[u] * xs[d];
-    }
-    const float s = wave_sum(part);
-    const float gs = 1.0f / (float)((long long)F.b * (long long)(k.n_ent + 1));
-    const float G = bce_g(s, k.yhi, gs);
-#pragma unroll
-    for (int u = 0; u < 10; ++u) gw[u] += G * v[u];
-  };
-  int j = wave;
-  for (; j + 4 < A.f_count; j += 8) {
-    const CvFInst F0 = fi[A.f_begin + j], F1 = fi[A.f_begin + j + 4];
-    float v0[10], v1[10];
-    load_pair(F0, v0);
-    load_pair(F1, v1);
-    add_pair(F0, v0);
-    add_pair(F1, v1);
-  }
-  if (j < A.f_count) {
-    const CvFInst F0 = fi[A.f_begin + j];
-    float v0[10];
-    load_pair(F0, v0);
-    add_pair(F0, v0);
-  }
-#pragma unroll
-  for (int u = 0; u < 10; ++u) {
-    const int d = lane + 64 * u;
-    if (d < k.dim) gw_s[wave][d] = gw[u];
-  }
   __syncthreads();
   for (int u = 0; u < 3; ++u) {
     const int d = tid + 256 * u;
     if (d >= k.dim) continue;
     if (wide) g[u] = (gk_s[0][d] + gk_s[1][d]) + (gk_s[2][d] + gk_s[3][d]);
-    g[u] += (gw_s[0][d] + gw_s[1][d]) + (gw_s[2][d] + gw_s[3][d]);
+    float fw = 0.f;
+    for (int c = 0; c < A.pad1; ++c) fw += fpart[(size_t)(A.pad0 + c) * k.dim + d];
+    g[u] += fw;
   }
   for (int u = 0; u < 3; ++u) {
     const int d = tid + 256 * u;
@@ -614,7 +664,16 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   std::vector<int> kin_off(T + 1, 0), fin_off(T + 1, 0), act_o(T + 1, 0), enc_off(T + 1, 0);
   std::vector<int2> enc_src;
   std::vector<CvBits> enc_bits;
-  int max_k = 0, max_enc = 0;
+  // the shared-encoder path's kelpie rows per step (one per slot with a kelpie pair in the
+  // step: its source and its pairs' range in the step's list), and per kelpie pair (its
+  // kelpie row, first pair of that row)
+  std::vector<int> sr_off(T + 1, 0);
+  // the frozen-head pairs' chunks per step (kp_cv_fgrad)
+  std::vector<int> fch_off(T + 1, 0);
+  std::vector<int4> fchunks;
+  int max_fch = 0;
+  std::vector<int2> sr_src, sr_rng, psr;
+  int max_k = 0, max_enc = 0, max_sr = 0;
   for (int t = 0; t < T; ++t) {
     kin_off[t] = (int)kinst.size();
     fin_off[t] = (int)finst.size();
@@ -622,6 +681,8 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     enc_off[t] = (int)enc_src.size();
     std::vector<int2> fr_hr;  // the step's frozen-head (h, r), with fr_step
     int local_k = 0;
+    sr_off[t] = (int)sr_src.size();
+    fch_off[t] = (int)fchunks.size();
     for (int s = 0; s < ns; ++s) {
       const int nb = plan[s].nb;
       if (nb == 0 || t >= E_ * nb) continue;
@@ -633,9 +694,16 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       A.slot = s;
       A.k_begin = local_k;
       A.f_begin = (int)finst.size() - fin_off[t];
+      int my_sr = -1;
       for (int q = p0; q < p1; ++q) {
         const auto& pr = P[q];
         if (pr.h == K) {
+          const bool first = my_sr < 0;
+          if (first) {
+            my_sr = (int)sr_src.size() - sr_off[t];
+            sr_src.push_back(make_int2(-s - 1, 0));
+          }
+          psr.push_back(make_int2(my_sr, first ? 1 : 0));
           CvInst I{};
           I.slot = s;
           I.rel = pr.r;
@@ -663,8 +731,15 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       }
       A.k_count = local_k - A.k_begin;
       A.f_count = (int)finst.size() - fin_off[t] - A.f_begin;
+      A.pad0 = (int)fchunks.size() - fch_off[t];
+      A.pad1 = (A.f_count + FCH - 1) / FCH;
+      for (int f = 0; f < A.f_count; f += FCH)
+        fchunks.push_back(make_int4((int)acts.size() - act_o[t], f, std::min(FCH, A.f_count - f), 0));
       acts.push_back(A);
+      if (my_sr >= 0) sr_rng.push_back(make_int2(A.k_begin, A.k_begin + A.k_count));
     }
+    max_sr = std::max(max_sr, (int)sr_src.size() - sr_off[t]);
+    max_fch = std::max(max_fch, (int)fchunks.size() - fch_off[t]);
     for (int i = kin_off[t]; i < (int)kinst.size(); ++i) {
       enc_src.push_back(make_int2(-kinst[i].slot - 1, kinst[i].rel));
       enc_bits.push_back(kinst[i].mb);
@@ -679,6 +754,8 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     max_enc = std::max(max_enc, (int)enc_src.size() - enc_off[t]);
   }
   enc_off[T] = (int)enc_src.size();
+  sr_off[T] = (int)sr_src.size();
+  fch_off[T] = (int)fchunks.size();
   kin_off[T] = (int)kinst.size();
   fin_off[T] = (int)finst.size();
   act_o[T] = (int)acts.size();
@@ -733,9 +810,73 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     dRelu = reinterpret_cast<uint8_t*>(c->ws[24].ensure((size_t)me * kpcvf::MASK_B));
     dG3 = reinterpret_cast<__bf16*>(c->ws[25].ensure(3 * sizeof(__bf16) * (size_t)mk * kpcvf::KB));
   }
+  // the shared-encoder split (kp_cv_fused.hpp): kelpie rows' map rows 0-17 in NB_L bands,
+  // the pairs' rows 18-19 in NB_M, the relations' rows 20-37 (once per context) in NB_L
+  const bool shared = fused && c->cv_shared && !kc.has_in && !kc.has_fm;
+  constexpr int NB_L = 24;
+  const int msr = std::max(1, max_sr);
+  int2* dSrSrc = nullptr;
+  int2* dSrRng = nullptr;
+  int2* dPsr = nullptr;
+  uint8_t* dReluS = nullptr;
+  float* dSlabL = nullptr;  // kelpie rows' FC split-K slabs [KSL][rows][dim]
+  float* dMid = nullptr;    // pairs' map-row-18-19 FC terms [pairs][dim]
+  float* dMapL = nullptr;   // kelpie rows' map rows 0-17, then (backward) g W_lhs
+  float* dMapM = nullptr;   // pairs' map rows 18-19, then (backward) dfc W_mid [pairs][512]
+  float* dGs = nullptr;     // kelpie rows' summed pair dfc
+  float* dDls = nullptr;    // kelpie rows' lhs image gradient [rows][DP]
+  if (shared) {
+    if (!c->cv_shared_ready) {
+      float* wtm = reinterpret_cast<float*>(c->cv_wtm.ensure(sizeof(float) * (size_t)c->dim * kpcvf::NMID));
+      hipLaunchKernelGGL(kpcvf::kp_cv_mid_wt, dim3((c->dim * kpcvf::NMID + 255) / 256), dim3(256), 0, c->stream,
+                         c->d_fc_w, c->dim, wtm);
+      KP_HIP(hipGetLastError());
+      float* wtl = reinterpret_cast<float*>(c->cv_wtl.ensure(sizeof(float) * (size_t)c->dim * kpcvf::NLHS));
+      float* wlc = reinterpret_cast<float*>(c->cv_wlc.ensure(sizeof(float) * (size_t)c->dim * kpcvf::NLHS));
+      float* wfm = reinterpret_cast<float*>(c->cv_wfm.ensure(sizeof(float) * (size_t)c->dim * kpcvf::NMID));
+      const int nw = (kpcvf::NLHS + kpcvf::NMID) * c->dim;
+      hipLaunchKernelGGL(kpcvf::kp_cv_lhs_wt, dim3((nw + 255) / 256), dim3(256), 0, c->stream, c->d_fc_w, c->dim, wlc,
+                         wtl, wfm);
+      KP_HIP(hipGetLastError());
+      // the relations' FC terms: map rows 20-37 (the relation half only), no bias
+      const int nr = c->n_rel2;
+      std::vector<int2> rs(nr);
+      for (int r = 0; r < nr; ++r) rs[r] = make_int2(0, r);
+      DevBuf bs, bo;
+      int2* dRs = upload(c, bs, rs.data(), rs.size());
+      float* sl = reinterpret_cast<float*>(bo.ensure(sizeof(float) * (size_t)NB_L * nr * c->dim));
+      const int g = NB_L * ((nr + kpcvf::MT - 1) / kpcvf::MT);
+      hipLaunchKernelGGL(kpcvf::kp_cv_fwd_fused<false>, dim3(g), dim3(512), kpcvf::FWD_LDS, c->stream, nr, dRs, c->dE,
+                         dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, cvf_fw, nullptr, c->dim,
+                         nullptr, dBits, 1.0f, 1.0f, sl, nullptr, 8 * (kpcvf::MID_Y + 2),
+                         8 * (kpcvf::FR - kpcvf::MID_Y - 2), NB_L, 2);
+      KP_HIP(hipGetLastError());
+      float* tr = reinterpret_cast<float*>(c->cv_trel.ensure(sizeof(float) * (size_t)nr * c->dim));
+      hipLaunchKernelGGL(kpcvf::kp_cv_slab_sum, dim3((nr * c->dim + 255) / 256), dim3(256), 0, c->stream, nr, NB_L,
+                         c->dim, sl, tr);
+      KP_HIP(hipGetLastError());
+      KP_HIP(hipStreamSynchronize(c->stream));
+      bs.release();
+      bo.release();
+      c->cv_shared_ready = true;
+    }
+    dSrSrc = upload(c, c->cvs[0], sr_src.data(), std::max<size_t>(1, sr_src.size()));
+    dSrRng = upload(c, c->cvs[1], sr_rng.data(), std::max<size_t>(1, sr_rng.size()));
+    dPsr = upload(c, c->cvs[2], psr.data(), std::max<size_t>(1, psr.size()));
+    dReluS = reinterpret_cast<uint8_t*>(c->cvs[3].ensure((size_t)msr * kpcvf::MASK_B));
+    KP_HIP(hipMemsetAsync(dReluS, 0, (size_t)msr * kpcvf::MASK_B, c->stream));  // rows 18-19 stay 0
+    dSlabL = reinterpret_cast<float*>(c->cvs[4].ensure(sizeof(float) * (size_t)kpcvf::KSL * msr * c->dim));
+    dMapM = reinterpret_cast<float*>(c->cvs[9].ensure(sizeof(float) * (size_t)mk * kpcvf::NMID));
+    dMid = reinterpret_cast<float*>(c->cvs[5].ensure(sizeof(float) * (size_t)mk * c->dim));
+    dMapL = reinterpret_cast<float*>(c->cvs[6].ensure(sizeof(float) * (size_t)msr * kpcvf::NLHS));
+    dGs = reinterpret_cast<float*>(c->cvs[7].ensure(sizeof(float) * (size_t)msr * c->dim));
+    dDls = reinterpret_cast<float*>(c->cvs[8].ensure(sizeof(float) * (size_t)msr * DP));
+  }
   const int n_dl = fused ? kpcvf::NSPLIT : 1;  // lhs image-gradient slabs per pair (kp_cv_bwd_fused, reduced in slab 0)
   float* dQ = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)me * DP));
   int2* dSrc = upload(c, c->ws[15], enc_src.data(), std::max<size_t>(1, enc_src.size()));
+  int4* dFch = upload(c, c->ws[28], fchunks.data(), std::max<size_t>(1, fchunks.size()));
+  float* dFpart = reinterpret_cast<float*>(c->ws[31].ensure(sizeof(float) * (size_t)std::max(1, max_fch) * c->dim));
   CvBits* dEncBits = upload(c, c->ws[26], enc_bits.data(), std::max<size_t>(1, enc_bits.size()));
   float* dgs = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)std::max<size_t>(1, kinst.size())));
   {
@@ -794,17 +935,34 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     const CvInst* KI = dKI + kin_off[t];
     const int2* ES = dSrc + enc_off[t];
     const CvBits* EB = dEncBits + enc_off[t];
-    if (ne > 0) {  // encoder forward (conve.py:133-153, train-mode dropouts)
+    const int nsr = sr_off[t + 1] - sr_off[t];
+    if (ne > 0 && shared) {  // encoder forward, shared split (kp_cv_fused.hpp); ne == nk here
+      hipLaunchKernelGGL(kpcvf::kp_cv_lhs_map, dim3(nsr), dim3(256), 0, c->stream, nsr, dSrSrc + sr_off[t], dX, DP,
+                         c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dMapL, dReluS);
+      KP_HIP(hipGetLastError());
+      launch_gemm_abt(c, dMapL, kpcvf::NLHS, nsr, c->cv_wlc.as<float>(), kpcvf::NLHS, c->dim, kpcvf::NLHS, dSlabL,
+                      c->dim, c->d_fc_b, 0, kpcvf::KSL);
+      hipLaunchKernelGGL(kpcvf::kp_cv_mid_map, dim3((ne * kpcvf::CH * 2 + 255) / 256), dim3(256), 0, c->stream, ne, ES,
+                         c->dE, dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, dMapM, dRelu);
+      KP_HIP(hipGetLastError());
+      launch_gemm_abt(c, dMapM, kpcvf::NMID, ne, c->cv_wtm.as<float>(), kpcvf::NMID, c->dim, kpcvf::NMID, dMid, c->dim,
+                      nullptr, 0, 1);
+      hipLaunchKernelGGL(kp_cv_post_fc3, dim3(ne), dim3(256), 0, c->stream, ne, dSlabL, kpcvf::KSL, nsr, dMid, 1,
+                         c->cv_trel.as<float>(), ES, dPsr + kin_off[t], kc, EB, dBits, c->d_bn_a, c->d_bn_b, dQ);
+      KP_HIP(hipGetLastError());
+    } else if (ne > 0) {  // encoder forward (conve.py:133-153, train-mode dropouts)
       if (fused) {
         const int fgrid = kpcvf::NSPLIT * ((ne + kpcvf::MT - 1) / kpcvf::MT);
         if (kc.fr_step)
           hipLaunchKernelGGL(kpcvf::kp_cv_fwd_fused<true>, dim3(fgrid), dim3(512), kpcvf::FWD_LDS, c->stream, ne, ES,
                              c->dE, dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, cvf_fw, c->d_fc_b,
-                             c->dim, EB, dBits, s_in, s_fm, dslab, dRelu);
+                             c->dim, EB, dBits, s_in, s_fm, dslab, dRelu, 0, kpcvf::FR * 8,
+                             kpcvf::NSPLIT, 8);
         else
           hipLaunchKernelGGL(kpcvf::kp_cv_fwd_fused<false>, dim3(fgrid), dim3(512), kpcvf::FWD_LDS, c->stream, ne, ES,
                              c->dE, dX, c->dR, DP, c->d_conv_w, c->d_conv_b, c->d_bn_a, c->d_bn_b, cvf_fw, c->d_fc_b,
-                             c->dim, EB, dBits, s_in, s_fm, dslab, dRelu);
+                             c->dim, EB, dBits, s_in, s_fm, dslab, dRelu, 0, kpcvf::FR * 8,
+                             kpcvf::NSPLIT, 8);
         KP_HIP(hipGetLastError());
       } else {
         KP_CONV_FWD(dim3(ne), dim3(256), 0, c->stream, ne, ES, c->dE, dX, c->dR, kc, c->d_conv_w, c->d_conv_b,
@@ -853,9 +1011,25 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       }
       ++launches;
       hipLaunchKernelGGL(kp_cv_dx, dim3(nk), dim3(256), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE, dX,
-                         dBits, c->d_bn_a, ddfc, dgk, dG3);
+                         dBits, c->d_bn_a, ddfc, dgk, shared ? nullptr : dG3);
       KP_HIP(hipGetLastError());
-      if (fused) {
+      if (shared) {
+        // map rows 0-17 once per kelpie row (the sum of its pairs' dfc; rows 18-19 of its
+        // ReLU bytes are 0), then rows 18-19 per pair, assembled into the pairs' dl rows
+        hipLaunchKernelGGL(kpcvf::kp_cv_slot_g, dim3(nsr), dim3(256), 0, c->stream, nsr, dSrRng + sr_off[t], ddfc,
+                           c->dim, dGs);
+        KP_HIP(hipGetLastError());
+        launch_gemm_abt(c, dGs, c->dim, nsr, c->cv_wtl.as<float>(), c->dim, kpcvf::NLHS, c->dim, dMapL, kpcvf::NLHS,
+                        nullptr, 0, 1);
+        hipLaunchKernelGGL(kpcvf::kp_cv_lhs_convt, dim3(nsr), dim3(256), 0, c->stream, nsr, dMapL, dReluS, c->d_conv_w,
+                           c->d_bn_a, DP, dDls);
+        KP_HIP(hipGetLastError());
+        launch_gemm_abt(c, ddfc, c->dim, nk, c->cv_wfm.as<float>(), c->dim, kpcvf::NMID, c->dim, dMapM, kpcvf::NMID,
+                        nullptr, 0, 1);
+        hipLaunchKernelGGL(kpcvf::kp_cv_mid_convt, dim3((nk + kpcvf::MPW - 1) / kpcvf::MPW), dim3(256), 0, c->stream, nk,
+                           dMapM, dRelu, c->d_conv_w, c->d_bn_a, dPsr + kin_off[t], dDls, DP, ddl);
+        KP_HIP(hipGetLastError());
+      } else if (fused) {
         const int bgrid = kpcvf::NSPLIT * ((nk + kpcvf::MT - 1) / kpcvf::MT);
         hipLaunchKernelGGL(kpcvf::kp_cv_bwd_fused, dim3(bgrid), dim3(512), kpcvf::BWD_LDS, c->stream, nk, dG3,
                            cvf_bw, dRelu, c->d_conv_w, c->d_bn_a, s_fm, DP, ddl);
@@ -883,8 +1057,14 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     if (na > 0) {
       // dAct entries index kinst/finst relative to this step's lists; the frozen-head pairs
       // read their encodings from dQ (fr_step) or the batch's FC rows
-      hipLaunchKernelGGL(kp_cv_update, dim3(na), dim3(256), 0, c->stream, kc, dAct + act_o[t], KI, dFI + fin_off[t], dQ,
-                         dgk, ddl, kc.fr_step ? dQ : dFcf, dBits, c->d_bn_a, c->d_bn_b, dX, dS1, dS2, opt);
+      const int nch = fch_off[t + 1] - fch_off[t];
+      if (nch > 0) {
+        hipLaunchKernelGGL(kp_cv_fgrad, dim3(nch), dim3(256), 0, c->stream, kc, dFch + fch_off[t], dAct + act_o[t],
+                           dFI + fin_off[t], kc.fr_step ? dQ : dFcf, dBits, c->d_bn_a, c->d_bn_b, dX, dFpart);
+        KP_HIP(hipGetLastError());
+      }
+      hipLaunchKernelGGL(kp_cv_update, dim3(na), dim3(256), 0, c->stream, kc, dAct + act_o[t], dQ, dgk, ddl, dFpart,
+                         dX, dS1, dS2, opt);
       KP_HIP(hipGetLastError());
     }
   }

@@ -89,6 +89,12 @@ __device__ __forceinline__ void xcd_map(int b, int& z, int& mt) {
   z = x + 8 * (j & 1);
   mt = j >> 1;
 }
+// the same for nb bands (a multiple of 8): XCD x owns bands x, x + 8, x + 16, ...
+__device__ __forceinline__ void xcd_map_n(int b, int nb, int& z, int& mt) {
+  const int x = b & 7, j = b >> 3, per = nb >> 3;
+  z = x + 8 * (j % per);
+  mt = j / per;
+}
 
 // W [dim][HID] fp32 -> forward image [3][NR][HID] (k' order) and backward image
 // [3][NBL][KB] (row = 160 c + 8 y + x, y < 20; column = FC output; zero padded)
@@ -120,8 +126,13 @@ __global__ void kp_cv_bwd_image(const float* __restrict__ W, int dim, __bf16* __
   out[2 * ps + i] = l;
 }
 
-// forward: out[z][i][n] = sum over band z of map_i[k] W[n][k] (+ fc bias in band 0);
-// relu[i][20 ch + y] = ReLU signs of row y < 20 of channel ch
+// forward: out[z][i][n] = sum over band z of map_i[k] W[n][k] (+ fc bias in band 0 when
+// fcb is given); relu[i][20 ch + y] = ReLU signs of row y < 20 of channel ch.
+// The k steps (32 deep: one map row y and one group of four channels cg, q = 8 y + cg)
+// [q_lo, q_lo + n_q) are cut into n_band bands (a multiple of 8) on multiples of gran
+// steps (even): the whole map is (0, 304, 16, 8), 16 bands of whole rows; the shared-
+// encoder path (kp_conve.hip) runs the kelpie rows' map rows 0-17, the pairs' rows 18-19
+// and the relations' rows 20-37 apart.
 // DROP: the input / feature-map dropout code is compiled in (the model has one of them)
 template <bool DROP>
 __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __restrict__ src,
@@ -132,14 +143,15 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
                                                        const __bf16* __restrict__ W3, const float* __restrict__ fcb,
                                                        int dim, const CvBits* __restrict__ mb,
                                                        const int32_t* __restrict__ bits, float s_in, float s_fm,
-                                                       float* __restrict__ out, uint8_t* __restrict__ relu) {
+                                                       float* __restrict__ out, uint8_t* __restrict__ relu,
+                                                       int q_lo, int n_q, int n_band, int gran) {
   extern __shared__ __attribute__((aligned(16))) __bf16 bsh[];  // [stage][piece][NR][RS]
   __shared__ float sw[CH * 9], sc[CH], sa[CH], sbb[CH];
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   int z, mt;
-  xcd_map(blockIdx.x, z, mt);
+  xcd_map_n(blockIdx.x, n_band, z, mt);
   const int m0 = mt * MT;
   if (m0 >= M) return;  // whole-workgroup exit (uniform), before any barrier
   for (int j = tid; j < CH * 9; j += 512) sw[j] = cw[j];
@@ -174,14 +186,16 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
       if (DROP && pb.in >= 0) o[xx] *= ((kb >> xx) & 1u) ? s_in : 0.f;
     }
   };
-  const int y0 = band_y0(z), y1 = band_y0(z + 1);
-  const int nst = (y1 - y0) * 8;
+  const int ng = n_q / gran;
+  const int q0 = q_lo + gran * ((ng * z) / n_band), q1 = q_lo + gran * ((ng * (z + 1)) / n_band);
+  const int y0 = q0 >> 3;
+  const int nst = q1 - q0;  // even
 
   // staging: thread -> weight rows tid >> 2 and (while < NR) tid >> 2 + 128, k 8 (tid & 3) .. + 7
   const int srow = tid >> 2, sk = 8 * (tid & 3);
   const bool two = srow + 128 < NR;  // wave-uniform (tid < 320)
   const size_t ps = (size_t)NR * HID;
-  const __bf16* gp = W3 + (size_t)srow * HID + (size_t)y0 * 256 + sk;
+  const __bf16* gp = W3 + (size_t)srow * HID + (size_t)q0 * 32 + sk;
   // the second row's loads are unconditional (a wave without one re-reads its first row and
   // does not store it): loads under a branch were waited for at once and parked in scratch
   const __bf16* gp2 = gp + (two ? (size_t)128 * HID : 0);
@@ -237,7 +251,7 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
   // lambda called twice the accumulators were not promoted to registers)
 #define KP_CVF_KSTEP(Q, ST)                                                                    \
   do {                                                                                         \
-    const int y = y0 + ((Q) >> 3), cg = (Q) & 7;                                               \
+    const int y = (q0 + (Q)) >> 3, cg = (q0 + (Q)) & 7;                                        \
     if (cg == 0 && (Q) > 0) {                                                                  \
       bn1_row(y + 2, nx);                                                                      \
       _Pragma("unroll") for (int xx = 0; xx < IW; ++xx) {                                      \
@@ -281,7 +295,7 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
 
   // two register stages of weight loads in flight (each load is consumed two k steps after
   // it is issued: one step of cover left the barrier waiting on L2 misses), two LDS
-  // stages, one barrier per k step; nst = 8 x rows is even
+  // stages, one barrier per k step; nst is even
   KP_CVF_GLOAD(ra, 0);
   KP_CVF_GLOAD(rb, 1);
   KP_CVF_LSTORE(ra, 0);
@@ -304,7 +318,7 @@ __global__ __launch_bounds__(512) void kp_cv_fwd_fused(int M, const int2* __rest
   for (int n = 0; n < NBF; ++n) {
     const int col = 16 * n + c;
     if (col >= dim) continue;
-    const float bias = z == 0 ? fcb[col] : 0.f;
+    const float bias = (z == 0 && fcb) ? fcb[col] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + 16 * w + 4 * g + r;
@@ -489,6 +503,242 @@ __global__ void kp_cv_dl_reduce(int M, int dp, const CvBits* __restrict__ mb, co
     v *= (((uint32_t)bits[b >> 5] >> (b & 31)) & 1u) ? s_in : 0.f;
   }
   dl[o] = v;
+}
+
+// ---------------------------------------------------------------------------------
+// Shared-encoder path (no input or feature-map dropout; kp_conve.hip, KP_CV_SHARED).
+// Map rows 0-17 read only the kelpie half of the image (rows 0-19), rows 20-37 only the
+// relation half, rows 18-19 both.  So per step the FC input splits as
+//   fc_i = W_lhs map_lhs(x_slot) + W_mid map_mid(x_slot, r_i) + W_rel map_rel(r_i) + b:
+// the first term once per kelpie row (slot) instead of once per pair, the last once per
+// relation and context (relations and layers are frozen), and only the 512 columns of
+// rows 18-19 per pair.  The backward splits the same way: the ReLU signs of rows 0-17
+// are the kelpie row's, so the pairs' gradients of those rows are one product with the
+// sum of the pairs' dfc; rows 18-19 go per pair.  On the bench's ConvE step (3,456 pairs of
+// 160 kelpie rows) that is under 10 % of the fused path's multiply-adds.
+constexpr int MID_Y = 18;          // first map row that reads the relation half
+constexpr int NMID = CH * 2 * FW;  // its 512 columns (rows 18-19 of every channel)
+constexpr int MPW = 16;            // pairs per workgroup of kp_cv_mid_bwd
+
+// W [dim][HID] -> the transposed mid columns [dim][512], col = 16 ch + 8 (y - 18) + x
+__global__ void kp_cv_mid_wt(const float* __restrict__ W, int dim, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= dim * NMID) return;
+  const int d = i / NMID, col = i % NMID;
+  const int ch = col >> 4, y = MID_Y + ((col >> 3) & 1), x = col & 7;
+  out[i] = W[(size_t)d * HID + ch * (FR * FW) + y * FW + x];
+}
+
+// The maps and transposed convolutions are small fp32 kernels; the four products (the
+// kelpie rows' map rows 0-17 and the pairs' rows 18-19 through the FC, and the two
+// transposed products of the backward) go to the fp32 MFMA GEMM (kp_gemm_abt, 64 x 64
+// tiles).  A step has ~160 kelpie rows, too few for the 128-row bf16x3 tiles above (their
+// per-workgroup latency, not the arithmetic, set the time), and the plain fp32 loops over
+// an LDS operand that were tried first ran 3 TFLOP/s.
+constexpr int LHS_Y = 18;              // map rows 0-17 read the kelpie half only
+constexpr int NLHS = CH * LHS_Y * FW;  // their 4608 columns, l = 144 c + 8 y + x
+constexpr int KSL = 16;                // split-K slabs of the kelpie rows' FC product
+
+__host__ __device__ constexpr int lhs_col(int l) { return (l / 144) * (FR * FW) + l % 144; }
+
+// W [dim][HID] -> the kelpie rows' columns [dim][4608] and transposed [4608][dim], and the
+// mid columns transposed [512][dim] (col = 16 ch + 8 (y - 18) + x)
+__global__ void kp_cv_lhs_wt(const float* __restrict__ W, int dim, float* __restrict__ wlc, float* __restrict__ wl,
+                             float* __restrict__ wm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < NLHS * dim) {
+    const int l = i / dim, o = i % dim;
+    wl[i] = W[(size_t)o * HID + lhs_col(l)];
+    const int o2 = i / NLHS, l2 = i % NLHS;
+    wlc[i] = W[(size_t)o2 * HID + lhs_col(l2)];
+  } else if (i < (NLHS + NMID) * dim) {
+    const int e = i - NLHS * dim, col = e / dim, o = e % dim;
+    const int ch = col >> 4, y = MID_Y + ((col >> 3) & 1), x = col & 7;
+    wm[e] = W[(size_t)o * HID + ch * (FR * FW) + y * FW + x];
+  }
+}
+
+// per pair i: map rows 18-19 (image rows 18-21: the kelpie half's rows 18-19 and the
+// relation half's rows 0-1; BN1, conv, bias, BN2, ReLU) -> mm[i][512] and their ReLU
+// sign bytes relu[i][20 ch + y]; one thread per (pair, channel, row)
+__global__ void kp_cv_mid_map(int M, const int2* __restrict__ src, const float* __restrict__ E,
+                              const float* __restrict__ X, const float* __restrict__ R, int dp,
+                              const float* __restrict__ cw, const float* __restrict__ cb,
+                              const float* __restrict__ bna, const float* __restrict__ bnb, float* __restrict__ mm,
+                              uint8_t* __restrict__ relu) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= M * CH * 2) return;
+  const int i = e / (CH * 2), c = (e / 2) % CH, yy = e % 2;
+  const int2 s = src[i];
+  const float* lhs = s.x >= 0 ? E + (size_t)s.x * dp : X + (size_t)(-s.x - 1) * dp;
+  const float* rel = R + (size_t)s.y * dp;
+  const float a1 = bna[0], b1 = bnb[0];
+  float im[3][IW];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int yr = MID_Y + yy + ky;
+    const float* row = yr < LR ? lhs + yr * IW : rel + (yr - LR) * IW;
+#pragma unroll
+    for (int xx = 0; xx < IW; ++xx) im[ky][xx] = row[xx] * a1 + b1;
+  }
+  float w[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) w[t] = cw[c * 9 + t];
+  const float bias = cb[c], a2 = bna[1 + c], b2 = bnb[1 + c];
+  unsigned rb = 0;
+#pragma unroll
+  for (int xx = 0; xx < FW; ++xx) {
+    float v = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) v += w[ky * 3 + kx] * im[ky][xx + kx];
+    v += bias;
+    v = v * a2 + b2;
+    rb |= (v > 0.f ? 1u : 0u) << xx;
+    mm[(size_t)i * NMID + c * 16 + yy * 8 + xx] = fmaxf(v, 0.f);
+  }
+  relu[(size_t)i * MASK_B + c * LR + MID_Y + yy] = (uint8_t)rb;
+}
+
+// per pair i (MPW per workgroup): dmap = [ReLU > 0] a2_c dmr[i] (dmr = dfc_i W_mid, from the
+// GEMM) through the transposed 3x3 convolution into lhs image rows 18-19 (times a1); the
+// pair's dl row [dp] gets that, plus, for the first pair of its kelpie row (psr[i] =
+// (kelpie row, first)), the row's shared part dls (map rows 0-17), zero elsewhere
+__global__ __launch_bounds__(256) void kp_cv_mid_convt(int M, const float* __restrict__ dmr,
+                                                       const uint8_t* __restrict__ relu, const float* __restrict__ cw,
+                                                       const float* __restrict__ bna, const int2* __restrict__ psr,
+                                                       const float* __restrict__ dls, int dp, float* __restrict__ dl) {
+  __shared__ float dm[MPW][NMID + 4];
+  __shared__ float img[MPW][2 * IW];
+  const int tid = threadIdx.x;
+  const int i0 = blockIdx.x * MPW;
+  if (i0 >= M) return;
+  for (int e = tid; e < MPW * NMID; e += 256) {
+    const int p = e / NMID, col = e % NMID, i = i0 + p;
+    const int ch = col >> 4, y = MID_Y + ((col >> 3) & 1), x = col & 7;
+    const bool on = i < M && ((relu[(size_t)i * MASK_B + ch * LR + y] >> x) & 1u);
+    dm[p][col] = on ? dmr[(size_t)i * NMID + col] * bna[1 + ch] : 0.f;
+  }
+  __syncthreads();
+  const float a1 = bna[0];
+  for (int e = tid; e < MPW * 2 * IW; e += 256) {
+    const int p = e / (2 * IW), r = e % (2 * IW), yi = MID_Y + r / IW, xx = r % IW;
+    float acc = 0.f;
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int y = yi - ky;
+        if (y < MID_Y || y > MID_Y + 1) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int x = xx - kx;
+          if (x >= 0 && x < FW) acc += dm[p][ch * 16 + (y - MID_Y) * 8 + x] * cw[ch * 9 + ky * 3 + kx];
+        }
+      }
+    img[p][r] = acc * a1;
+  }
+  __syncthreads();
+  for (int e = tid; e < MPW * dp; e += 256) {
+    const int p = e / dp, j = e % dp, i = i0 + p;
+    if (i >= M) continue;
+    float v = 0.f;
+    if (j >= MID_Y * IW && j < LR * IW) v = img[p][j - MID_Y * IW];
+    const int2 s = psr[i];
+    if (s.y && j < LR * IW) v += dls[(size_t)s.x * dp + j];
+    dl[(size_t)i * dp + j] = v;
+  }
+}
+
+// kelpie row k (src[k].x = -slot - 1): map rows 0-17 (BN1, conv, bias, BN2, ReLU; the
+// forward's tap order) -> map[k][l]; their ReLU sign bytes -> relu[k][20 ch + y]
+__global__ __launch_bounds__(256) void kp_cv_lhs_map(int n, const int2* __restrict__ src, const float* __restrict__ X,
+                                                     int dp, const float* __restrict__ cw, const float* __restrict__ cb,
+                                                     const float* __restrict__ bna, const float* __restrict__ bnb,
+                                                     float* __restrict__ map, uint8_t* __restrict__ relu) {
+  __shared__ float img[LR][IW];
+  const int k = blockIdx.x;
+  if (k >= n) return;
+  const float* x = X + (size_t)(-src[k].x - 1) * dp;
+  const float a1 = bna[0], b1 = bnb[0];
+  for (int e = threadIdx.x; e < LR * IW; e += blockDim.x) img[e / IW][e % IW] = x[e] * a1 + b1;
+  __syncthreads();
+  for (int e = threadIdx.x; e < CH * LHS_Y; e += blockDim.x) {
+    const int c = e / LHS_Y, y = e % LHS_Y;
+    float w[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) w[t] = cw[c * 9 + t];
+    const float bias = cb[c], a2 = bna[1 + c], b2 = bnb[1 + c];
+    unsigned rb = 0;
+#pragma unroll
+    for (int xx = 0; xx < FW; ++xx) {
+      float v = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) v += w[ky * 3 + kx] * img[y + ky][xx + kx];
+      v += bias;
+      v = v * a2 + b2;
+      rb |= (v > 0.f ? 1u : 0u) << xx;
+      map[(size_t)k * NLHS + c * 144 + y * FW + xx] = fmaxf(v, 0.f);
+    }
+    relu[(size_t)k * MASK_B + c * LR + y] = (uint8_t)rb;
+  }
+}
+
+// per kelpie row k: g[k] = the sum of its pairs' dfc (pairs [rng.x, rng.y) in order)
+__global__ void kp_cv_slot_g(int n, const int2* __restrict__ rng, const float* __restrict__ dfc, int dim,
+                             float* __restrict__ g) {
+  const int k = blockIdx.x;
+  if (k >= n) return;
+  const int2 r = rng[k];
+  for (int d = threadIdx.x; d < dim; d += blockDim.x) {
+    float v = 0.f;
+    for (int i = r.x; i < r.y; ++i) v += dfc[(size_t)i * dim + d];
+    g[(size_t)k * dim + d] = v;
+  }
+}
+
+// dls[k][j] (j = 10 y + x, lhs image rows 0-19) = a1 times the transposed 3x3 convolution
+// over map rows 0-17 (channels in order) of dmap = [ReLU > 0] a2_c dmr[k] (dmr = g_k W_lhs,
+// from the GEMM)
+__global__ __launch_bounds__(256) void kp_cv_lhs_convt(int n, const float* __restrict__ dmr,
+                                                       const uint8_t* __restrict__ relu, const float* __restrict__ cw,
+                                                       const float* __restrict__ bna, int dp, float* __restrict__ dls) {
+  __shared__ float dm[NLHS];
+  const int k = blockIdx.x;
+  if (k >= n) return;
+  for (int e = threadIdx.x; e < NLHS; e += blockDim.x) {
+    const int c = e / 144, rem = e % 144, y = rem >> 3, x = rem & 7;
+    const bool on = (relu[(size_t)k * MASK_B + c * LR + y] >> x) & 1u;
+    dm[e] = on ? dmr[(size_t)k * NLHS + e] * bna[1 + c] : 0.f;
+  }
+  __syncthreads();
+  const int j = threadIdx.x;
+  if (j >= LR * IW) return;
+  const int yi = j / IW, xi = j % IW;
+  float acc = 0.f;
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int y = yi - ky;
+      if (y < 0 || y >= LHS_Y) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int x = xi - kx;
+        if (x >= 0 && x < FW) acc += dm[c * 144 + y * FW + x] * cw[c * 9 + ky * 3 + kx];
+      }
+    }
+  dls[(size_t)k * dp + j] = acc * bna[0];
+}
+
+// out[i] = sum over nz slabs [nz][n][dim] (slab order)
+__global__ void kp_cv_slab_sum(int n, int nz, int dim, const float* __restrict__ slab, float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)n * dim) return;
+  float v = 0.f;
+  for (int z = 0; z < nz; ++z) v += slab[(size_t)z * n * dim + i];
+  out[i] = v;
 }
 
 }  // namespace kpcvf
