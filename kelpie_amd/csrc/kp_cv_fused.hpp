@@ -611,14 +611,22 @@ __global__ __launch_bounds__(256) void kp_cv_mid_convt(int M, const float* __res
                                                        const float* __restrict__ dls, int dp, float* __restrict__ dl) {
   __shared__ float dm[MPW][NMID + 4];
   __shared__ float img[MPW][2 * IW];
+  __shared__ uint8_t rbs[MPW][CH * 2];  // the pairs' ReLU bytes of rows 18-19
+  __shared__ float a2s[CH];
   const int tid = threadIdx.x;
   const int i0 = blockIdx.x * MPW;
   if (i0 >= M) return;
+  for (int e = tid; e < MPW * CH * 2; e += 256) {
+    const int p = e / (CH * 2), c = (e >> 1) % CH, yy = e & 1, i = i0 + p;
+    rbs[p][e % (CH * 2)] = i < M ? relu[(size_t)i * MASK_B + c * LR + MID_Y + yy] : 0;
+  }
+  if (tid < CH) a2s[tid] = bna[1 + tid];
+  __syncthreads();
   for (int e = tid; e < MPW * NMID; e += 256) {
     const int p = e / NMID, col = e % NMID, i = i0 + p;
-    const int ch = col >> 4, y = MID_Y + ((col >> 3) & 1), x = col & 7;
-    const bool on = i < M && ((relu[(size_t)i * MASK_B + ch * LR + y] >> x) & 1u);
-    dm[p][col] = on ? dmr[(size_t)i * NMID + col] * bna[1 + ch] : 0.f;
+    const int ch = col >> 4, yy = (col >> 3) & 1, x = col & 7;
+    const bool on = (rbs[p][2 * ch + yy] >> x) & 1u;
+    dm[p][col] = on ? dmr[(size_t)min(i, M - 1) * NMID + col] * a2s[ch] : 0.f;
   }
   __syncthreads();
   const float a1 = bna[0];
@@ -706,12 +714,17 @@ __global__ __launch_bounds__(256) void kp_cv_lhs_convt(int n, const float* __res
                                                        const uint8_t* __restrict__ relu, const float* __restrict__ cw,
                                                        const float* __restrict__ bna, int dp, float* __restrict__ dls) {
   __shared__ float dm[NLHS];
+  __shared__ uint8_t rbs[CH * LR];
+  __shared__ float a2s[CH];
   const int k = blockIdx.x;
   if (k >= n) return;
+  for (int e = threadIdx.x; e < CH * LR; e += blockDim.x) rbs[e] = relu[(size_t)k * MASK_B + e];
+  if (threadIdx.x < CH) a2s[threadIdx.x] = bna[1 + threadIdx.x];
+  __syncthreads();
   for (int e = threadIdx.x; e < NLHS; e += blockDim.x) {
     const int c = e / 144, rem = e % 144, y = rem >> 3, x = rem & 7;
-    const bool on = (relu[(size_t)k * MASK_B + c * LR + y] >> x) & 1u;
-    dm[e] = on ? dmr[(size_t)k * NLHS + e] * bna[1 + c] : 0.f;
+    const bool on = (rbs[c * LR + y] >> x) & 1u;
+    dm[e] = on ? dmr[(size_t)k * NLHS + e] * a2s[c] : 0.f;
   }
   __syncthreads();
   const int j = threadIdx.x;

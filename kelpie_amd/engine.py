@@ -602,7 +602,14 @@ class PostTrainingEngine(RelevanceEngine):
         # The scheduling thread and the batch threads' packing share the interpreter lock;
         # KELPIE_GIL_SWITCH_US shortens the interpreter's switch interval while the
         # pipeline runs (A/B switch; unset: the interpreter's default)
+        import gc
         import sys
+        # KELPIE_PIPELINE_NOGC=1 (A/B): no cyclic garbage collection while batches are in
+        # flight; a collection pass on the scheduling thread
+        # holds the interpreter lock for milliseconds, long enough to leave the device idle
+        nogc = os.environ.get("KELPIE_PIPELINE_NOGC") == "1" and gc.isenabled()
+        if nogc:
+            gc.disable()
         old_switch = sys.getswitchinterval()
         if os.environ.get("KELPIE_GIL_SWITCH_US"):
             sys.setswitchinterval(float(os.environ["KELPIE_GIL_SWITCH_US"]) * 1e-6)
@@ -654,6 +661,8 @@ class PostTrainingEngine(RelevanceEngine):
             for st in inflight:  # an earlier batch raised: let the others' device work end
                 st["thread"].join()
             sys.setswitchinterval(old_switch)
+            if nogc:
+                gc.enable()
         self.last_batch_stats = stats
         return outs
 

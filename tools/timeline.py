@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--kernel", default="kp_attn3<25, 0>")
     ap.add_argument("--window", type=float, default=0.4, help="seconds at the end of the trace")
     ap.add_argument("--skip-end", type=float, default=0.0, help="seconds cut off the end (the pipeline's drain)")
+    ap.add_argument("--gaps", action="store_true", help="list the idle gaps over 1 ms with the kernels around them")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end from kernels").fetchall()
@@ -75,6 +76,13 @@ def main():
     for lo, hi in ((0, 1e4), (1e4, 1e5), (1e5, 1e6), (1e6, 1e12)):
         g = [x for x in gaps if lo <= x < hi]
         print(f"  idle gaps {lo / 1e3:g}-{hi / 1e3:g} us: {len(g)} gaps, {sum(g) / span:.3f} of the window")
+    if a.gaps:
+        for a_, b in zip(busy, busy[1:]):
+            if b[0] - a_[1] >= 1e6:
+                before = [n for n, s, e in rows if abs(e - a_[1]) < 1e3]
+                after = [n for n, s, e in rows if abs(s - b[0]) < 1e3]
+                print(f"  gap {(b[0] - a_[1]) / 1e3:8.1f} us at {(a_[1] - t0) / 1e6:7.2f} ms: after "
+                      f"{[short_name(n)[:40] for n in before]} before {[short_name(n)[:40] for n in after]}")
     per = defaultdict(list)
     for n, s, e in rows:
         per[short_name(n)].append((s, e))
