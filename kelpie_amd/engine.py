@@ -623,6 +623,7 @@ class PostTrainingEngine(RelevanceEngine):
                 state["error"] = e
 
         outs, stats, inflight = [], [], collections.deque()
+        late_collect = os.environ.get("KELPIE_PIPELINE_EARLY_START", "1") == "0"  # A/B: collect, then start
 
         def finish(state):
             state["thread"].join()
@@ -647,14 +648,26 @@ class PostTrainingEngine(RelevanceEngine):
                     slots, pending, jobs = self._schedule_all(items, None)
                 err, self._deferred_error = self._deferred_error, None
                 t_sched = time.perf_counter() - t0
-                # batch b uses context b % depth: the batch before it on that context is done
+                # batch b uses context b % depth: the batch before it on that context is done.
+                # Its device work is waited for first and batch b started on the freed context,
+                # then its results are collected: the collection (and the gather, sharded) runs
+                # while batch b packs and launches instead of ahead of it
+                done = []
                 while len(inflight) >= len(ctxs):
-                    finish(inflight.popleft())
+                    old = inflight.popleft()
+                    old["thread"].join()
+                    done.append(old)
+                if late_collect or any(d.get("error") is not None for d in done):
+                    for d in done:
+                        finish(d)  # raises the first device failure before batch b starts
+                    done = []
                 state = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched, "error": None,
                          "deferred": err, "ctx": ctxs[b % len(ctxs)]}
                 state["thread"] = threading.Thread(target=run, args=(state,), daemon=True)
                 state["thread"].start()
                 inflight.append(state)
+                for d in done:
+                    finish(d)
                 if err is not None:
                     break  # the sequential reference stops at the failing call
             while inflight:

@@ -14,6 +14,12 @@ test time from the seed and checked by sha256.  The preds file is copied as data
 
     python tests/golden/make_dbpedia50_golden.py
 writes tests/golden/dbpedia50_transe.json (+ dbpedia50_preds.tsv)
+
+    python tests/golden/make_dbpedia50_golden.py --fp64
+runs the same pipeline with the reference model in float64 (``tools/conditioning.py``'s
+patches: the random draws made in float32 as the fp32 run makes them, then widened) and
+writes tests/golden/dbpedia50_transe_fp64.json: the second reference variant of the
+element-wise rule (tests/test_dbpedia50.py).
 """
 from __future__ import annotations
 
@@ -40,6 +46,7 @@ SEED = 2024
 
 
 def main():
+    fp64 = "--fp64" in sys.argv[1:]
     src = ref_harness.load_reference()
     ref = ref_harness.REF_ROOT
     ds = Dataset.from_directory(os.path.join(ref, "data", "DBpedia50"))
@@ -60,6 +67,11 @@ def main():
     from src.explain import build_pipeline
     from src.link_prediction import MODEL_REGISTRY
     torch.set_num_threads(8)
+    patches = None
+    if fp64:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from conditioning import _Patches, to_double
+        patches = _Patches(fp64=True, dim=cfg["model_params"]["dimension"]).__enter__()
     ref_harness.seed_all(42)  # explain.py:144
     dataset = RefDataset("DBpedia50_real")
     assert dataset.num_entities == ds.num_entities and len(dataset.training_triples) == len(ds.training_triples)
@@ -69,6 +81,8 @@ def main():
         model.entity_embeddings.data = torch.from_numpy(w["entity_embeddings"].copy())
         model.relation_embeddings.data = torch.from_numpy(w["relation_embeddings"].copy())
     model.eval()
+    if fp64:
+        to_double(model)
     pipeline = build_pipeline(model, dataset, cfg["training"], "necessary", None, None, None, None)
     out, per_pred = [], []
     t_all = time.time()
@@ -78,6 +92,12 @@ def main():
         per_pred.append(time.time() - t0)
         out.append(json.loads(json.dumps(ex, default=lambda x: x.item() if hasattr(x, "item") else list(x))))
         print(pred, ex["#relevances"], f"{per_pred[-1]:.1f}s", flush=True)
+    if fp64:
+        patches.__exit__(None, None, None)
+        with open(os.path.join(HERE, "dbpedia50_transe_fp64.json"), "w") as f:
+            json.dump({"variant": "reference in float64 (tools/conditioning.py patches)", "weights_seed": SEED,
+                       "weights_sha256": sha, "explanations": out, "reference_seconds": time.time() - t_all}, f)
+        return
     rec = {"config": "BASELINE.json configs[0]: TransE DBpedia50 necessary-mode, 10 predictions",
            "dataset": "reference data/DBpedia50 (train/valid/test.txt), ids: sorted training labels",
            "num_entities": ds.num_entities, "num_relations": ds.num_relations,

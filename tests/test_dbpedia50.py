@@ -23,6 +23,9 @@ from kelpie_amd.pipeline import read_preds, run_explain
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 GOLD_PATH = os.path.join(HERE, "dbpedia50_transe.json")
+# the same reference pipeline run in float64 (make_dbpedia50_golden.py --fp64): the second
+# variant of the element-wise rule of tests/test_fullsize_reference.py
+GOLD64_PATH = os.path.join(HERE, "dbpedia50_transe_fp64.json")
 DATA = os.path.join(HERE, "dbpedia50")
 pytestmark = pytest.mark.skipif(not os.path.exists(GOLD_PATH), reason="DBpedia50 golden not generated")
 
@@ -77,14 +80,26 @@ def _run(backend, tmpdir, n_preds):
     with open(out_path) as f:
         got = json.load(f)
     assert len(got) == n_preds
-    for g, e in zip(got, rec["explanations"][:n_preds]):
+    ex64 = [None] * n_preds
+    if os.path.exists(GOLD64_PATH):
+        with open(GOLD64_PATH) as f:
+            ex64 = json.load(f)["explanations"][:n_preds]
+    for g, e, e64 in zip(got, rec["explanations"][:n_preds], ex64):
         assert set(g) == {"triple", "rule_to_relevance", "#relevances", "execution_time"}
         assert list(g["triple"]) == list(e["triple"])
         assert g["#relevances"] == e["#relevances"], (g["triple"], g["#relevances"], e["#relevances"])
         assert len(g["rule_to_relevance"]) == len(e["rule_to_relevance"])
+        rel64 = {json.dumps(r): v for r, v in e64["rule_to_relevance"]} if e64 else {}
         for (rule, rel), (erule, erel) in zip(g["rule_to_relevance"], e["rule_to_relevance"]):
             assert [list(t) for t in rule] == [list(t) for t in erule]
-            assert abs(rel - erel) <= TOL * max(1.0, abs(erel)), (rule, rel, erel)
+            tol = TOL * max(1.0, abs(erel))
+            if abs(rel - erel) <= tol:
+                continue
+            # element-wise rule: where the reference's float32 and float64 runs disagree (a
+            # near-tie the ranks resolve differently), the engine may lie anywhere between them
+            v64 = rel64.get(json.dumps(erule))
+            assert v64 is not None and abs(v64 - erel) > tol, (rule, rel, erel, v64)
+            assert min(erel, v64) - tol <= rel <= max(erel, v64) + tol, (rule, rel, erel, v64)
 
 
 def test_dbpedia50_pipeline_host_protocol(tmp_path):
