@@ -24,6 +24,9 @@
 //   the batch, so every epoch reuses one plan; otherwise each (epoch, step)
 //   gets its own plan from the permutation.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <unordered_map>
 
@@ -449,7 +452,15 @@ int cx_pick_db(int dim) {
   return -1;
 }
 
+// KP_HOST_TIMES=1 (diagnostic): per call, on stderr, the host time before the first upload
+// (checks and planning), up to the last launch enqueued, and waiting for the device
+static const bool g_host_times = std::getenv("KP_HOST_TIMES") != nullptr;
+static double host_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
+  const double t_in = g_host_times ? host_ms() : 0.0;
   const int DBV = c->dp / 16;
   const int K = c->n_ent;  // kelpie id
   const int ns = bt->n_slots;
@@ -617,6 +628,7 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   t_off[T] = (int)stept.size();
 
   const int DP = c->dp;
+  const double t_plan = g_host_times ? host_ms() : 0.0;
   // ---- uploads
   float* dX = nullptr;
   {
@@ -754,7 +766,11 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   }
   KP_HIP(hipMemcpyAsync(bt->out_score, dTarget, sizeof(float) * ns, hipMemcpyDeviceToHost, c->stream));
   KP_HIP(hipMemcpyAsync(bt->out_rank, dRank, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, c->stream));
+  const double t_enq = g_host_times ? host_ms() : 0.0;
   KP_HIP(hipStreamSynchronize(c->stream));
+  if (g_host_times)
+    std::fprintf(stderr, "[kp_cx] slots %d steps %d: plan %.2f ms, enqueue %.2f ms, wait %.2f ms\n", ns, T,
+                 t_plan - t_in, t_enq - t_plan, host_ms() - t_enq);
   float ms_all = 0.f, ms_loop = 0.f;
   KP_HIP(hipEventElapsedTime(&ms_all, c->ev0, c->ev1));
   KP_HIP(hipEventElapsedTime(&ms_loop, h0, h1));
