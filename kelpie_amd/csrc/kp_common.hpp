@@ -120,7 +120,7 @@ struct kp_ctx {
   DevBuf cv_wtl, cv_wfm;    // the kelpie rows' FC columns and the mid columns, transposed (built once)
   DevBuf cv_wlc;            // the kelpie rows' FC columns [dim][4608] (built once)
   bool cv_shared_ready = false;
-  DevBuf cvs[10];           // its per-batch workspaces (kp_conve.hip)
+  DevBuf cvs[12];           // per-batch ConvE workspaces (kp_conve.hip)
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
   kp_cv_train* cvtrain = nullptr;   // kp_conve_train_*'s state (freed with the context)

@@ -655,6 +655,20 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float* dQpair = reinterpret_cast<float*>(c->ws[11].ensure(sizeof(float) * (size_t)std::max(npairs, 1) * DP));
   float* dLsef = reinterpret_cast<float*>(c->ws[12].ensure(sizeof(float) * (size_t)std::max(npairs, 1)));
 
+  // the ranking's inputs and buffers now, ahead of the step loop: an upload from pageable
+  // memory after the loop waited for the whole loop on the device, so the rank kernels
+  // were enqueued only then (a host round trip per batch with the context idle)
+  double* dQ64 = reinterpret_cast<double*>(c->ws[29].ensure(sizeof(double) * (size_t)ns * DP));
+  double* dT64 = reinterpret_cast<double*>(c->ws[30].ensure(sizeof(double) * 2 * (size_t)ns));
+  int32_t* dPred = upload(c, c->ws[18], bt->pred, (size_t)ns * 3);
+  std::vector<int32_t> po(ns);
+  for (int s = 0; s < ns; ++s) po[s] = bt->pred[3 * s + 2];
+  int32_t* dPo = upload(c, c->ws[19], po.data(), po.size());
+  int32_t* dFo = upload(c, c->ws[20], bt->filt_off, (size_t)ns + 1);
+  int32_t* dF = upload(c, c->ws[21], bt->filt, (size_t)bt->filt_off[ns]);
+  float* dTarget = reinterpret_cast<float*>(c->ws[22].ensure(sizeof(float) * (size_t)ns));
+  int64_t* dRank = reinterpret_cast<int64_t*>(c->ws[23].ensure(sizeof(int64_t) * (size_t)ns));
+
   const int half = c->dim / 2;
   KP_HIP(hipEventRecord(c->ev0, c->stream));
   if (npq > 0) {
@@ -710,6 +724,8 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   KP_HIP(hipEventCreate(&lev.b));
   hipEvent_t h0 = lev.a, h1 = lev.b;
   KP_HIP(hipEventRecord(h0, c->stream));
+  const double t_loop0 = g_host_times ? host_ms() : 0.0;
+  double t_steps[4] = {0, 0, 0, 0};  // host time after enqueueing steps 0, 1, T/2, T-1
   int64_t hot_launches = 0;
   c->hot_pairs.clear();
   c->hot_iv.clear();
@@ -738,21 +754,17 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     CX_DISPATCH(DBV, launch_update<DB>(c, na, dActs + act_off[t], dPlans, dPq, dStepQ + q_off[t], nq,
                                        dStepT + t_off[t], t_off[t + 1] - t_off[t], dTsum, dQpair, dLsef, dAm, dAl, dAO,
                                        sp, dContrib, dX, dS1, dS2, opt));
+    if (g_host_times) {
+      if (t == 0) t_steps[0] = host_ms();
+      if (t == 1) t_steps[1] = host_ms();
+      if (t == T / 2) t_steps[2] = host_ms();
+      if (t == T - 1) t_steps[3] = host_ms();
+    }
   }
   KP_HIP(hipEventRecord(h1, c->stream));
 
   // ---- ranking: scores of (kelpie, p, .) over E plus the kelpie column, in fp64
   // (launch_rank_f64: at the reference init the target's neighbours are ~1e-5 relative away)
-  double* dQ64 = reinterpret_cast<double*>(c->ws[29].ensure(sizeof(double) * (size_t)ns * DP));
-  double* dT64 = reinterpret_cast<double*>(c->ws[30].ensure(sizeof(double) * 2 * (size_t)ns));
-  int32_t* dPred = upload(c, c->ws[18], bt->pred, (size_t)ns * 3);
-  std::vector<int32_t> po(ns);
-  for (int s = 0; s < ns; ++s) po[s] = bt->pred[3 * s + 2];
-  int32_t* dPo = upload(c, c->ws[19], po.data(), po.size());
-  int32_t* dFo = upload(c, c->ws[20], bt->filt_off, (size_t)ns + 1);
-  int32_t* dF = upload(c, c->ws[21], bt->filt, (size_t)bt->filt_off[ns]);
-  float* dTarget = reinterpret_cast<float*>(c->ws[22].ensure(sizeof(float) * (size_t)ns));
-  int64_t* dRank = reinterpret_cast<int64_t*>(c->ws[23].ensure(sizeof(int64_t) * (size_t)ns));
   CX_DISPATCH(DBV, launch_rankq64<DB>(c, dX, dPred, ns, dQ64, dT64, dT64 + ns));
   launch_rank_f64(c, ns, dQ64, dT64, dT64 + ns, dPo, dFo, dF, dTarget, dRank);
   KP_HIP(hipEventRecord(c->ev1, c->stream));
@@ -769,8 +781,11 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   const double t_enq = g_host_times ? host_ms() : 0.0;
   KP_HIP(hipStreamSynchronize(c->stream));
   if (g_host_times)
-    std::fprintf(stderr, "[kp_cx] slots %d steps %d: plan %.2f ms, enqueue %.2f ms, wait %.2f ms\n", ns, T,
-                 t_plan - t_in, t_enq - t_plan, host_ms() - t_enq);
+    std::fprintf(stderr,
+                 "[kp_cx] slots %d steps %d: plan %.2f ms, enqueue %.2f ms (uploads+pairs %.2f, step 0 %.2f, step 1 "
+                 "%.2f, to T/2 %.2f, to T-1 %.2f), wait %.2f ms\n",
+                 ns, T, t_plan - t_in, t_enq - t_plan, t_loop0 - t_plan, t_steps[0] - t_loop0, t_steps[1] - t_steps[0],
+                 t_steps[2] - t_steps[1], t_steps[3] - t_steps[2], host_ms() - t_enq);
   float ms_all = 0.f, ms_loop = 0.f;
   KP_HIP(hipEventElapsedTime(&ms_all, c->ev0, c->ev1));
   KP_HIP(hipEventElapsedTime(&ms_loop, h0, h1));

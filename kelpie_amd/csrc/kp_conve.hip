@@ -875,7 +875,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   const int n_dl = fused ? kpcvf::NSPLIT : 1;  // lhs image-gradient slabs per pair (kp_cv_bwd_fused, reduced in slab 0)
   float* dQ = reinterpret_cast<float*>(c->ws[14].ensure(sizeof(float) * (size_t)me * DP));
   int2* dSrc = upload(c, c->ws[15], enc_src.data(), std::max<size_t>(1, enc_src.size()));
-  int4* dFch = upload(c, c->ws[28], fchunks.data(), std::max<size_t>(1, fchunks.size()));
+  int4* dFch = upload(c, c->cvs[10], fchunks.data(), std::max<size_t>(1, fchunks.size()));
   float* dFpart = reinterpret_cast<float*>(c->ws[31].ensure(sizeof(float) * (size_t)std::max(1, max_fch) * c->dim));
   CvBits* dEncBits = upload(c, c->ws[26], enc_bits.data(), std::max<size_t>(1, enc_bits.size()));
   float* dgs = reinterpret_cast<float*>(c->ws[16].ensure(sizeof(float) * (size_t)std::max<size_t>(1, kinst.size())));
