@@ -78,7 +78,7 @@ WORKLOADS = {
                                       cpu_conversions=2, depth=3),
     # BASELINE.json configs[4]
     "conve-yago310-necessary": dict(model="ConvE", shape="YAGO3-10", dim=200, mode="necessary", hp=CONVE_HP,
-                                    candidates=20, preds_per_step=8, hidden_dropout=0.2),
+                                    candidates=20, preds_per_step=8, hidden_dropout=0.2, depth=3),
 }
 
 
@@ -363,8 +363,10 @@ def main():
     # step k+1's reference-order draws on the host while step k runs on the GPU.
     # batches in flight (one device context each): 3 for the sufficient workloads, whose
     # small batches leave the device idle during a batch's planning and download
-    # (default 588 -> 649 cand/s, profiles/r02v_depth.txt), 2 for the others (a third
-    # context costs the necessary workload 10 %)
+    # (default 588 -> 649 cand/s, profiles/r02v_depth.txt), and for ConvE, whose batch
+    # boundaries (host planning of ~100 steps x 3,456 pair records, uploads) left the
+    # device idle ~70 ms with two (433 / 436 -> 450 / 448 cand/s, profiles/r04x/); 2 for
+    # the others (a third context costs the ComplEx necessary workload 10 %)
     depth = int(os.environ.get("KELPIE_PIPELINE_DEPTH", wl.get("depth", 2)))
     if args.warmup:
         eng.compute_relevance_pipeline([items_of(jobs[i]) for i in range(args.warmup)], depth=depth)
