@@ -21,6 +21,8 @@
 //   kelpie-column corrections and the encoder backward (kp_cv_dx, FC^T GEMM,
 //   kp_cv_conv_bwd) -> kp_cv_update (+ the kelpie-column gradient of every pair;
 //   pairs with a frozen head reuse their precomputed FC output) -> Adam.
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <unordered_map>
 
@@ -577,7 +579,15 @@ static void conve_fused_images(kp_ctx* c, const __bf16** fw, const __bf16** bw) 
 
 void conve_encode_dev(kp_ctx* c, int n, const int2* d_src, float* d_out) { encode_eval(c, n, d_src, nullptr, d_out); }
 
+// KP_HOST_TIMES=1 (diagnostic): per call, on stderr, the host time of the planning, the
+// uploads, enqueueing the step loop, and the rank with the final wait
+static const bool g_cv_host_times = std::getenv("KP_HOST_TIMES") != nullptr;
+static double cv_host_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
+  const double t_in = g_cv_host_times ? cv_host_ms() : 0.0;
   const int ns = bt->n_slots;
   const int K = c->n_ent;
   const int DP = c->dp;
@@ -590,6 +600,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   struct Pair {
     int h, r;
     std::vector<int> tails;
+    int tail_begin = -1, tail_count = 0;  // kelpie pair: its distinct tails in `tails`; frozen: its FC row
   };
   std::vector<int2> fpairs;                // frozen (h, r) -> fc precompute
   std::unordered_map<long long, int> fp_id;
@@ -687,7 +698,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       const int nb = plan[s].nb;
       if (nb == 0 || t >= E_ * nb) continue;
       const int j = t % nb;
-      const auto& P = plan[s].pairs;
+      auto& P = plan[s].pairs;
       const int p0 = j * hp->batch_size, p1 = std::min((int)P.size(), p0 + hp->batch_size);
       const int b = p1 - p0;
       CvAct A{};
@@ -696,7 +707,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       A.f_begin = (int)finst.size() - fin_off[t];
       int my_sr = -1;
       for (int q = p0; q < p1; ++q) {
-        const auto& pr = P[q];
+        auto& pr = P[q];
         if (pr.h == K) {
           const bool first = my_sr < 0;
           if (first) {
@@ -710,18 +721,21 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
           I.b = b;
           I.pos = q - p0;
           I.mb = pair_bits(moff[s][t], I.pos);
-          I.tail_begin = (int)tails.size();
-          std::vector<int> uniq;
-          for (int tt : pr.tails)
-            if (std::find(uniq.begin(), uniq.end(), tt) == uniq.end()) uniq.push_back(tt);
-          tails.insert(tails.end(), uniq.begin(), uniq.end());
-          I.tail_count = (int)uniq.size();
+          if (pr.tail_begin < 0) {  // the pair's distinct tails, stored once for every step
+            pr.tail_begin = (int)tails.size();
+            for (int tt : pr.tails)
+              if (std::find(tails.begin() + pr.tail_begin, tails.end(), tt) == tails.end()) tails.push_back(tt);
+            pr.tail_count = (int)tails.size() - pr.tail_begin;
+          }
+          I.tail_begin = pr.tail_begin;
+          I.tail_count = pr.tail_count;
           kinst.push_back(I);
           ++local_k;
         } else {
           CvFInst F{};
           F.slot = s;
-          F.fp = kc.fr_step ? (int)finst.size() - fin_off[t] : fp_id.at((long long)pr.h * c->n_rel2 + pr.r);
+          if (!kc.fr_step && pr.tail_begin < 0) pr.tail_begin = fp_id.at((long long)pr.h * c->n_rel2 + pr.r);
+          F.fp = kc.fr_step ? (int)finst.size() - fin_off[t] : pr.tail_begin;  // (frozen pair: its FC row)
           F.b = b;
           F.pos = q - p0;
           F.mb = pair_bits(moff[s][t], F.pos);
@@ -760,6 +774,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   fin_off[T] = (int)finst.size();
   act_o[T] = (int)acts.size();
 
+  const double t_plan = g_cv_host_times ? cv_host_ms() : 0.0;
   // ---------------- uploads
   std::vector<float> xp((size_t)ns * DP, 0.f);
   for (int s = 0; s < ns; ++s) std::memcpy(&xp[(size_t)s * DP], bt->x0 + (size_t)s * c->dim, sizeof(float) * c->dim);
@@ -781,6 +796,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   KP_HIP(hipMemsetAsync(dBits + nbits, 0, 2 * sizeof(int32_t), c->stream));
   const int nfp = kc.fr_step ? 0 : (int)fpairs.size();
 
+  const double t_up = g_cv_host_times ? cv_host_ms() : 0.0;
   KP_HIP(hipEventRecord(c->ev0, c->stream));
   // frozen-head pairs without an input / feature-map dropout: FC output (pre-dropout)
   // once per batch
@@ -1069,6 +1085,7 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     }
   }
 
+  const double t_loop = g_cv_host_times ? cv_host_ms() : 0.0;
   // ---------------- rank: sigmoid(enc(x, R_p) . E_e), kelpie column, maximizer
   std::vector<int2> rsrc(ns);
   std::vector<int32_t> po(ns);
@@ -1108,6 +1125,10 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   KP_HIP(hipMemcpyAsync(bt->out_score, dTarget, sizeof(float) * ns, hipMemcpyDeviceToHost, c->stream));
   KP_HIP(hipMemcpyAsync(bt->out_rank, dRank, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
+  if (g_cv_host_times)
+    std::fprintf(stderr, "[kp_cv] slots %d steps %d pairs %zu: plan %.2f ms, uploads %.2f ms, loop enqueue %.2f ms, "
+                 "rank + wait %.2f ms\n", ns, T, kinst.size(), t_plan - t_in, t_up - t_plan, t_loop - t_up,
+                 cv_host_ms() - t_loop);
   if (bt->out_x)
     for (int s = 0; s < ns; ++s) std::memcpy(bt->out_x + (size_t)s * c->dim, &xp[(size_t)s * DP], sizeof(float) * c->dim);
   float ms_all = 0.f;
