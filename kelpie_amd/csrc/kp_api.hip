@@ -161,6 +161,8 @@ int kp_ctx_destroy(kp_ctx* c) {
   c->eT.release();
   c->cvf_fw3.release();
   c->cvf_bw3.release();
+  for (DevBuf* b : {&c->cv_wtm, &c->cv_trel, &c->cv_wtl, &c->cv_wfm, &c->cv_wlc}) b->release();
+  for (auto& b : c->cvs) b.release();
   train_state_free(c);
   cv_train_free(c);
   for (auto e : c->evpool) (void)hipEventDestroy(e);

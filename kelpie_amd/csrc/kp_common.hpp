@@ -36,14 +36,18 @@ struct KpError {
     if (!(cond)) throw KpError{KP_EINVAL, (msg)};     \
   } while (0)
 
-// grow-only device buffer
+// grow-only device buffer.  A grown buffer's old allocation is kept until release()
+// (the context's teardown) instead of freed at once: hipFree waits for the whole device,
+// every context's queued work included, so a mid-run free stalled the batch thread that
+// grew the buffer behind the other batches in flight
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  std::vector<void*> old;
   void* ensure(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes > cap) {
-      if (p) (void)hipFree(p);
+      if (p) old.push_back(p);
       p = nullptr;
       size_t want = bytes + bytes / 4;
       KP_HIP(hipMalloc(&p, want));
@@ -55,6 +59,8 @@ struct DevBuf {
   T* as() { return reinterpret_cast<T*>(p); }
   void release() {
     if (p) (void)hipFree(p);
+    for (void* q : old) (void)hipFree(q);
+    old.clear();
     p = nullptr;
     cap = 0;
   }
@@ -120,7 +126,7 @@ struct kp_ctx {
   DevBuf cv_wtl, cv_wfm;    // the kelpie rows' FC columns and the mid columns, transposed (built once)
   DevBuf cv_wlc;            // the kelpie rows' FC columns [dim][4608] (built once)
   bool cv_shared_ready = false;
-  DevBuf cvs[12];           // per-batch ConvE workspaces (kp_conve.hip)
+  DevBuf cvs[14];           // per-batch ConvE workspaces (kp_conve.hip)
   int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
   kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
   kp_cv_train* cvtrain = nullptr;   // kp_conve_train_*'s state (freed with the context)

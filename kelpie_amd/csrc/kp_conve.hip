@@ -1101,10 +1101,10 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   encode_eval(c, ns, dRsrc, dX, dQr);
   int32_t* dPo = upload(c, c->ws[22], po.data(), po.size());
   int32_t* dFo = upload(c, c->ws[23], bt->filt_off, (size_t)ns + 1);
-  DevBuf bF, bT, bR;
-  int32_t* dF = upload(c, bF, bt->filt, (size_t)std::max(1, bt->filt_off[ns]));
-  float* dTarget = reinterpret_cast<float*>(bT.ensure(sizeof(float) * ns));
-  int64_t* dRank = reinterpret_cast<int64_t*>(bR.ensure(sizeof(int64_t) * ns));
+  // context buffers (a per-call buffer's hipFree waits for the whole device, every context)
+  int32_t* dF = upload(c, c->cvs[11], bt->filt, (size_t)std::max(1, bt->filt_off[ns]));
+  float* dTarget = reinterpret_cast<float*>(c->cvs[12].ensure(sizeof(float) * ns));
+  int64_t* dRank = reinterpret_cast<int64_t*>(c->cvs[13].ensure(sizeof(int64_t) * ns));
   if (c->cv_rank64) {
     double* dQ64 = reinterpret_cast<double*>(c->ws[29].ensure(sizeof(double) * (size_t)ns * DP));
     double* dT64 = reinterpret_cast<double*>(c->ws[30].ensure(sizeof(double) * 2 * (size_t)ns));
@@ -1140,7 +1140,6 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     kp_push_interval(c, c->event(2 * i), c->event(2 * i + 1));
     work += c->hot_pairs[i].first * (double)K;
   }
-  for (DevBuf* b : {&bF, &bT, &bR}) b->release();
   c->timing.device_s = ms_all * 1e-3;
   c->timing.loop_s = ms_all * 1e-3;
   c->timing.hot_s = hot;
