@@ -11,7 +11,7 @@ LIB := kelpie_amd/libkelpie_hip.so
 
 all: $(LIB)
 
-build/%.o: kelpie_amd/csrc/%.hip kelpie_amd/csrc/kp_common.hpp kelpie_amd/csrc/kp_attn.hpp kelpie_amd/csrc/kp_attn3.hpp kelpie_amd/csrc/kp_cv_fused.hpp kelpie_amd/csrc/kp_attn5.hpp include/kelpie_hip.h
+build/%.o: kelpie_amd/csrc/%.hip kelpie_amd/csrc/kp_common.hpp kelpie_amd/csrc/kp_attn.hpp kelpie_amd/csrc/kp_attn3.hpp kelpie_amd/csrc/kp_cv_fused.hpp include/kelpie_hip.h
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) -c $< -o $@
 
@@ -51,7 +51,7 @@ clean:
 # host sanitizer builds of the library's host C++ (kp_rng.cpp worker pool / arenas,
 # kp_graph.cpp) linked into tests/native/host_san_driver.cpp; run by
 # tests/test_host_sanitizers.py (CPU suite), or by hand: make asan tsan
-SAN_SRC := kelpie_amd/csrc/kp_rng.cpp kelpie_amd/csrc/kp_graph.cpp tests/native/host_san_driver.cpp
+SAN_SRC := kelpie_amd/csrc/kp_rng.cpp kelpie_amd/csrc/kp_graph.cpp kelpie_amd/csrc/kp_sched.cpp tests/native/host_san_driver.cpp
 SAN_FLAGS := -O1 -g -std=c++17 -fno-omit-frame-pointer -mavx2 -mfma -ffp-contract=off -pthread -Iinclude
 asan: build/san/host_asan
 tsan: build/san/host_tsan

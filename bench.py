@@ -82,25 +82,34 @@ WORKLOADS = {
 }
 
 
-def committed_traffic(workload, kernel):
-    """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 FETCH_SIZE
-    pass of this workload (profiles/rNN_<workload>_pmc.json, tools/prof_summary.py).
-    PMC counters cannot be read from inside the timed run, so the bench line cites them."""
+def committed_counters(workload, kernel):
+    """HBM bytes (FETCH_SIZE + WRITE_SIZE) and SQ counters per launch of ``kernel`` from the
+    newest committed rocprofv3 pass of this workload (profiles/rNN_<workload>_pmc.json,
+    tools/prof_summary.py) -- only a pass stamped with the library sources this run
+    executes (``library_source_sha16``): a pass of an older kernel is never cited, the
+    line then says traffic null.  PMC counters cannot be read inside the timed run."""
     import glob
     import json
     import re
+    from kelpie_amd._lib import source_sha16
     here = os.path.dirname(os.path.abspath(__file__))
     m = re.match(r"(kp_attn3?)<(\d+),(\w+)>", kernel)
     want = f"{m.group(1)}<{m.group(2)}, {ATT_MODES[m.group(3)]}>" if m else kernel
-    # newest first; a kernel-trace-only summary (no FETCH_SIZE pass) carries no bytes, so
-    # fall through to the newest file that does
+    sha = source_sha16()
     for path in sorted(glob.glob(os.path.join(here, "profiles", f"r*_{workload}_pmc.json")), reverse=True):
         with open(path) as f:
-            d = json.load(f).get("fetch_bytes_per_launch") or {}
-        for name, v in d.items():
+            d = json.load(f)
+        if d.get("library_source_sha16") != sha:
+            continue
+        fetch = d.get("fetch_bytes_per_launch") or {}
+        for name, v in fetch.items():
             if want in name and v.get("hbm_bytes"):
-                return v["hbm_bytes"], os.path.relpath(path, here)
-    return None, None
+                w = next((x["hbm_bytes"] for n2, x in (d.get("write_bytes_per_launch") or {}).items() if n2 == name),
+                         None)
+                sq = next((x for n2, x in (d.get("sq_per_launch") or {}).items() if want in n2), None)
+                return {"read": v["hbm_bytes"], "write": w, "sq": sq, "source": os.path.relpath(path, here)}
+    return {"read": None, "write": None, "sq": None, "source": None,
+            "note": f"no committed counter pass of library sources {sha}"}
 
 
 ATT_MODES = {"ATT_SOFTMAX_O": 0, "ATT_SOFTMAX": 1, "ATT_BCE_O": 2}
@@ -431,7 +440,17 @@ def main():
                 "frac": (achieved / peak) if achieved else None, "traffic": None, "kernel": kname,
                 "peak_basis": ("dense bf16 MFMA peak / 6 (six bf16 products per fp32 product)"
                                if peak != 157.3 else "dense fp32 MFMA peak")}
-    roof["traffic"], roof["traffic_source"] = committed_traffic(args.workload, roof["kernel"])
+    cc = committed_counters(args.workload, roof["kernel"])
+    roof["traffic"] = (cc["read"] + (cc["write"] or 0.0)) if cc["read"] else None
+    roof["traffic_read"], roof["traffic_write"] = cc["read"], cc["write"]
+    roof["traffic_source"] = cc["source"] or cc.get("note")
+    if wl["model"] == "TransE" and cc["sq"] and cc["sq"].get("SQ_INSTS_VALU") and hot[2] and hot_union > 0:
+        # its actual bound: VALU issue, one wave64 instruction per 2 cycles per SIMD
+        # (MI355X_MICROARCH.md constants), 1,024 SIMDs at 2.4 GHz
+        ach = cc["sq"]["SQ_INSTS_VALU"] / (hot_union / hot[2])
+        pk = 1024 * 2.4e9 / 2.0
+        roof["valu"] = {"achieved": ach, "peak": pk, "unit": "wave64 VALU instructions/s", "frac": ach / pk,
+                        "source": cc["source"]}
     roof["launches"] = hot[2]
     # per-launch durations (what rocprofv3 --kernel-trace reports); with two batches
     # in flight they include waiting for the other batch's workgroups

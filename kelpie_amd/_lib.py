@@ -128,6 +128,23 @@ def lib():
     return _LIB
 
 
+def source_sha16() -> str:
+    """sha256 (16 hex digits) over the library's sources -- every file of kelpie_amd/csrc
+    and include/kelpie_hip.h, in name order.  tools/prof_summary.py stamps each committed
+    counter pass with it, and bench.py cites a pass only when it matches the tree it
+    runs (a pass older than the kernels it describes is never reported)."""
+    import hashlib
+    h = hashlib.sha256()
+    src = os.path.join(_HERE, "csrc")
+    paths = sorted(os.path.join(src, f) for f in os.listdir(src))
+    paths.append(os.path.join(os.path.dirname(_HERE), "include", "kelpie_hip.h"))
+    for path in paths:
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def attention_contraction():
     """The ComplEx / ConvE attention kernel a new Context uses (kp_api.hip reads the same
     variable): "bf16x3" (kp_attn3, default) or "f32" (kp_attn, KP_ATTN=f32)."""

@@ -93,16 +93,6 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     // the fp32-MFMA kernel of kp_attn.hpp
     c->attn_mode = 1;
     if (const char* a = std::getenv("KP_ATTN")) c->attn_mode = std::strcmp(a, "f32") == 0 ? 0 : 1;
-    // ComplEx D = 400 on bf16x3: the dimensions split over a wave pair, two waves per SIMD
-    // (kp_attn5.hpp); KP_ATTN_PAIR=0 keeps kp_attn3
-    if (const char* a = std::getenv("KP_ATTN_PAIR")) c->attn_pair = std::atoi(a) != 0;
-    // ConvE FC GEMMs in the step loop (bit 0 forward, bit 1 backward on kp_gemm3_abt):
-    // KP_FC=f32 | fwd | bwd | both; fp32 by default (the bf16x3 forms measured slower end to
-    // end) and always with the fp32 attention
-    c->fc_mode = 0;
-    if (const char* a = std::getenv("KP_FC"))
-      c->fc_mode = std::strcmp(a, "f32") == 0 ? 0 : std::strcmp(a, "fwd") == 0 ? 1 : std::strcmp(a, "bwd") == 0 ? 2 : 3;
-    if (c->attn_mode == 0) c->fc_mode = 0;
     // ConvE d = 200: fused conv + FC forward and FC^T + transposed-conv backward
     // (kp_cv_fused.hpp) by default; KP_CV_FUSED=0 selects the separate kernels (A/B)
     c->cv_fused = 1;
@@ -120,6 +110,15 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     if (const char* a = std::getenv("KP_ATTN_PART"))
       c->attn_part = std::strcmp(a, "streamk") == 0 ? 1 : std::strcmp(a, "ranges") == 0 ? 2 : 0;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // the context's own workspaces grow stream-ordered on its stream (DevBuf); the
+    // default pool keeps what they give back instead of returning it to the driver
+    {
+      hipMemPool_t pool;
+      KP_HIP(hipDeviceGetDefaultMemPool(&pool, device));
+      uint64_t keep = UINT64_MAX;
+      KP_HIP(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
+      for (DevBuf* d : c->bound_buffers()) d->s = c->stream;
+    }
     KP_HIP(hipEventCreate(&c->ev0));
     KP_HIP(hipEventCreate(&c->ev1));
     upload_padded(c, &c->dE, m->entity, m->n_ent, m->dim, c->dp);
@@ -155,14 +154,12 @@ int kp_ctx_destroy(kp_ctx* c) {
   c->e3.release();
   c->e3ts.release();
   c->e3pre.release();
-  c->fc3.release();
-  c->fct3.release();
-  c->e4.release();
   c->eT.release();
   c->cvf_fw3.release();
   c->cvf_bw3.release();
   for (DevBuf* b : {&c->cv_wtm, &c->cv_trel, &c->cv_wtl, &c->cv_wfm, &c->cv_wlc}) b->release();
   for (auto& b : c->cvs) b.release();
+  if (c->stream) (void)hipStreamSynchronize(c->stream);  // the stream-ordered frees above
   train_state_free(c);
   cv_train_free(c);
   for (auto e : c->evpool) (void)hipEventDestroy(e);

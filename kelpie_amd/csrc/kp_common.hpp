@@ -36,21 +36,32 @@ struct KpError {
     if (!(cond)) throw KpError{KP_EINVAL, (msg)};     \
   } while (0)
 
-// grow-only device buffer.  A grown buffer's old allocation is kept until release()
-// (the context's teardown) instead of freed at once: hipFree waits for the whole device,
-// every context's queued work included, so a mid-run free stalled the batch thread that
-// grew the buffer behind the other batches in flight
+// grow-only device buffer.  A buffer bound to its context's stream (`s`, set by
+// kp_ctx_create for the context's own workspaces) grows stream-ordered: the new
+// allocation comes from the device's default memory pool (hipMallocAsync) and the old one
+// goes back to it (hipFreeAsync) once the stream reaches the free -- no device-wide
+// synchronisation (hipFree waits for the whole device, every context's queued work
+// included, which stalled the batch thread that grew the buffer behind the other batches
+// in flight), and no superseded allocation is kept.  An unbound buffer (call-local
+// scratch) keeps its superseded allocations until release().
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  hipStream_t s = nullptr;
   std::vector<void*> old;
   void* ensure(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes > cap) {
-      if (p) old.push_back(p);
-      p = nullptr;
-      size_t want = bytes + bytes / 4;
-      KP_HIP(hipMalloc(&p, want));
+      const size_t want = bytes + bytes / 4;
+      void* q = nullptr;
+      if (s) {
+        KP_HIP(hipMallocAsync(&q, want, s));
+        if (p) KP_HIP(hipFreeAsync(p, s));
+      } else {
+        KP_HIP(hipMalloc(&q, want));
+        if (p) old.push_back(p);
+      }
+      p = q;
       cap = want;
     }
     return p;
@@ -58,7 +69,7 @@ struct DevBuf {
   template <class T>
   T* as() { return reinterpret_cast<T*>(p); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) (void)(s ? hipFreeAsync(p, s) : hipFree(p));
     for (void* q : old) (void)hipFree(q);
     old.clear();
     p = nullptr;
@@ -102,20 +113,13 @@ struct kp_ctx {
   bool time_hot = true;
   // attention contraction: 0 = fp32 MFMA (kp_attn.hpp), 1 = bf16x3 MFMA (kp_attn3.hpp)
   int attn_mode = 0;
-  int attn_pair = 0;       // ComplEx D = 400: the wave-pair kernel kp_attn5 (KP_ATTN_PAIR=1)
-  int attn5_wpc = 0;       // co-resident kp_attn5 workgroups per CU (cached)
-  int fc_mode = 0;  // ConvE step-loop FC GEMMs on kp_gemm3_abt (bf16x3): bit 0 forward, bit 1 backward
   int attn_part = 0;  // kp_attn3 partition: 0 chosen per launch, 1 stream-K, 2 XCD-grouped ranges (KP_ATTN_PART)
   DevBuf e3;               // kp_attn3's split image of dE, built on first use
   bool e3_ready = false;
   DevBuf e3ts, e3pre;      // kp_attn3's fp64 tile sums / prefix sums of dE over tiles
   bool e3pre_ready = false;
-  DevBuf e4;               // kp_attn4's blocked split image of dE, built on first use
-  bool e4_ready = false;
   DevBuf eT;               // dE transposed [dp][round_up(n_ent, 256)] fp32 (fp64 rank scoring), on first use
   bool eT_ready = false;
-  DevBuf fc3, fct3;        // ConvE: three-piece bf16 images of the FC weight and its transpose (kp_gemm3.hip)
-  bool fc3_ready = false;
   int cv_fused = 1;        // ConvE d = 200: fused encoder kernels (kp_cv_fused.hpp), KP_CV_FUSED
   int cv_rank64 = 1;       // ConvE post-training rank on fp64 logits (KP_CV_RANK=f32: fp32 sigmoid scores)
   int te_rank64 = 1;       // TransE post-training rank on fp64 squared distances (KP_TE_RANK=f32: fp32 norms)
@@ -133,6 +137,14 @@ struct kp_ctx {
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<double, double>> hot_pairs;  // (work units, seconds) per hot launch
   std::vector<double> hot_iv;  // [start, end] per hot launch, seconds since the device's time base
+  // the workspaces that live on the context's stream (DevBuf::s)
+  std::vector<DevBuf*> bound_buffers() {
+    std::vector<DevBuf*> v = {&e3, &e3ts, &e3pre, &eT, &cvf_fw3, &cvf_bw3,
+                              &cv_wtm, &cv_trel, &cv_wtl, &cv_wfm, &cv_wlc};
+    for (auto& b : ws) v.push_back(&b);
+    for (auto& b : cvs) v.push_back(&b);
+    return v;
+  }
   hipEvent_t event(size_t i) {
     while (evpool.size() <= i) {
       hipEvent_t e;
@@ -221,15 +233,6 @@ void conve_train_read(kp_ctx* c, float* conv_w, float* conv_b, float* fc_w, floa
 // out[z][m][n] = act(sum_{k in split z} A[m][k] B[n][k] + (z == 0 ? bias[n] : 0)), fp32 MFMA
 void launch_gemm_abt(kp_ctx* c, const float* A, int lda, int M, const float* B, int ldb, int N, int K, float* out,
                      int ldo, const float* bias, int act, int ksplit);
-// the same on bf16 MFMA with three-piece operands (kp_gemm3.hip): B3 is a split image
-// ([3][rows][ld] bf16, split3_rows), A one too or fp32 (a_f32: split while staged);
-// K and the leading dims multiples of 8
-void launch_gemm3_abt(kp_ctx* c, const void* A, bool a_f32, int lda, int M, const uint16_t* B3, int ldb, int N,
-                      int K, float* out, int ldo, const float* bias, int act, int ksplit);
-// X [rows][ld] fp32 -> [3][rows][ld] bf16 pieces (columns [0, cols); the rest left as is)
-void split3_rows(kp_ctx* c, const float* X, int rows, int cols, int ld, uint16_t* out);
-// ConvE: the FC weight's [dim][hidden] and its transpose's [hidden][dim] split images (built once)
-const uint16_t* conve_fc3(kp_ctx* c, bool transposed);
 enum { RANK_TRIPLE_RESULTS = 0, RANK_PREDICT_TAILS = 1, RANK_SORT_POSITION = 2 };
 // get_triple_results of a maximizer in fp64 (kp_rank.hip): q64 [n][dp] the ranking queries,
 // t64 [n] their target scores (q . E_o, or the kelpie column when o is the kelpie),

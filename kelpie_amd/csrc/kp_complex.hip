@@ -32,7 +32,6 @@
 
 #include "kp_attn.hpp"
 #include "kp_attn3.hpp"
-#include "kp_attn5.hpp"
 
 namespace {
 using namespace kpattn;
@@ -372,7 +371,6 @@ void launch_stepq(kp_ctx* c, const int4* stepq, const float* X, int nq, float* Q
 // (kp_attn3: as many as the occupancy API reports)
 template <int DB>
 int attn_slots_db(kp_ctx* c) {
-  if (c->attn_mode == 1 && c->attn_pair && DB == 25) return c->n_cu * attn5_wpc(c);
   if (c->attn_mode == 1) return c->n_cu * attn3_wpc<DB>(c);
   return c->n_cu * (DB <= 13 ? 2 : 1);
 }
@@ -381,13 +379,6 @@ template <int DB>
 void launch_attn(kp_ctx* c, bool with_o, const float* Q, int nq, const AttnPlan& plan, float* m, float* l,
                  float* O) {
   if (nq <= 0) return;
-  if (c->attn_mode == 1 && c->attn_pair && DB == 25) {
-    if (with_o)
-      launch_attn5<ATT_SOFTMAX_O>(c, c->n_ent, Q, nq, plan, m, l, O);
-    else
-      launch_attn5<ATT_SOFTMAX>(c, c->n_ent, Q, nq, plan, m, l, O);
-    return;
-  }
   if (c->attn_mode == 1) {
     if (with_o)
       launch_attn3<DB, ATT_SOFTMAX_O>(c, c->n_ent, Q, nq, plan, m, l, O, nullptr, 0.f);

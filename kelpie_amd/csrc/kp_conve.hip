@@ -925,9 +925,6 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   float* ddflat = reinterpret_cast<float*>(c->ws[20].ensure(sizeof(float) * (size_t)(fused ? 1 : mk) * c->hidden));
   float* ddl = reinterpret_cast<float*>(c->ws[21].ensure(sizeof(float) * (size_t)n_dl * mk * DP));
   float* dWt = conve_fc_wt(c);
-  // kp_gemm3_abt stages 8-value chunks: other widths (d = 60 in the goldens) stay on fp32
-  const int fcm = (c->dim % 8 == 0 && c->hidden % 8 == 0) ? c->fc_mode : 0;
-  uint16_t* ddfc3 = reinterpret_cast<uint16_t*>(c->ws[27].ensure(3 * sizeof(uint16_t) * (size_t)mk * c->dim));
   // the masks' multipliers as the fused kernels take them (1: not drawn)
   const float s_in = kc.has_in ? kc.scale_in : 1.0f, s_fm = kc.has_fm ? kc.scale_fm : 1.0f;
 
@@ -984,12 +981,8 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
         KP_CONV_FWD(dim3(ne), dim3(256), 0, c->stream, ne, ES, c->dE, dX, c->dR, kc, c->d_conv_w, c->d_conv_b,
                     c->d_bn_a, c->d_bn_b, EB, dBits, dflat);
         KP_HIP(hipGetLastError());
-        if (fcm & 1)
-          launch_gemm3_abt(c, dflat, true, c->hidden, ne, conve_fc3(c, false), c->hidden, c->dim, c->hidden, dslab,
-                           c->dim, c->d_fc_b, 0, KS);
-        else
-          launch_gemm_abt(c, dflat, c->hidden, ne, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b,
-                          0, KS);
+        launch_gemm_abt(c, dflat, c->hidden, ne, c->d_fc_w, c->hidden, c->dim, c->hidden, dslab, c->dim, c->d_fc_b, 0,
+                        KS);
       }
       hipLaunchKernelGGL(kp_cv_post_fc, dim3(ne), dim3(256), 0, c->stream, ne, dslab, KS, kc, EB, dBits, c->d_bn_a,
                          c->d_bn_b, dQ);
@@ -1054,10 +1047,6 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
         hipLaunchKernelGGL(kpcvf::kp_cv_dl_reduce, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, c->stream, nk, DP,
                            kc.has_in ? EB : nullptr, dBits, s_in, ddl);
         KP_HIP(hipGetLastError());
-      } else if (fcm & 2) {
-        split3_rows(c, ddfc, nk, c->dim, c->dim, ddfc3);
-        launch_gemm3_abt(c, ddfc3, false, c->dim, nk, conve_fc3(c, true), c->dim, c->hidden, c->dim, ddflat,
-                         c->hidden, nullptr, 0, 1);
       } else {
         launch_gemm_abt(c, ddfc, c->dim, nk, dWt, c->dim, c->hidden, c->dim, ddflat, c->hidden, nullptr, 0, 1);
       }
@@ -1158,20 +1147,6 @@ float* conve_fc_wt(kp_ctx* c) {
     KP_HIP(hipMemcpy(c->dEt, wt.data(), sizeof(float) * wt.size(), hipMemcpyHostToDevice));
   }
   return c->dEt;
-}
-
-const uint16_t* conve_fc3(kp_ctx* c, bool transposed) {
-  // three-piece images of fc.weight [dim][hidden] and of its transpose [hidden][dim] for
-  // kp_gemm3_abt (built once, kept in the context like conve_fc_wt)
-  if (!c->fc3_ready) {
-    const size_t n = (size_t)c->dim * c->hidden;
-    uint16_t* a = reinterpret_cast<uint16_t*>(c->fc3.ensure(3 * n * sizeof(uint16_t)));
-    uint16_t* b = reinterpret_cast<uint16_t*>(c->fct3.ensure(3 * n * sizeof(uint16_t)));
-    split3_rows(c, c->d_fc_w, c->dim, c->hidden, c->hidden, a);
-    split3_rows(c, conve_fc_wt(c), c->hidden, c->dim, c->dim, b);
-    c->fc3_ready = true;
-  }
-  return transposed ? c->fct3.as<uint16_t>() : c->fc3.as<uint16_t>();
 }
 
 void conve_scores_dev(kp_ctx* c, int n, const int32_t* d_heads, const int32_t* d_rels, float* d_out, int ld) {

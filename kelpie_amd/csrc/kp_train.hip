@@ -414,7 +414,6 @@ void complex_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* tripl
   c->e3_ready = false;
   c->e3pre_ready = false;
   c->eT_ready = false;
-  c->e4_ready = false;
 }
 
 // One PairwiseRankingOptimizer epoch (TransE) on the context's own tables: positive
@@ -533,5 +532,4 @@ void transe_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* pos, c
   c->e3_ready = false;
   c->e3pre_ready = false;
   c->eT_ready = false;
-  c->e4_ready = false;
 }

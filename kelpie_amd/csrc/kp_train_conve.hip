@@ -572,7 +572,7 @@ void conve_train_step(kp_ctx* c, int B, const int32_t* pairs, const int32_t* tai
   KP_HIP(hipGetLastError());
   KP_HIP(hipStreamSynchronize(s));
   // the tables and layers changed: every derived image is stale
-  c->e3_ready = c->e3pre_ready = c->eT_ready = c->e4_ready = c->fc3_ready = c->cvf_ready = false;
+  c->e3_ready = c->e3pre_ready = c->eT_ready = c->cvf_ready = false;
   if (c->dEt) {
     (void)hipFree(c->dEt);
     c->dEt = nullptr;

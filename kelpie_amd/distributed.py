@@ -35,12 +35,14 @@ import torch
 import torch.distributed as dist
 
 
-def init_from_env(backend=None):
-    """Initialise torch.distributed when launched by torchrun; returns (rank, world, local_rank)."""
+def init_from_env(backend=None, force=False):
+    """Initialise torch.distributed when launched by torchrun; returns (rank, world, local_rank).
+    ``force``: initialise a process group even for a world of one (tests that drive the
+    collective path on a single device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = os.environ.get("KELPIE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -108,11 +110,14 @@ def _device():
 class SlotSharding:
     """Split each engine batch's slots over the ranks (see the module docstring)."""
 
-    def __init__(self, rank=None, world=None, device=None):
+    def __init__(self, rank=None, world=None, device=None, force_collective=False):
         init = dist.is_initialized()
         self.rank = dist.get_rank() if rank is None and init else (rank or 0)
         self.world = dist.get_world_size() if world is None and init else (world or 1)
         self.device = device
+        # run the gathers through the process group even at world 1 (a one-rank RCCL
+        # group on one GPU exercises the device-tensor all_gather_into_tensor path)
+        self.force_collective = force_collective
         self.gathers = 0
         self.collectives = 0  # collective calls issued (the slot gather: one per batch)
         self.loads = [0] * self.world
@@ -146,7 +151,9 @@ class SlotSharding:
             counts = self._gather_counts(len(idx))
         m = int(max(counts)) + 1 if len(counts) else 1
         if len(idx) > m - 1:
-            raise RuntimeError("slot sharding: more records than the slots this rank owns")
+            # never raise before the collective (the other ranks would wait in it):
+            # send nothing but the failure status, and every rank raises after the gather
+            idx, score, rank, failed = idx[:0], score[:0], rank[:0], True
         recs = np.zeros((m, 3), np.float64)
         recs[:, 0] = -2.0
         if len(idx):
@@ -190,7 +197,7 @@ class SlotSharding:
         one collective, no host synchronisation before it."""
         self.gathers += 1
         self.collectives += 1
-        if self.world == 1 or not dist.is_initialized():
+        if not dist.is_initialized() or (self.world == 1 and not self.force_collective):
             return recs
         device = self.device or _device()
         buf = torch.from_numpy(np.ascontiguousarray(recs)).to(device)

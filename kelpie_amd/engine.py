@@ -418,6 +418,10 @@ class PostTrainingEngine(RelevanceEngine):
             mine = [i for i, s in enumerate(slots) if s.own]
             stats = {"slots": 0, "rows": 0, "pack_s": 0.0, "lib_s": 0.0}
             score, rank, err = [], [], None
+            if any(slots[i].owner != self.sharding.rank for i in mine):
+                # an owned slot must carry this rank as its owner (the record counts of the
+                # gather come from the owners): report it through the gather, never before it
+                err, mine = RuntimeError("slot sharding: an owned slot records another rank as its owner"), []
             if mine:
                 try:
                     stats = self._run_slots([slots[i] for i in mine], ctx, fill=False)

@@ -105,7 +105,7 @@ def _engine_run(name, sharding, backend="cpu"):
     if sharding is not None:
         # one collective per gather: every rank's block size is known from the claims
         assert sharding.collectives == sharding.gathers, (sharding.collectives, sharding.gathers)
-    if sharding is not None:
+    if sharding is not None and sharding.world > 1:
         # the last batch: this rank scheduled in full only the slots it claimed
         eng.set_cache()
         with eng.rng.deferred():
@@ -194,6 +194,48 @@ def test_engine_sharding_world2_gpu():
             got, exp = dict(res[name]), dict(single[name])
             got.pop("gathers"), exp.pop("gathers")
             assert got == exp, (rank, name)
+
+
+def _nccl_world1_worker(port, q):
+    """One rank, one RCCL (`nccl` backend) group on the GPU, the gathers forced through
+    the collective: every slot record goes out as a device tensor through
+    all_gather_into_tensor over RCCL and comes back."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": "0", "WORLD_SIZE": "1",
+                       "LOCAL_RANK": "0"})
+    import torch
+    import torch.distributed as dist
+    from kelpie_amd import distributed as kd
+    kd.init_from_env(backend="nccl", force=True)
+    try:
+        sh = kd.SlotSharding(device=torch.device("cuda", 0), force_collective=True)
+        res = {name: _engine_run(name, sh, backend="gpu") for name in ENGINE_CASES}
+        q.put((dist.get_backend(), sh.collectives, res))
+    except BaseException as e:
+        q.put(("error", 0, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_engine_gather_over_rccl_world1():
+    """The RCCL branch of the slot gather on the MI355X: a world-1 `nccl` process group
+    with the gathers forced through `all_gather_into_tensor` on device tensors
+    (SlotSharding.force_collective); results equal the run without a process group."""
+    single = {name: _engine_run(name, None, backend="gpu") for name in ENGINE_CASES}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1_worker, args=(_free_port(), q))
+    p.start()
+    backend, collectives, res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and backend == "nccl", (backend, res)
+    assert collectives > 0
+    for name in ENGINE_CASES:
+        got, exp = dict(res[name]), dict(single[name])
+        assert got.pop("gathers") > 0
+        exp.pop("gathers")
+        assert got == exp, name
 
 
 def _failing_worker(rank, world, port, q):

@@ -315,8 +315,8 @@ def test_complex_db100k_sufficient_batch_equals_sequential(db100k):
 
 @pytest.mark.parametrize("model_name", ["ComplEx", "ConvE"])
 def test_attention_contractions_agree(model_name, monkeypatch):
-    """kp_attn3 (bf16 MFMA, exact three-piece operand splits) and, for ComplEx, the
-    wave-pair kp_attn5 against kp_attn (fp32 MFMA, KP_ATTN=f32) on the same
+    """kp_attn3 (bf16 MFMA, exact three-piece operand splits) against kp_attn (fp32
+    MFMA, KP_ATTN=f32) on the same
     post-trainings at the production widths (ComplEx D = 400, ConvE d = 200): target
     scores within 1e-5 relative, ranks equal.  They differ from the fp32 FMA chain only
     in accumulation order."""
@@ -340,10 +340,8 @@ def test_attention_contractions_agree(model_name, monkeypatch):
                                 bn=bn, hidden_dropout_rate=0.2)
         hp = CV_HP
     out = {}
-    # ComplEx also runs the wave-pair kernel (kp_attn5, KP_ATTN_PAIR=1) on bf16x3
-    for mode in ("f32", "bf16x3", "pair") if model_name == "ComplEx" else ("f32", "bf16x3"):
-        monkeypatch.setenv("KP_ATTN", "f32" if mode == "f32" else "bf16x3")
-        monkeypatch.setenv("KP_ATTN_PAIR", "1" if mode == "pair" else "0")
+    for mode in ("f32", "bf16x3"):
+        monkeypatch.setenv("KP_ATTN", mode)
         model = make()
         seed_all(42)
         eng = ka.NecessaryPostTrainingEngine(model, ds, hp)
