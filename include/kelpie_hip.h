@@ -89,7 +89,10 @@ typedef struct {
   float hidden_dropout;  /* ConvE hidden dropout rate (masks are inputs) */
   float input_dropout;   /* ConvE input dropout rate (conve.py:142) */
   float fmap_dropout;    /* ConvE feature-map Dropout2d rate (conve.py:147) */
+  int32_t reg_kind;      /* ComplEx regulariser (multiclass_nll_optimizer.py:45-48): KP_REG_N3 | KP_REG_N2 */
 } kp_hp;
+
+enum { KP_REG_N3 = 0, KP_REG_N2 = 1 }; /* regularizers.py:37-46 (N3), :25-35 (N2) */
 
 /* One batch of post-training slots.  A slot is one KelpieModel post-training
  * (PostTrainingEngine.post_train, post_training_engine.py:64-76) followed by

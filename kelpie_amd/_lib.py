@@ -41,7 +41,11 @@ class HP(C.Structure):
     _fields_ = [("optimizer", C.c_int32), ("epochs", C.c_int32), ("batch_size", C.c_int32), ("lr", C.c_float),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("reg_weight", C.c_float),
                 ("margin", C.c_float), ("neg_ratio", C.c_int32), ("label_smoothing", C.c_float),
-                ("hidden_dropout", C.c_float), ("input_dropout", C.c_float), ("fmap_dropout", C.c_float)]
+                ("hidden_dropout", C.c_float), ("input_dropout", C.c_float), ("fmap_dropout", C.c_float),
+                ("reg_kind", C.c_int32)]
+
+
+KP_REG = {"N3": 0, "N2": 1}
 
 
 class Batch(C.Structure):

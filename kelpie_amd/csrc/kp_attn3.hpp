@@ -71,7 +71,7 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 // KP_DIAGNOSTIC_BUILD, which `make diag` sets for the variants/ libraries; the product
 // library can never carry one by a stray define.
 #if (defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O) || defined(KP_ATTN_NODMA) || defined(KP_DIAG_DMA_LGKM0) || \
-     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE) || defined(KP_DIAG_NO_OSTORE) || defined(KP_DIAG_EARLY_EXIT)) && \
+     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE) || defined(KP_DIAG_NO_OSTORE) || defined(KP_DIAG_EARLY_EXIT) || defined(KP_DIAG_O_HALF) || defined(KP_DIAG_S_HALF)) && \
     !defined(KP_DIAGNOSTIC_BUILD)
 #error "kp_attn3 diagnostic define without KP_DIAGNOSTIC_BUILD (these builds compute wrong results: make diag)"
 #endif
@@ -507,7 +507,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                 else
                   acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, rt[u][kPA[k]]),
                                                                   __builtin_bit_cast(s16x4, qt4[kPB[k]]), acc, 0, 0, 0);
+#ifdef KP_DIAG_S_HALF
+                if (u == 0 && s + 2 <= LAST && (k & 1) == 0) {  // diagnostic: half the S-phase operand reads
+#else
                 if (u == 0 && s + 2 <= LAST) {
+#endif
                   // read k of step s + 2: (sub-tile k % 2, piece k / 2)
                   const int j = s + 2, uu = k & 1, pp = k >> 1;
                   if (j < NK)
@@ -695,7 +699,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #pragma unroll
               for (int k = 0; k < 6; ++k) {
                 O[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kPA[k]], pb[kPB[k]], O[m], 0, 0, 0);
+#ifdef KP_DIAG_O_HALF
+                if (m + 2 < DB && ((m + 2) & 1) == 0) {  // diagnostic: half the O-phase operand reads
+#else
                 if (m + 2 < DB) {
+#endif
                   const int mm = m + 2, pp = k >> 1;
                   if (k & 1)
                     oh[mm % 3][pp] = lds_rd_tr<true>(ob, 16 * ROW_B + pp * PART_B + 32 * mm);

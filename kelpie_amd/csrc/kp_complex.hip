@@ -99,6 +99,7 @@ struct CxOpt {
   float step_size;  // Adam: lr / (1 - b1^t)
   float bc2_sqrt;   // Adam: sqrt(1 - b2^t)
   float reg_w;
+  int reg_n2;  // KP_REG_N2: N2 on the whole row's L2 norm (regularizers.py:25-35) instead of N3
 };
 
 #define UPD_MAXSPLIT 16
@@ -242,6 +243,23 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
     }
     __syncthreads();
   }
+  // N2 (regularizers.py:25-35): the factor of each batch row holding the kelpie entity
+  // is ||f||^3 with f_i = |x_i| (complex modulus, complex.py:80-84), so its gradient is
+  // 3 w / B * ||f|| * x per such row; ||f|| over the whole row, before the update
+  float n2 = 0.f;
+  if (opt.reg_w != 0.f && opt.reg_n2) {
+    __shared__ float n2red[4];
+    float ps = 0.f;
+    for (int i = tid; i < half; i += 256) {
+      const float a = x[i], b = x[i + half];
+      const float f = sqrtf(a * a + b * b);
+      ps += f * f;
+    }
+    ps = wave_sum(ps);
+    if ((tid & 63) == 0) n2red[tid >> 6] = ps;
+    __syncthreads();
+    n2 = sqrtf((n2red[0] + n2red[1]) + (n2red[2] + n2red[3]));
+  }
 #pragma unroll
   for (int u = 0; u < (DP / 2 + 255) / 256; ++u) {
     const int i = tid + 256 * u;
@@ -261,7 +279,7 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
     gv[1] *= inv_b;
     const float a = x[i], b = x[i + half];
     if (opt.reg_w != 0.f) {
-      const float mod = sqrtf(a * a + b * b);
+      const float mod = opt.reg_n2 ? n2 : sqrtf(a * a + b * b);
       const float k3 = 3.0f * opt.reg_w * inv_b * (float)(P.cnt_l + P.cnt_r) * mod;
       gv[0] += k3 * a;
       gv[1] += k3 * b;
@@ -703,6 +721,8 @@ void complex_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   opt.one_minus_b1 = (float)(1.0 - (double)hp->beta1);
   opt.one_minus_b2 = (float)(1.0 - (double)hp->beta2);
   opt.reg_w = hp->reg_weight;
+  KP_REQUIRE(hp->reg_kind == KP_REG_N3 || hp->reg_kind == KP_REG_N2, "ComplEx: unknown regulariser");
+  opt.reg_n2 = hp->reg_kind == KP_REG_N2;
   // loop-interval events, destroyed on every exit path (a KP_HIP / KP_REQUIRE below throws)
   struct LoopEvents {
     hipEvent_t a = nullptr, b = nullptr;

@@ -131,11 +131,13 @@ class ComplEx(FrozenModel):
         name = hp["optimizer_name"]
         if name not in _lib.KP_OPT:
             raise ValueError(f"unknown optimizer {name}")
-        if float(hp.get("regularizer_weight", 0.0)) != 0.0 and hp.get("regularizer_name", "N3") != "N3":
-            raise NotImplementedError("only the N3 regulariser is supported with a non-zero weight")
+        reg = hp.get("regularizer_name", "N3")
+        if reg not in _lib.KP_REG:  # multiclass_nll_optimizer.py:45-48: {"N3", "N2"}[name]
+            raise KeyError(reg)
         return _lib.HP(optimizer=_lib.KP_OPT[name], epochs=int(hp["epochs"]), batch_size=int(hp["batch_size"]),
                        lr=float(hp["lr"]), beta1=float(hp.get("decay1", 0.9)), beta2=float(hp.get("decay2", 0.999)),
-                       eps=1e-10 if name == "Adagrad" else 1e-8, reg_weight=float(hp.get("regularizer_weight", 0.0)))
+                       eps=1e-10 if name == "Adagrad" else 1e-8, reg_weight=float(hp.get("regularizer_weight", 0.0)),
+                       reg_kind=_lib.KP_REG[reg])
 
     def posttrain_draws(self, rows, hp, rng):
         return rng.complex_epochs(len(rows), int(hp["epochs"]), int(hp["batch_size"]))

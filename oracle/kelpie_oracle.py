@@ -580,6 +580,7 @@ def posttrain_complex(model: OracleModel, ds, triples, x0, hp, rng):
     else:
         opt = SGDState(D, hp["lr"])
     w_reg = float(hp.get("regularizer_weight", 0.0))
+    n2 = hp.get("regularizer_name", "N3") == "N2"  # multiclass_nll_optimizer.py:45-48
     for _ in range(int(hp["epochs"])):
         perm = rng.randperm(n)
         prow = rows[perm]
@@ -613,6 +614,8 @@ def posttrain_complex(model: OracleModel, ds, triples, x0, hp, rng):
                     if mask.any():
                         a_, b_ = side[mask, :d].astype(np.float64), side[mask, d:].astype(np.float64)
                         mod = np.sqrt(a_ ** 2 + b_ ** 2)
+                        if n2:  # regularizers.py:25-35: ||f||^3, f = complex moduli of the row
+                            mod = np.sqrt((mod ** 2).sum(1, keepdims=True))
                         g[:d] += (3 * w_reg / b * mod * a_).sum(0)
                         g[d:] += (3 * w_reg / b * mod * b_).sum(0)
             x = opt.step(x, g.astype(F32))

@@ -114,7 +114,8 @@ class OracleBackedContext:
         if self.model.name == "ComplEx":
             names = {0: "Adagrad", 1: "Adam", 2: "SGD"}
             return {"optimizer_name": names[hp.optimizer], "batch_size": hp.batch_size, "epochs": hp.epochs,
-                    "lr": hp.lr, "decay1": hp.beta1, "decay2": hp.beta2, "regularizer_weight": hp.reg_weight}
+                    "lr": hp.lr, "decay1": hp.beta1, "decay2": hp.beta2, "regularizer_weight": hp.reg_weight,
+                    "regularizer_name": {0: "N3", 1: "N2"}[hp.reg_kind]}
         if self.model.name == "TransE":
             return {"batch_size": hp.batch_size, "epochs": hp.epochs, "lr": hp.lr, "margin": hp.margin,
                     "negative_triples_ratio": hp.neg_ratio, "regularizer_weight": hp.reg_weight}

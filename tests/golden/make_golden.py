@@ -99,6 +99,18 @@ CASES = {
                               hp={"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0427, "decay": 0.995,
                                   "epochs": 40},
                               xsi=5.0, suff_xsi=0.9, conve_random_bn=True),
+    # the two multiclass-NLL regularisers with a non-zero weight in post-training
+    # (multiclass_nll_optimizer.py:45-48, regularizers.py:25-46)
+    "complex_n3_tiny": dict(model="ComplEx", shape="tiny", dim=8, model_params={"dimension": 8, "init_scale": 1e-3},
+                            hp={"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 43, "lr": 0.043,
+                                "decay1": 0.9, "decay2": 0.999, "regularizer_name": "N3",
+                                "regularizer_weight": 0.05},
+                            xsi=5.0, suff_xsi=0.9, skip_builder=True, trained_scale=0.5),
+    "complex_n2_tiny": dict(model="ComplEx", shape="tiny", dim=8, model_params={"dimension": 8, "init_scale": 1e-3},
+                            hp={"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 43, "lr": 0.043,
+                                "decay1": 0.9, "decay2": 0.999, "regularizer_name": "N2",
+                                "regularizer_weight": 0.05},
+                            xsi=5.0, suff_xsi=0.9, skip_builder=True, trained_scale=0.5),
     # the production kernel instantiations (ComplEx D = 400 -> kp_attn3<25>, TransE d = 200),
     # pinned by reference vectors directly (2,000-entity graph; hub subject -> multi-step epochs)
     "complex200_small": dict(model="ComplEx", shape="small", dim=200,

@@ -10,7 +10,8 @@ import pytest
 from engine_cases import check_builder, check_necessary, check_pipeline, check_pipeline_explain, check_sufficient
 from golden_io import CASES
 
-FAST = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve60_tiny", "conve60_drop_tiny"]
+FAST = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve60_tiny", "conve60_drop_tiny", "complex_n3_tiny",
+        "complex_n2_tiny"]
 
 
 @pytest.mark.parametrize("name", FAST)
