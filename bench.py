@@ -79,6 +79,12 @@ WORKLOADS = {
     # BASELINE.json configs[4]
     "conve-yago310-necessary": dict(model="ConvE", shape="YAGO3-10", dim=200, mode="necessary", hp=CONVE_HP,
                                     candidates=20, preds_per_step=8, hidden_dropout=0.2, depth=3),
+    # the same with all three ConvE dropouts in post-training at the rates of the reference's
+    # ConvE YAGO4-20 config (configs/ConvE_YAGO4-20_training.json: input 0.2, feature map 0.3,
+    # hidden 0.1; conve.py:142,147,151): the frozen-head pairs are re-encoded every step
+    "conve-yago310-necessary-drop": dict(model="ConvE", shape="YAGO3-10", dim=200, mode="necessary", hp=CONVE_HP,
+                                         candidates=20, preds_per_step=8, hidden_dropout=0.1, input_dropout=0.2,
+                                         fmap_dropout=0.3, depth=3),
 }
 
 
@@ -167,7 +173,8 @@ def build(wl, device, rank):
     else:
         model = ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
                       w["conv_bias"], w["fc_weight"], w["fc_bias"], hidden_dropout_rate=wl["hidden_dropout"],
-                      device=device)
+                      input_dropout_rate=wl.get("input_dropout", 0.0),
+                      feature_map_dropout_rate=wl.get("fmap_dropout", 0.0), device=device)
     log(f"[rank {rank}] graph+indices {time.time() - t0:.1f}s  |E|={g.num_entities} train={len(g.train)}")
     return ds, model, w
 
@@ -224,7 +231,9 @@ def cpu_baseline(wl, ds, weights, pred, cands, ents=None, fixture=None):
     from threadpoolctl import threadpool_info
     from oracle import kelpie_oracle as ko
     om = ko.OracleModel(wl["model"], weights, wl["dim"],
-                        {"init_scale": 1e-3, "hidden_dropout_rate": wl.get("hidden_dropout", 0.0)})
+                        {"init_scale": 1e-3, "hidden_dropout_rate": wl.get("hidden_dropout", 0.0),
+                         "input_dropout_rate": wl.get("input_dropout", 0.0),
+                         "feature_map_dropout_rate": wl.get("fmap_dropout", 0.0)})
     ods = ko.OracleDataset(ds.num_entities, ds.num_relations, ds.training_triples, ds.validation_triples,
                            ds.testing_triples)
     seed_all(42)

@@ -31,6 +31,8 @@
 // is where the S^T accumulators already put P, so P's pieces are the B operand as
 // they sit; A = E^T by two ds_read_b64_tr_b16 per piece (rows 4g.. and 16 + 4g..).
 #pragma once
+#include <type_traits>
+
 #include "kp_attn.hpp"
 
 #ifdef KP_ATTN3_STAMPS
@@ -85,6 +87,9 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #endif
 #ifndef KP_ILV
 #define KP_ILV 1
+#endif
+#ifndef KP_ATTN_FULLTILE
+#define KP_ATTN_FULLTILE 1  // full key tiles skip the per-key masks (bitwise the same)
 #endif
 #ifndef KP_ASM_ALL
 #define KP_ASM_ALL 0  // 1: the asm read form for every DB (ConvE included)
@@ -590,7 +595,13 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #pragma unroll
           for (int m = 0; m < OA && m < DB; ++m) load_o(m, m);
         }
+        // weights of the tile (softmax or the BCE gradient) and the centred accumulation;
+        // a full tile (every key < key_end: all but a range's last) runs without the key
+        // masks (KP_ATTN_FULLTILE, the same bits)
         float pw[2][4];
+        auto weights = [&](auto full_c) {
+          constexpr bool FULL = decltype(full_c)::value;
+          auto keep = [&](int u, int r) { return FULL || (k0 + 16 * u + 4 * g + r < key_end); };
         if (MODE == ATT_BCE_O) {
 #pragma unroll
           for (int u = 0; u < 2; ++u)
@@ -598,9 +609,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             for (int r = 0; r < 4; ++r) {
               const float x0 = __builtin_amdgcn_rcpf(1.0f + __expf(-sc[u][r]));
               const float w0 = (1.0f - x0) * x0;
-              pw[u][r] = (k0 + 16 * u + 4 * g + r < key_end)
-                             ? (((x0 - ylo) * __builtin_amdgcn_rcpf(fmaxf(w0, 1e-12f))) * gsc) * w0
-                             : 0.f;
+              pw[u][r] = keep(u, r) ? (((x0 - ylo) * __builtin_amdgcn_rcpf(fmaxf(w0, 1e-12f))) * gsc) * w0 : 0.f;
             }
         } else {
           float v[2][4];
@@ -609,7 +618,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              v[u][r] = (k0 + 16 * u + 4 * g + r < key_end) ? sc[u][r] : kNegInf;
+              v[u][r] = keep(u, r) ? sc[u][r] : kNegInf;
               tmax = fmaxf(tmax, v[u][r]);
             }
           m_seen = fmaxf(m_seen, tmax);
@@ -631,7 +640,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             for (int u = 0; u < 2; ++u)
 #pragma unroll
               for (int r = 0; r < 4; ++r)
-                if (k0 + 16 * u + 4 * g + r < key_end) mn = fminf(mn, pw[u][r]);
+                if (keep(u, r)) mn = fminf(mn, pw[u][r]);
             mn = fminf(mn, __shfl_xor(mn, 16, 64));
             mn = fminf(mn, __shfl_xor(mn, 32, 64));
             csh = (mn < kPosInf) ? mn : 0.f;
@@ -640,12 +649,19 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              pw[u][r] = (k0 + 16 * u + 4 * g + r < key_end) ? __fsub_rn(pw[u][r], csh) : 0.f;
+            for (int r = 0; r < 4; ++r) pw[u][r] = keep(u, r) ? __fsub_rn(pw[u][r], csh) : 0.f;
             lt += (pw[u][0] + pw[u][1]) + (pw[u][2] + pw[u][3]);
           }
           l_run += lt;
         }
+        };
+        // (the asm read form only: with the compiler-visible reads of the ConvE width the
+        // branch moved the compiler's LDS reads against the asm LDS-DMA burst and the
+        // results went wrong -- DESIGN.md section 5, the LDS-DMA hazard)
+        if (KP_ATTN_FULLTILE && ASM && k0 + KT <= key_end)
+          weights(std::true_type{});
+        else
+          weights(std::false_type{});
         if (WITH_O && KP_DIAG_O) {
           // P pieces in the B layout: element j of lane group g = entity 4g + j (j < 4)
           // or 16 + 4g + j - 4

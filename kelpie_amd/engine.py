@@ -139,7 +139,7 @@ class RelevanceEngine:
             fl.extend(F)
             fo.append(len(fl))
         sh = self.sharding
-        if sh is not None and sh.world > 1:
+        if sh is not None and (sh.world > 1 or getattr(sh, "force_collective", False)):
             # entity-range shard of the conversion test, keep mask all-gathered
             lo, hi = len(ents) * sh.rank // sh.world, len(ents) * (sh.rank + 1) // sh.world
             part = np.zeros(0, bool)
@@ -191,7 +191,9 @@ class PostTrainingEngine(RelevanceEngine):
 
     def _sharded(self):
         sh = self.sharding
-        return sh is not None and sh.world > 1
+        # a one-rank sharding with force_collective takes the sharded path too (its
+        # gathers then run through the process group: the RCCL test on one GPU)
+        return sh is not None and (sh.world > 1 or getattr(sh, "force_collective", False))
 
     def _skip_slot(self, kp, rows=None, n_rows=0):
         """A slot another rank post-trains: advance the generators past its draws only."""

@@ -196,19 +196,21 @@ def test_engine_sharding_world2_gpu():
             assert got == exp, (rank, name)
 
 
-def _nccl_world1_worker(port, q):
+def _nccl_world1_worker(port, q, backend="nccl"):
     """One rank, one RCCL (`nccl` backend) group on the GPU, the gathers forced through
     the collective: every slot record goes out as a device tensor through
-    all_gather_into_tensor over RCCL and comes back."""
+    all_gather_into_tensor over RCCL and comes back (backend "gloo": the same on the
+    CPU stand-in)."""
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": "0", "WORLD_SIZE": "1",
                        "LOCAL_RANK": "0"})
     import torch
     import torch.distributed as dist
     from kelpie_amd import distributed as kd
-    kd.init_from_env(backend="nccl", force=True)
+    kd.init_from_env(backend=backend, force=True)
     try:
-        sh = kd.SlotSharding(device=torch.device("cuda", 0), force_collective=True)
-        res = {name: _engine_run(name, sh, backend="gpu") for name in ENGINE_CASES}
+        dev = torch.device("cuda", 0) if backend == "nccl" else "cpu"
+        sh = kd.SlotSharding(device=dev, force_collective=True)
+        res = {name: _engine_run(name, sh, backend="gpu" if backend == "nccl" else "cpu") for name in ENGINE_CASES}
         q.put((dist.get_backend(), sh.collectives, res))
     except BaseException as e:
         q.put(("error", 0, repr(e)))
@@ -230,6 +232,25 @@ def test_engine_gather_over_rccl_world1():
     backend, collectives, res = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0 and backend == "nccl", (backend, res)
+    assert collectives > 0
+    for name in ENGINE_CASES:
+        got, exp = dict(res[name]), dict(single[name])
+        assert got.pop("gathers") > 0
+        exp.pop("gathers")
+        assert got == exp, name
+
+
+def test_engine_gather_forced_collective_world1_cpu():
+    """The forced-collective path of the RCCL test on the CPU stand-in: a world-1 gloo
+    group, every gather through the process group; results equal the plain run."""
+    single = {name: _engine_run(name, None) for name in ENGINE_CASES}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1_worker, args=(_free_port(), q, "gloo"))
+    p.start()
+    backend, collectives, res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and backend == "gloo", (backend, res)
     assert collectives > 0
     for name in ENGINE_CASES:
         got, exp = dict(res[name]), dict(single[name])

@@ -19,6 +19,10 @@
 #include "kp_attn5.hpp"
 #define KP_MICRO_HAS_ATTN5 1
 #endif
+#if __has_include("kp_attn6.hpp")
+#include "kp_attn6.hpp"
+#define KP_MICRO_HAS_ATTN6 1
+#endif
 #if __has_include("kp_attn4.hpp")
 #include "kp_attn4.hpp"
 #define KP_MICRO_HAS_ATTN4 1
@@ -166,7 +170,18 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
   const float ylo = 0.05f;
   // KP_MICRO_ATTN4=1: the pipelined kernel (kp_attn4.hpp) where it exists
   const bool use4 = std::getenv("KP_MICRO_ATTN4") && std::atoi(std::getenv("KP_MICRO_ATTN4")) == 1;
+  // KP_MICRO_ATTN6=1: the pair-shared O phase (kp_attn6.hpp) for the D = 400 softmax step
+  const bool use6 = std::getenv("KP_MICRO_ATTN6") && std::atoi(std::getenv("KP_MICRO_ATTN6")) == 1;
   auto launch = [&]() {
+#ifdef KP_MICRO_HAS_ATTN6
+    if constexpr (DB == 25 && MODE == ATT_SOFTMAX_O) {
+      if (use6) {
+        launch_attn6<DB>(&c, n_ent, dQ, nq, plan, dm, dl, dO);
+        return;
+      }
+    }
+#endif
+    (void)use6;
 #ifdef KP_MICRO_HAS_ATTN4
     if constexpr (attn4_supported(DB) && MODE == ATT_SOFTMAX_O) {
       if (use4) {

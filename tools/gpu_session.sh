@@ -36,19 +36,23 @@ run_step() {
       local rc=$?
       grep -E "passed|failed|error" $O/tests_${a[1]:-all}.txt | tail -2
       return $rc ;;
-    micro|microfb)
-      local v=${a[1]} reps=${a[2]:-2}
+    micro|microfb|microdb)
+      local v=${a[1]} reps=${a[2]:-2} envs=() tagx=""
+      if [ -n "${a[3]}" ]; then IFS=',' read -r -a envs <<< "${a[3]}"; tagx="_$(echo ${a[3]} | tr ',=' '__')"; fi
       local shapes=("${MICRO_SHAPES[@]}")
       [ $n = microfb ] && shapes=("${MICRO_SHAPES[0]}")
+      [ $n = microdb ] && shapes=("${MICRO_SHAPES[0]}" "${MICRO_SHAPES[1]}")
       for rep in $(seq 1 $reps); do
         for args in "${shapes[@]}"; do
-          timeout -k 10 120 variants/attn_micro_$v $args 0.05 >> $O/micro_$v.jsonl || return 1
+          env "${envs[@]}" timeout -k 10 120 variants/attn_micro_$v $args 0.05 >> $O/micro_$v$tagx.jsonl || return 1
         done
       done
-      grep -v stamps $O/micro_$v.jsonl | cut -c1-260 | tail -$(( reps * ${#shapes[@]} )) || true
-      grep stamps $O/micro_$v.jsonl | tail -2 || true ;;
+      grep -v stamps $O/micro_$v$tagx.jsonl | cut -c1-260 | tail -$(( reps * ${#shapes[@]} )) || true
+      grep stamps $O/micro_$v$tagx.jsonl | tail -2 || true ;;
     pmcmicro)
-      local v=${a[1]} i=0
+      local v=${a[1]} i=0 envs=()
+      [ -n "${a[2]}" ] && IFS=',' read -r -a envs <<< "${a[2]}"
+      for e in "${envs[@]}"; do export "$e"; done
       export TMPDIR=/tmp
       for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
                "GRBM_GUI_ACTIVE GRBM_COUNT TCC_HIT_sum TCC_MISS_sum" \

@@ -53,8 +53,9 @@ def reference_model(src, wl, g, w):
     elif wl["model"] == "TransE":
         mp["norm"] = 2
     else:
-        mp.update({"input_dropout_rate": 0, "hidden_dropout_rate": wl.get("hidden_dropout", 0.0),
-                   "feature_map_dropout_rate": 0, "hidden_layer_size": 9728})
+        mp.update({"input_dropout_rate": wl.get("input_dropout", 0.0),
+                   "hidden_dropout_rate": wl.get("hidden_dropout", 0.0),
+                   "feature_map_dropout_rate": wl.get("fmap_dropout", 0.0), "hidden_layer_size": 9728})
     model = cls(dataset=dataset, hp=cls.get_hyperparams_class()(**mp))
     with torch.no_grad():
         model.entity_embeddings.data = torch.from_numpy(w["entity_embeddings"].copy())
@@ -151,7 +152,9 @@ def main():
     if not args.no_oracle:
         from oracle import kelpie_oracle as ko
         om = ko.OracleModel(wl["model"], w, wl["dim"],
-                            {"init_scale": 1e-3, "hidden_dropout_rate": wl.get("hidden_dropout", 0.0)})
+                            {"init_scale": 1e-3, "hidden_dropout_rate": wl.get("hidden_dropout", 0.0),
+                             "input_dropout_rate": wl.get("input_dropout", 0.0),
+                             "feature_map_dropout_rate": wl.get("fmap_dropout", 0.0)})
         ods = ko.OracleDataset(ds.num_entities, ds.num_relations, ds.training_triples, ds.validation_triples,
                                ds.testing_triples)
         bench.seed_all(42)

@@ -33,7 +33,10 @@ def main():
     eng = cls(model, ds, wl["hp"])
     per = wl.get("preds_per_step", 1)
     preds = bench.pick_preds(ds, a.batches * per * a.world, seed=1234)
-    fx = bench.load_fixture(a.workload)
+    # conversion entities (sufficient): the fixture's, as the reference selected them for its
+    # prediction (the rehearsal has no GPU for kp_convertible); the schedule's cost depends
+    # on their degrees, not on which prediction they were selected for
+    fx = bench.load_fixture(a.workload) or bench.load_fixture(a.workload + "__p0")
     ents = fx["entities_to_convert"] if fx and wl["mode"] == "sufficient" else None
 
     def items(b, n):
