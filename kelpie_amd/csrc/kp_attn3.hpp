@@ -91,6 +91,9 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_ATTN_FULLTILE
 #define KP_ATTN_FULLTILE 1  // full key tiles skip the per-key masks (bitwise the same)
 #endif
+#ifndef KP_ATTN_FULLTILE_ALL
+#define KP_ATTN_FULLTILE_ALL 0  // ... on the compiler-visible read form (ConvE) as well
+#endif
 #ifndef KP_ASM_ALL
 #define KP_ASM_ALL 0  // 1: the asm read form for every DB (ConvE included)
 #endif
@@ -658,7 +661,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         // (the asm read form only: with the compiler-visible reads of the ConvE width the
         // branch moved the compiler's LDS reads against the asm LDS-DMA burst and the
         // results went wrong -- DESIGN.md section 5, the LDS-DMA hazard)
-        if (KP_ATTN_FULLTILE && ASM && k0 + KT <= key_end)
+        if (KP_ATTN_FULLTILE && (ASM || KP_ATTN_FULLTILE_ALL) && k0 + KT <= key_end)
           weights(std::true_type{});
         else
           weights(std::false_type{});

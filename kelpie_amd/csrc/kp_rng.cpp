@@ -111,6 +111,194 @@ inline uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
+// ---------------------------------------------------------------------------------
+// MT19937 jump-ahead.  The generator is linear over GF(2): with T the map that advances
+// the 624-word window (x_k .. x_{k+623}) by one word and P(x) its characteristic
+// polynomial (degree 19937, primitive), T^D = g(T) for g = x^D mod P.  P is found once
+// by Berlekamp-Massey on the low bits of a stream of untempered words; g by square-and-
+// multiply in GF(2)[x] mod P; g(T) W by Horner over g's 19937 coefficients, each step
+// one window advance plus (for a set coefficient) a 624-word xor.  A jump costs the same
+// for every distance, so skipping the draws of the slots other ranks post-train (the
+// ConvE constructions and dropout masks: ~8 M words per slot) no longer costs the walk.
+// The lowest 31 bits of the window's first word do not feed the recurrence, so Horner
+// leaves them unreliable: a jump by D is g = x^(D-1) followed by one plain advance.
+// ---------------------------------------------------------------------------------
+constexpr int kDeg = 19937;
+constexpr int kPW = kDeg / 64 + 1;  // 312 words: coefficients x^0 .. x^19967
+
+struct MtPoly {
+  uint64_t w[kPW];
+};
+
+// one window advance on a circular 624-word buffer whose element 0 is at head h
+inline void mt_step(uint32_t* b, int& h) {
+  const uint32_t a = b[h], c = b[h + 1 < kN ? h + 1 : h + 1 - kN], m = b[(h + kM) % kN];
+  const uint32_t y = (a & 0x80000000u) | (c & 0x7fffffffu);
+  b[h] = m ^ (y >> 1) ^ ((0u - (c & 1u)) & 0x9908b0dfu);
+  h = h + 1 < kN ? h + 1 : 0;
+}
+
+// P(x) by Berlekamp-Massey over the bit 0 of 2 * 19937 words of a seeded generator
+const MtPoly& mt_charpoly() {
+  static MtPoly P;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    constexpr int NB = 2 * kDeg;
+    constexpr int SW = NB / 64 + 2;
+    std::vector<uint64_t> seq(SW, 0), rev(SW + kPW + 2, 0);
+    uint32_t st[kN];
+    st[0] = 5489u;
+    for (int i = 1; i < kN; ++i) st[i] = 1812433253u * (st[i - 1] ^ (st[i - 1] >> 30)) + (uint32_t)i;
+    int h = 0;
+    for (int i = 0; i < NB; ++i) {
+      mt_step(st, h);
+      const uint32_t x = st[(h + kN - 1) % kN];  // the word just made
+      if (x & 1u) seq[i >> 6] |= 1ull << (i & 63);
+    }
+    // rev bit j = seq bit NB - 1 - j, so the window s[n-1], s[n-2], ... is rev from NB - n
+    for (int i = 0; i < NB; ++i)
+      if (seq[i >> 6] >> (i & 63) & 1) {
+        const int j = NB - 1 - i;
+        rev[j >> 6] |= 1ull << (j & 63);
+      }
+    auto rev_word = [&](int bit) -> uint64_t {  // rev bits [bit, bit + 64)
+      const int q = bit >> 6, r = bit & 63;
+      return r ? (rev[q] >> r) | (rev[q + 1] << (64 - r)) : rev[q];
+    };
+    std::vector<uint64_t> C(kPW + 2, 0), B(kPW + 2, 0), T(kPW + 2, 0);
+    C[0] = B[0] = 1;
+    int L = 0, m = 1;
+    for (int n = 0; n < NB; ++n) {
+      // d = s[n] ^ sum_{i=1..L} c_i s[n - i]; c_i s[n - i] = C bit i & rev bit (NB - 1 - n + i)
+      uint64_t acc = 0;
+      const int off = NB - 1 - n;
+      const int words = (L >> 6) + 1;
+      for (int k = 0; k < words; ++k) acc ^= C[k] & rev_word(off + 64 * k);
+      int d = (int)(__builtin_popcountll(acc) & 1);  // includes c_0 s[n] (c_0 = 1)
+      if (!d) {
+        ++m;
+        continue;
+      }
+      auto xor_shift = [&](std::vector<uint64_t>& dst, const std::vector<uint64_t>& src, int sh) {
+        const int q = sh >> 6, r = sh & 63;
+        for (int k = kPW + 1; k >= q; --k) {
+          uint64_t v = src[k - q] << r;
+          if (r && k - q - 1 >= 0) v |= src[k - q - 1] >> (64 - r);
+          dst[k] ^= v;
+        }
+      };
+      if (2 * L <= n) {
+        T = C;
+        xor_shift(C, B, m);
+        L = n + 1 - L;
+        B = T;
+        m = 1;
+      } else {
+        xor_shift(C, B, m);
+        ++m;
+      }
+    }
+    if (L != kDeg) throw std::runtime_error("mt19937 jump: characteristic polynomial of unexpected degree");
+    // BM's C is the connection polynomial (c_0 = 1 ... c_L); the characteristic
+    // polynomial is its reciprocal x^L C(1/x)
+    for (int i = 0; i <= kDeg; ++i)
+      if (C[i >> 6] >> (i & 63) & 1) {
+        const int j = kDeg - i;
+        P.w[j >> 6] |= 1ull << (j & 63);
+      }
+  });
+  return P;
+}
+
+// g = x^D mod P
+void mt_jump_poly(uint64_t D, MtPoly& g) {
+  const MtPoly& P = mt_charpoly();
+  // P shifted left by 0..63 bits (each XOR of the reduction word-aligned)
+  static std::vector<uint64_t> Psh;
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    Psh.assign(64 * (kPW + 1), 0);
+    for (int r = 0; r < 64; ++r)
+      for (int k = 0; k <= kPW; ++k) {
+        uint64_t v = k < kPW ? P.w[k] << r : 0;
+        if (r && k > 0) v |= P.w[k - 1] >> (64 - r);
+        Psh[64 * 0 + r * (kPW + 1) + k] = v;
+      }
+  });
+  std::vector<uint64_t> sq(2 * kPW + 2);
+  std::memset(g.w, 0, sizeof(g.w));
+  g.w[0] = 1;
+  int top = 63;
+  while (top > 0 && !((D >> top) & 1)) --top;
+  auto reduce = [&](uint64_t* a, int hi_bit) {  // a: bits up to hi_bit, reduced below 19937
+    for (int i = hi_bit; i >= kDeg; --i) {
+      if (!(a[i >> 6] >> (i & 63) & 1)) continue;
+      const int sh = i - kDeg, q = sh >> 6, r = sh & 63;
+      const uint64_t* ps = &Psh[r * (kPW + 1)];
+      for (int k = 0; k <= kPW && q + k < 2 * kPW + 2; ++k) a[q + k] ^= ps[k];
+    }
+  };
+  for (int b = top; b >= 0; --b) {
+    // square: coefficient i -> 2i
+    std::fill(sq.begin(), sq.end(), 0);
+    for (int k = 0; k < kPW; ++k) {
+      uint64_t v = g.w[k];
+      if (!v) continue;
+      uint64_t lo = 0, hi = 0;
+      for (int j = 0; j < 32; ++j) {
+        lo |= ((v >> j) & 1ull) << (2 * j);
+        hi |= ((v >> (j + 32)) & 1ull) << (2 * j);
+      }
+      sq[2 * k] = lo;
+      sq[2 * k + 1] = hi;
+    }
+    reduce(sq.data(), 2 * (kDeg - 1));
+    std::memcpy(g.w, sq.data(), sizeof(g.w));
+    if ((D >> b) & 1) {
+      // times x
+      uint64_t carry = 0;
+      for (int k = 0; k < kPW; ++k) {
+        const uint64_t v = g.w[k];
+        g.w[k] = (v << 1) | carry;
+        carry = v >> 63;
+      }
+      if (g.w[kDeg >> 6] >> (kDeg & 63) & 1)
+        for (int k = 0; k < kPW; ++k) g.w[k] ^= P.w[k];
+    }
+  }
+}
+
+// the window s (x_k .. x_{k+623}, element 0 first) -> (x_{k+D} .. x_{k+D+623}), D >= 1
+void mt_jump_window(uint32_t* s, uint64_t D) {
+  MtPoly g;
+  mt_jump_poly(D - 1, g);
+  uint32_t acc[kN];
+  std::memset(acc, 0, sizeof(acc));
+  int h = 0;
+  int deg = kDeg - 1;
+  while (deg > 0 && !(g.w[deg >> 6] >> (deg & 63) & 1)) --deg;
+  for (int i = deg; i >= 0; --i) {
+    mt_step(acc, h);
+    if (g.w[i >> 6] >> (i & 63) & 1) {
+      // acc element j (at (h + j) % N) ^= s[j]
+      const int n1 = kN - h;
+      for (int j = 0; j < n1; ++j) acc[h + j] ^= s[j];
+      for (int j = n1; j < kN; ++j) acc[j - n1] ^= s[j];
+    }
+  }
+  mt_step(acc, h);  // one plain advance: the first word's low bits are valid again
+  for (int j = 0; j < kN; ++j) s[j] = acc[(h + j) % kN];
+}
+
+// skips at least this many outputs go by jump-ahead (KP_MT_JUMP_MIN; 0 never)
+uint64_t mt_jump_min() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("KP_MT_JUMP_MIN");
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)60000000;
+  }();
+  return v;
+}
+
 // ATen's mt19937 over the CPU-generator state blob of torch.get_rng_state():
 //   { u64 seed; i32 left; i32 seeded; u64 next; u64 state[624]; ... }.
 // operator(): if (--left == 0) twist (left = 624, next = 0); return temper(state[next++]).
@@ -137,6 +325,18 @@ struct TorchMt {
   }
   // advance by n outputs (operator() semantics, nothing tempered)
   void skip(uint64_t n) {
+    const uint64_t jmin = mt_jump_min();
+    if (jmin && n >= jmin && n > (uint64_t)(left - 1) + kN) {
+      // the rest of this block, then t whole twists by jump-ahead; c words of the last
+      // block consumed (the twisting call takes its first word: left = kN, next = 1)
+      const uint64_t rest = n - (uint64_t)(left - 1);
+      const uint64_t t = (rest + kN - 1) / kN;
+      const uint64_t c = rest - (uint64_t)kN * (t - 1);
+      mt_jump_window(s, (uint64_t)kN * t);
+      left = (int32_t)(kN - c + 1);
+      next = c;
+      return;
+    }
     while (n > 0) {
       const uint64_t k = std::min<uint64_t>(n, (uint64_t)(left - 1));
       left -= (int32_t)k;

@@ -122,15 +122,35 @@ class SlotSharding:
         self.collectives = 0  # collective calls issued (the slot gather: one per batch)
         self.loads = [0] * self.world
 
-    def begin_batch(self):
-        """Start claiming the slots of a new engine batch."""
+    def begin_batch(self, costs=None):
+        """Start claiming the slots of a new engine batch.  With ``costs`` (every slot's
+        cost in schedule order, engine._plan_costs) the slots are cut into ``world``
+        contiguous runs of about equal total cost -- slot i goes to the rank whose share
+        of the cost range holds the midpoint of its cost -- and the claims follow that
+        plan; without, each claim goes online to the least loaded rank."""
         self.loads = [0] * self.world
+        self._plan, self._plan_pos = None, 0
+        if costs:
+            tot = float(sum(costs))
+            owners, cum = [], 0.0
+            for c in costs:
+                owners.append(min(self.world - 1, int((cum + 0.5 * c) * self.world / tot)))
+                cum += c
+            self._plan, self._plan_costs = owners, list(costs)
 
     def claim_owner(self, cost) -> int:
         """Assign the next slot of the batch (in scheduling order) to the rank with the
         least claimed cost so far, ties to the lowest rank, and return that rank.  Every
         rank makes the same calls in the same order, so all agree on every owner."""
         loads = self.loads
+        plan = getattr(self, "_plan", None)
+        if plan is not None and self._plan_pos < len(plan):
+            i = self._plan_pos
+            if int(cost) != int(self._plan_costs[i]):
+                raise RuntimeError("slot sharding: the schedule departed from the planned slot costs")
+            self._plan_pos += 1
+            loads[plan[i]] += int(cost)
+            return plan[i]
         r = loads.index(min(loads))  # the first (lowest) rank among the least loaded
         loads[r] += int(cost)
         return r

@@ -399,11 +399,36 @@ class PostTrainingEngine(RelevanceEngine):
         if fc >= 0:
             raise self._edit_error(calls[fc], code, k)
 
+    def _plan_costs(self, items):
+        """The claim cost of every slot the batch will schedule, in schedule order, without
+        drawing anything: a base slot (first call of an uncached prediction) costs its
+        base rows, a post-trained slot its rows after the edit (the costs _schedule_sharded
+        claims with); the list stops where the schedule stops (an edit that raises)."""
+        costs, pending = [], set()
+        for pred, triples, mode in self._calls(items):
+            pred = tuple(int(v) for v in pred)
+            view = self._get_kelpie_dataset(pred[0])
+            if pred not in self.base_pt_results and pred not in pending:
+                pending.add(pred)
+                costs.append(max(1, len(view.base_rows)))
+            edit = view.removed if mode == "necessary" else view.added
+            try:
+                n_pt, _ = edit(triples, rows=False)
+            except Exception:  # noqa: BLE001 -- the schedule raises there too
+                break
+            costs.append(max(1, n_pt))
+        return costs
+
     def _schedule_all(self, items, checkpoints):
         """_schedule_multi, with every queued TransE call's draws made before it returns or raises."""
         self._sched = None  # this batch's natively assembled slots (TransE), made on first use
         if self._sharded():
-            self.sharding.begin_batch()
+            # ComplEx / ConvE: every rank owns one contiguous run of the batch's slots, so it
+            # skips the others' draws in two long runs (before and after its own), each one
+            # MT19937 jump-ahead instead of a walk (kp_mt19937_discard); TransE's fused calls
+            # keep the online greedy claims (its numpy stream cannot be jumped)
+            fused = getattr(self.model, "fused_call_draws", False)
+            self.sharding.begin_batch(None if fused else self._plan_costs(items))
         try:
             return self._schedule_multi(items, checkpoints)
         finally:
@@ -702,6 +727,14 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
         equal to the sequential compute_relevance calls in that order."""
         return self._multi(items, checkpoints)
 
+    def _calls(self, items):
+        """(pred, rule, mode) of every call _schedule_multi makes, in order."""
+        for pred, rules in items:
+            for rule in rules:
+                yield pred, [tuple(t) for t in rule], "necessary"
+                if not rule:
+                    return
+
     def _schedule_multi(self, items, checkpoints):
         slots, pending, jobs = [], {}, []
         fast = checkpoints is None and getattr(self.model, "fused_call_draws", False)
@@ -760,6 +793,20 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
     def compute_relevance_multi(self, items, checkpoints: list | None = None):
         """[(pred, rules, entities_to_convert), ...] in ONE device batch."""
         return self._multi(items, checkpoints)
+
+    def _calls(self, items):
+        """(pred, rule, mode) of every call _schedule_multi makes, in order."""
+        for pred, rules, ents in items:
+            pred = tuple(int(v) for v in pred)
+            s = pred[0]
+            for rule in rules:
+                if not ents:
+                    return
+                for e in ents:
+                    crule = Dataset.replace_entity_in_triples([tuple(t) for t in rule], s, e)
+                    yield Dataset.replace_entity_in_triple(pred, s, e), crule, "sufficient"
+                    if not crule:
+                        return
 
     def _schedule_multi(self, items, checkpoints):
         slots, pending, jobs = [], {}, []

@@ -1,4 +1,7 @@
 """The host RNG protocol's shortcuts consume exactly what the reference's calls consume."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -304,3 +307,45 @@ def test_fused_transe_calls_match_reference_sequence():
                 assert np.array_equal(epochs(Rp), draws[i][1])
     assert torch.equal(torch.rand(3), after[0])
     assert np.array_equal(np.random.randint(0, 1 << 30, 4), after[1])
+
+
+_JUMP_SCRIPT = r"""
+import hashlib, json, sys
+import numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from kelpie_amd import _lib
+torch.manual_seed(321)
+base = torch.get_rng_state().numpy().copy()
+out = {}
+for pre in (0, 1, 300, 623):
+    st = base.copy()
+    if pre:
+        _lib.mt19937_discard(st, pre)
+    for n in (1, 623, 624, 625, 1248, 4369, 123457, 1946040, 30000001):
+        s2 = st.copy()
+        _lib.mt19937_discard(s2, n)
+        out[f"{pre}_{n}"] = hashlib.sha1(s2.tobytes()).hexdigest()
+st = base.copy()
+_lib.mt19937_discard(st, 30000001)
+torch.set_rng_state(torch.from_numpy(st))
+out["draw"] = torch.rand(8).tolist()
+print(json.dumps(out))
+"""
+
+
+def test_mt19937_jump_ahead_equals_the_walk():
+    """kp_mt19937_discard by MT19937 jump-ahead (GF(2) characteristic polynomial,
+    x^D mod P, Horner) leaves the torch generator exactly where the twist-by-twist walk
+    does, across block boundaries and from every in-block position; torch then draws
+    the same values.  KP_MT_JUMP_MIN=1 forces the jump for every skip past the block."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for jmin in ("0", "1"):
+        env = dict(os.environ, KP_MT_JUMP_MIN=jmin)
+        r = subprocess.run([sys.executable, "-c", _JUMP_SCRIPT, root], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert outs[0] == outs[1]

@@ -31,7 +31,7 @@ run_step() {
     tests)
       local k=()
       [ -n "${a[1]}" ] && k=(-k "${a[1]}")
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "${k[@]}" \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread "${k[@]}" \
         > $O/tests_${a[1]:-all}.txt 2>&1
       local rc=$?
       grep -E "passed|failed|error" $O/tests_${a[1]:-all}.txt | tail -2
@@ -107,6 +107,9 @@ run_step() {
           mv $O/bench_${w}_${var}_$v.json $O/ab_${w}_${var}_${v}_$rep.json
         done
       done ;;
+    fullsize)
+      timeout -k 10 900 python tools/fullsize_table.py $(echo ${a[1]} | tr ',' ' ') > $O/fullsize_table.jsonl 2> $O/fullsize_table.err || { tail -3 $O/fullsize_table.err; return 1; }
+      cut -c1-400 $O/fullsize_table.jsonl ;;
     rehearse)
       timeout -k 10 900 python tools/sched_rehearsal.py $(echo ${a[1]} | tr ',' ' ') > $O/rehearse_${a[1]//,/_}.txt 2>&1 || return 1
       tail -5 $O/rehearse_${a[1]//,/_}.txt ;;
