@@ -239,10 +239,9 @@ class ConvE(FrozenModel):
                        fmap_dropout=self.feature_map_dropout_rate)
 
     def er_vocab_sizes(self, rows: np.ndarray, batch_size: int, epochs: int):
-        pairs = {}
-        for h, r, _ in rows.tolist():
-            pairs.setdefault((h, r), None)
-        P = len(pairs)
+        # the distinct (head, relation) pairs of the rows (BCEOptimizer's er_vocab keys)
+        rows = np.asarray(rows, dtype=np.int64).reshape(-1, 3)
+        P = int(np.unique(rows[:, 0] * (int(rows[:, 1].max()) + 1) + rows[:, 1]).size) if len(rows) else 0
         per_epoch = [min(batch_size, P - s) for s in range(0, P, batch_size)]
         return per_epoch * epochs
 
