@@ -65,8 +65,11 @@ WORKLOADS = {
     "complex-fb15k237-sufficient-k100": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="sufficient",
                                              hp=COMPLEX_HP, candidates=20, convert=100, preds_per_step=1, depth=3,
                                              cpu_conversions=2),
+    # three batches in flight (round 5: 3,412 / 3,545 vs 3,225 / 3,347 cand/s at two, alternating
+    # on one box, profiles/r05/necessary_depth_ab.txt: at two the device idled 11 % of the time
+    # in 15-26 ms gaps at batch boundaries, profiles/r05/timeline_complex-fb15k237-necessary.txt)
     "complex-fb15k237-necessary": dict(model="ComplEx", shape="FB15k-237", dim=200, mode="necessary",
-                                       hp=COMPLEX_HP, candidates=20, preds_per_step=16),
+                                       hp=COMPLEX_HP, candidates=20, preds_per_step=16, depth=3),
     # BASELINE.json configs[1]
     "transe-fb15k237-necessary": dict(model="TransE", shape="FB15k-237", dim=200, mode="necessary",
                                       hp=TRANSE_HP, candidates=20, preds_per_step=16),

@@ -67,17 +67,7 @@ __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
                  : "s"(lds_base), "v"(gp)
                  : "memory");
 #else
-#ifdef KP_DMA_NO_LGKM_GUARD
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
-#else
-    // no LDS read of this wave may be in flight across the copy's issue: the compiler
-    // places its own reads (and their waits) freely around an asm statement, and a copy
-    // issued between two outstanding reads corrupted results
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(
-                     lds_base),
-                 "v"(gp)
-                 : "memory");
-#endif
 #endif
   }
 }

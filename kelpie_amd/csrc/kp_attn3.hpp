@@ -658,9 +658,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           l_run += lt;
         }
         };
-        // (the asm read form only: with the compiler-visible reads of the ConvE width the
-        // branch moved the compiler's LDS reads against the asm LDS-DMA burst and the
-        // results went wrong -- DESIGN.md section 5, the LDS-DMA hazard)
+        // (the asm read form only: on the compiler-visible read form of the ConvE width the
+        // same branch gave wrong, run-to-run different partials, with or without a
+        // lgkmcnt(0) before each asm LDS-DMA piece -- DESIGN.md section 5)
         if (KP_ATTN_FULLTILE && (ASM || KP_ATTN_FULLTILE_ALL) && k0 + KT <= key_end)
           weights(std::true_type{});
         else
