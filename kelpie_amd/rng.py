@@ -89,9 +89,29 @@ _skip = 0
 _torch_async = False
 
 
+# set when a background walk or draw task failed (sync): the generators then sit at a
+# state the reference never reaches, so every later draw or state read raises until the
+# caller reseeds and calls clear_poison(), or restores a StateCheckpoint
+_poisoned = None
+
+
+def clear_poison():
+    """Accept the generators' current state again after a failed background draw (call
+    after reseeding them)."""
+    global _poisoned
+    _poisoned = None
+
+
+def _check_poison():
+    if _poisoned is not None:
+        raise RuntimeError("reference RNG stream lost by a failed background draw (" + _poisoned + "); reseed the "
+                           "generators and call kelpie_amd.rng.clear_poison(), or restore a StateCheckpoint")
+
+
 def _torch_current():
     """Make torch's generator current: take the stream back from an asynchronous walk."""
     global _torch_async
+    _check_poison()
     if _torch_async:
         _torch_async = False
         st = torch.get_rng_state().numpy()
@@ -117,13 +137,15 @@ def sync():
         _outstanding = False
         try:
             _lib.rng_wait()
-        except Exception:
+        except Exception as exc:
             # a failed walk or draw task: the stream it carried is partial, so drop the
             # asynchronous state and the pending advance instead of installing either
-            # on a later draw, then report the failure
+            # on a later draw, mark the stream lost, then report the failure
+            global _poisoned
             _torch_async = False
             _skip = 0
             _inflight.clear()
+            _poisoned = repr(exc)
             raise
     _inflight.clear()
     _flush_skip()  # also takes the torch stream back from an asynchronous walk
@@ -190,6 +212,7 @@ class ReferenceRNG:
     def discard(self, n: int):
         """Advance the torch generator by n outputs (deferred to the next real draw)."""
         global _skip
+        _check_poison()
         if n > 0:
             _skip += int(n)
         if not self._defer_depth:
@@ -244,6 +267,7 @@ class ReferenceRNG:
         are complete on leaving :meth:`deferred` (or at once outside it).  ``want[i]``
         (bit 0 base, bit 1 pt; default all): an unwanted post-training's draws are not
         made, only the generators advance past them (its entry is an empty array)."""
+        _check_poison()
         global _outstanding, _torch_async
         addr = _np_mt_state_address()
         w = [3] * len(R_base) if want is None else list(want)
@@ -318,6 +342,11 @@ class StateCheckpoint:
         self.np_state = np.random.get_state()
 
     def restore(self):
-        sync()
+        global _poisoned
+        try:
+            sync()
+        except Exception:  # noqa: BLE001 -- the restored state replaces whatever was lost
+            pass
+        _poisoned = None
         torch.set_rng_state(self.torch_state)
         np.random.set_state(self.np_state)

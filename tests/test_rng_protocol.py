@@ -349,3 +349,31 @@ def test_mt19937_jump_ahead_equals_the_walk():
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     assert outs[0] == outs[1]
+
+
+def test_failed_background_draw_poisons_the_stream(monkeypatch):
+    """A failed background walk leaves the generators at a state the reference never
+    reaches: every later draw raises until the caller reseeds and clears the poison, or
+    restores a checkpoint."""
+    from kelpie_amd import rng as krng
+    cp = krng.StateCheckpoint()
+    r = ReferenceRNG()
+
+    def boom():
+        raise RuntimeError("walk failed")
+
+    monkeypatch.setattr(krng._lib, "rng_wait", boom)
+    monkeypatch.setattr(krng, "_outstanding", True)
+    with pytest.raises(RuntimeError, match="walk failed"):
+        krng.sync()
+    monkeypatch.undo()
+    with pytest.raises(RuntimeError, match="stream lost"):
+        r.rand_init(8)
+    with pytest.raises(RuntimeError, match="stream lost"):
+        r.discard(3)
+    cp.restore()  # a restored checkpoint is a known state again
+    assert r.rand_init(8).shape == (8,)
+    krng._poisoned = "x"
+    krng.clear_poison()
+    r.discard(2)
+    krng.sync()
