@@ -252,6 +252,17 @@ int kp_criage_relevance(kp_ctx* ctx, int32_t n, const int32_t* items, int32_t n_
  * construction makes (conve.py:46-52 via :202) without materialising them. */
 int kp_mt19937_discard(uint8_t* state, size_t state_len, uint64_t n);
 
+/* Batches of deferred draws (the host RNG protocol, kelpie_amd/rng.py): every task queued
+ * by kp_rng_transe_enqueue / kp_rng_transe_calls_async / kp_rng_conve_masks_enqueue is
+ * tagged with the batch open at the time (tasks queued by a task inherit its tag).
+ * kp_rng_batch_close closes the open batch and returns its id; kp_rng_batch_wait(id)
+ * returns once every task of the batches <= id is done, while later batches' tasks may
+ * still be queued or running -- so the thread that packs batch k waits for batch k's
+ * draws while the scheduling thread already queues batch k + 1's (kp_rng_wait waits
+ * for everything). */
+int kp_rng_batch_close(int64_t* id);
+int kp_rng_batch_wait(int64_t id);
+
 /* torch.empty(n).normal_(mean, std) on the CPU generator for float32, n >= 16
  * (ATen normal_fill / normal_fill_AVX2, aten/src/ATen/native/cpu/DistributionTemplates.h),
  * bit for bit, advancing the state blob like torch.  cap = 1 for torch's AVX2 / AVX512 CPU

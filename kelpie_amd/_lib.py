@@ -22,7 +22,7 @@ KP_OPT = {"Adagrad": 0, "Adam": 1, "SGD": 2}
 # symbols declared by include/kelpie_hip.h
 EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_rank", "kp_all_scores",
            "kp_convertible", "kp_mt19937_discard", "kp_last_timing", "kp_version", "kp_rng_bernoulli_bits",
-           "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_conve_masks", "kp_rng_conve_masks_enqueue", "kp_graph_create", "kp_graph_destroy",
+           "kp_rng_transe_epochs", "kp_rng_transe_enqueue", "kp_rng_wait", "kp_rng_batch_close", "kp_rng_batch_wait", "kp_rng_conve_masks", "kp_rng_conve_masks_enqueue", "kp_graph_create", "kp_graph_destroy",
            "kp_graph_last_error", "kp_graph_bfs", "kp_graph_set_classes", "kp_graph_dijkstra_pairs",
            "kp_predict_tails", "kp_dp_relevance", "kp_criage_relevance", "kp_hot_intervals", "kp_rng_normal",
            "kp_rng_transe_calls", "kp_train_epoch", "kp_read_tables", "kp_view_create", "kp_view_destroy",
@@ -97,6 +97,8 @@ def lib():
                                            C.c_int32, C.c_int64, C.c_void_p]
         L.kp_rng_transe_enqueue.argtypes = L.kp_rng_transe_epochs.argtypes
         L.kp_rng_wait.argtypes = []
+        L.kp_rng_batch_close.argtypes = [C.POINTER(C.c_int64)]
+        L.kp_rng_batch_wait.argtypes = [C.c_int64]
         L.kp_train_epoch.argtypes = [C.c_void_p, C.POINTER(HP), C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
         L.kp_read_tables.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.kp_rng_normal.argtypes = [C.c_void_p, C.c_size_t, C.c_int64, C.c_float, C.c_float, C.c_int32, C.c_void_p]
@@ -276,6 +278,18 @@ def torch_take(state: np.ndarray) -> bool:
 
 def rng_wait():
     check(lib().kp_rng_wait())
+
+
+def rng_batch_close() -> int:
+    """Close the open batch of deferred draws; returns its id (kp_rng_batch_close)."""
+    v = C.c_int64(0)
+    check(lib().kp_rng_batch_close(C.byref(v)))
+    return int(v.value)
+
+
+def rng_batch_wait(batch_id: int):
+    """Wait for every deferred draw of the batches <= batch_id (kp_rng_batch_wait)."""
+    check(lib().kp_rng_batch_wait(int(batch_id)))
 
 
 def _segments(segs):

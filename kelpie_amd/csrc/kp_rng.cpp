@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -799,6 +800,24 @@ struct Scratch {
 };
 using Task = std::function<void(Scratch&)>;
 
+// Batch tags of queued work (kp_rng_batch_close / kp_rng_batch_wait): every task carries
+// the batch that was open when it was queued -- or, queued from inside a task (the walk
+// queues shuffles, a shuffle queues its permutation chain), its parent's -- so a batch's
+// draws can be waited for while later batches' tasks are already queued behind them.
+std::atomic<int64_t> g_open_batch{1};
+thread_local int64_t t_task_batch = 0;  // the batch of the task this thread is running
+inline int64_t submit_tag() { return t_task_batch ? t_task_batch : g_open_batch.load(std::memory_order_acquire); }
+// per-batch pending counts of one queue (guarded by the queue's mutex)
+struct BatchPending {
+  std::map<int64_t, int64_t> n;
+  void add(int64_t tag) { ++n[tag]; }
+  void done(int64_t tag) {
+    auto it = n.find(tag);
+    if (it != n.end() && --it->second == 0) n.erase(it);
+  }
+  bool clear_upto(int64_t id) const { return n.empty() || n.begin()->first > id; }
+};
+
 // KP_RNG_STATS=1: per batch (at each kp_rng_wait), the busy time of the walker, the
 // sequential worker and the pool, and when the last task ended relative to the wait
 // call, on stderr (a diagnostic of where a batch's draw time goes; off by default)
@@ -847,14 +866,17 @@ class DrawQueue {
     if (!ensure_locked()) return false;
     // one wake-up per queued task, on the queue's own condition variable (a notify_all on a
     // shared one woke every pool thread for each of a batch's ~600 tasks)
+    const int64_t tag = submit_tag();
     if (seq) {
-      seq_.push_back(std::move(seq));
+      seq_.push_back(Item{std::move(seq), tag});
       ++pending_;
+      bp_.add(tag);
       cv_seq_.notify_one();
     }
     if (fill) {
-      fills_.push_back(std::move(fill));
+      fills_.push_back(Item{std::move(fill), tag});
       ++pending_;
+      bp_.add(tag);
       cv_fill_.notify_one();
     }
     return true;
@@ -866,6 +888,13 @@ class DrawQueue {
     fail_rc_ = KP_OK;
     return rc;
   }
+  // every task of the batches <= id done (later batches' tasks may still run); the
+  // first failure of any task so far (not cleared: wait() reports and clears it)
+  int wait_batch(int64_t id) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_done_.wait(lk, [&] { return bp_.clear_upto(id); });
+    return fail_rc_;
+  }
 
  private:
   bool ensure_locked() {
@@ -874,6 +903,7 @@ class DrawQueue {
     // first use, or a forked child (the parent's workers do not exist here)
     seq_.clear();
     fills_.clear();
+    bp_ = BatchPending();
     pending_ = 0;
     int nfill = 4;
     if (const char* e = std::getenv("KP_RNG_THREADS")) nfill = std::max(1, std::min(16, std::atoi(e)));
@@ -890,7 +920,7 @@ class DrawQueue {
     Scratch sc;
     const pid_t me = getpid();
     for (;;) {
-      Task t;
+      Item t;
       {
         std::unique_lock<std::mutex> lk(mu_);
         auto& q = sequential ? seq_ : fills_;
@@ -902,25 +932,34 @@ class DrawQueue {
       int rc = KP_OK;
       RngStats& st = rng_stats();
       const int64_t t0 = st.on ? RngStats::now() : 0;
+      t_task_batch = t.tag;
       try {
-        t(sc);
+        t.t(sc);
       } catch (const std::invalid_argument&) {
         rc = KP_EINVAL;
       } catch (...) {
         rc = KP_ENOMEM;
       }
+      t_task_batch = 0;
       if (st.on) {
         st.span(sequential ? st.seq_ns : st.pool_ns, t0);
         ++(sequential ? st.seq_tasks : st.pool_tasks);
       }
       std::lock_guard<std::mutex> lk(mu_);
       if (rc != KP_OK && fail_rc_ == KP_OK) fail_rc_ = rc;
-      if (--pending_ == 0) cv_done_.notify_all();
+      bp_.done(t.tag);
+      --pending_;
+      cv_done_.notify_all();
     }
   }
+  struct Item {
+    Task t;
+    int64_t tag = 0;
+  };
   std::mutex mu_;
   std::condition_variable cv_seq_, cv_fill_, cv_done_;
-  std::deque<Task> seq_, fills_;
+  std::deque<Item> seq_, fills_;
+  BatchPending bp_;
   int64_t pending_ = 0;
   int fail_rc_ = KP_OK;  // first failure of a queued task since the last wait()
   pid_t pid_ = 0;
@@ -985,10 +1024,19 @@ class TorchWalker {
       mt_.load(ts);
       carried_ = true;
     }
-    q_.push_back(std::move(task));
+    const int64_t tag = submit_tag();
+    q_.push_back(std::make_pair(std::move(task), tag));
     ++pending_;
+    bp_.add(tag);
     cv_work_.notify_all();
     return true;
+  }
+  // every walk of the batches <= id done (see DrawQueue::wait_batch); the carried stream
+  // stays with the walker
+  int wait_batch(int64_t id) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_done_.wait(lk, [&] { return bp_.clear_upto(id); });
+    return fail_rc_;
   }
   // wait for every queued walk; then, if a walk carries the stream, store it into ts and
   // release it (*taken = 1)
@@ -1013,6 +1061,7 @@ class TorchWalker {
     const pid_t me = getpid();
     if (pid_ == me) return true;
     q_.clear();
+    bp_ = BatchPending();
     pending_ = 0;
     carried_ = false;
     try {
@@ -1026,7 +1075,7 @@ class TorchWalker {
   void loop() {
     const pid_t me = getpid();
     for (;;) {
-      std::function<int(TorchMt&)> t;
+      std::pair<std::function<int(TorchMt&)>, int64_t> t;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_work_.wait(lk, [&] { return !q_.empty(); });
@@ -1037,22 +1086,27 @@ class TorchWalker {
       int rc;
       RngStats& st = rng_stats();
       const int64_t t0 = st.on ? RngStats::now() : 0;
+      t_task_batch = t.second;  // the shuffles it queues belong to the same batch
       try {
-        rc = t(mt_);  // mt_ is only touched here and under mu_ with the queue empty
+        rc = t.first(mt_);  // mt_ is only touched here and under mu_ with the queue empty
       } catch (const std::invalid_argument&) {
         rc = KP_EINVAL;
       } catch (...) {
         rc = KP_ENOMEM;
       }
+      t_task_batch = 0;
       if (st.on) st.span(st.walk_ns, t0);
       std::lock_guard<std::mutex> lk(mu_);
       if (rc != KP_OK && fail_rc_ == KP_OK) fail_rc_ = rc;
-      if (--pending_ == 0) cv_done_.notify_all();
+      bp_.done(t.second);
+      --pending_;
+      cv_done_.notify_all();
     }
   }
   std::mutex mu_;
   std::condition_variable cv_work_, cv_done_;
-  std::deque<std::function<int(TorchMt&)>> q_;
+  std::deque<std::pair<std::function<int(TorchMt&)>, int64_t>> q_;
+  BatchPending bp_;
   int64_t pending_ = 0;
   int fail_rc_ = KP_OK;
   bool carried_ = false;
@@ -1286,6 +1340,19 @@ int kp_rng_conve_masks_enqueue(uint8_t* ts, size_t tlen, int32_t n_steps, const 
     return KP_ENOMEM;
   }
   return KP_OK;
+}
+
+int kp_rng_batch_close(int64_t* id) {
+  if (!id) return KP_EINVAL;
+  *id = g_open_batch.fetch_add(1, std::memory_order_acq_rel);
+  return KP_OK;
+}
+
+int kp_rng_batch_wait(int64_t id) {
+  // the walks first: they queue the batch's shuffles and fills
+  const int rw = TorchWalker::get().wait_batch(id);
+  const int rd = DrawQueue::get().wait_batch(id);
+  return rw != KP_OK ? rw : rd;
 }
 
 int kp_rng_wait(void) {

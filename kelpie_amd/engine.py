@@ -647,14 +647,19 @@ class PostTrainingEngine(RelevanceEngine):
         if os.environ.get("KELPIE_GIL_SWITCH_US"):
             sys.setswitchinterval(float(os.environ["KELPIE_GIL_SWITCH_US"]) * 1e-6)
 
+        from . import rng as _rng_mod
+
         def run(state):
             try:
+                # this batch's deferred draws (the scheduling thread did not wait for them)
+                _rng_mod.wait_ticket(state.get("ticket"))
                 state["stats"] = dict(self._run(state["slots"], ctx=state["ctx"]))
             except BaseException as e:  # re-raised on the scheduling thread
                 state["error"] = e
 
         outs, stats, inflight = [], [], collections.deque()
         late_collect = os.environ.get("KELPIE_PIPELINE_EARLY_START", "1") == "0"  # A/B: collect, then start
+        detach = os.environ.get("KELPIE_PIPELINE_DETACH", "1") == "1"
 
         def finish(state):
             state["thread"].join()
@@ -675,8 +680,12 @@ class PostTrainingEngine(RelevanceEngine):
                 self.set_cache()
                 t0 = time.perf_counter()
                 self._deferred_error = None
-                with self.rng.deferred():
+                # detached: the next batch is scheduled while the workers still make this
+                # one's draws (TransE: the sequential numpy chain); the batch thread waits
+                # for them before packing (KELPIE_PIPELINE_DETACH=0: wait here, A/B)
+                with self.rng.deferred(detach=detach) as drng:
                     slots, pending, jobs = self._schedule_all(items, None)
+                ticket = drng.last_ticket
                 err, self._deferred_error = self._deferred_error, None
                 t_sched = time.perf_counter() - t0
                 # batch b uses context b % depth: the batch before it on that context is done.
@@ -693,7 +702,7 @@ class PostTrainingEngine(RelevanceEngine):
                         finish(d)  # raises the first device failure before batch b starts
                     done = []
                 state = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched, "error": None,
-                         "deferred": err, "ctx": ctxs[b % len(ctxs)]}
+                         "deferred": err, "ctx": ctxs[b % len(ctxs)], "ticket": ticket}
                 state["thread"] = threading.Thread(target=run, args=(state,), daemon=True)
                 state["thread"].start()
                 inflight.append(state)
@@ -709,6 +718,13 @@ class PostTrainingEngine(RelevanceEngine):
             sys.setswitchinterval(old_switch)
             if nogc:
                 gc.enable()
+            if sys.exc_info()[0] is None:
+                _rng_mod.sync()  # the generators are current again when the call returns
+            else:
+                try:
+                    _rng_mod.sync()
+                except Exception:  # noqa: BLE001 -- the error in flight is the one to report
+                    pass
         self.last_batch_stats = stats
         return outs
 

@@ -95,6 +95,19 @@ _torch_async = False
 _poisoned = None
 
 
+def wait_ticket(ticket):
+    """Wait for the draws of a detached deferred block (ReferenceRNG.deferred(detach=True))
+    and of every block before it; a failed draw marks the stream lost."""
+    global _poisoned
+    if ticket is None:
+        return
+    try:
+        _lib.rng_batch_wait(ticket)
+    except Exception as exc:
+        _poisoned = repr(exc)
+        raise
+
+
 def clear_poison():
     """Accept the generators' current state again after a failed background draw (call
     after reseeding them)."""
@@ -157,22 +170,33 @@ class ReferenceRNG:
     _defer_depth = 0
 
     @contextlib.contextmanager
-    def deferred(self):
+    def deferred(self, detach=False):
         """Inside this block :meth:`transe_epochs` returns arrays that the library's
         workers fill in the background (kp_rng_transe_enqueue): the caller keeps
         scheduling while the shuffles and randints of earlier slots are generated.
         The arrays are complete, and numpy's global state current, on exit (or
-        after :func:`sync`)."""
+        after :func:`sync`).
+
+        ``detach``: on exit the block's draws are only closed as one batch
+        (kp_rng_batch_close; ``self.last_ticket``) instead of waited for, so the caller
+        can schedule the next block while the workers still make these draws; whoever
+        reads this block's arrays first calls :func:`wait_ticket` (the pipeline's batch
+        thread, before packing).  The generators stay with the workers until the next
+        :func:`sync` (a state read or a torch draw on this thread syncs first)."""
         self._defer_depth += 1
         if self._defer_depth == 1:
             self._arena, self._arena_pos = None, 0
+        self.last_ticket = None
         try:
             yield self
         finally:
             self._defer_depth -= 1
             if self._defer_depth == 0:
                 self._arena = None
-                sync()
+                if detach and _outstanding and not _skip:
+                    self.last_ticket = _lib.rng_batch_close()
+                else:
+                    sync()
 
     # The deferred draws of one block are laid out back to back in an arena, so the
     # engine ships a batch's draws without concatenating them (engine._run).  A fresh
