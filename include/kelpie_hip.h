@@ -71,6 +71,9 @@ typedef struct {
   const float* fc_b;     /* [dim] */
   const float* bn_alpha; /* [1 + 32 + dim]: eval-mode BN1|BN2|BN3 scale  w/sqrt(var+eps) */
   const float* bn_beta;  /* [1 + 32 + dim]: eval-mode BN1|BN2|BN3 shift  b - mean*scale  */
+  /* TransE score norm p (TransEHyperParams.norm, transe.py:12-15,46; tune.py:19 searches
+   * {1, 2}): 2 = L2, 1 = L1, 0 = the default 2; must be 0 for the other models */
+  int32_t norm_p;
 } kp_model_desc;
 
 /* Post-training hyper-parameters (the *_explanation.json "training" block,

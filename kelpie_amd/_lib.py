@@ -34,7 +34,8 @@ EXPORTS = ["kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_posttrain_ran
 class ModelDesc(C.Structure):
     _fields_ = [("model", C.c_int32), ("n_ent", C.c_int32), ("n_rel2", C.c_int32), ("dim", C.c_int32),
                 ("entity", C.c_void_p), ("relation", C.c_void_p), ("conv_w", C.c_void_p), ("conv_b", C.c_void_p),
-                ("fc_w", C.c_void_p), ("fc_b", C.c_void_p), ("bn_alpha", C.c_void_p), ("bn_beta", C.c_void_p)]
+                ("fc_w", C.c_void_p), ("fc_b", C.c_void_p), ("bn_alpha", C.c_void_p), ("bn_beta", C.c_void_p),
+                ("norm_p", C.c_int32)]
 
 
 class HP(C.Structure):
@@ -333,12 +334,13 @@ def conve_masks(torch_state: np.ndarray, rows_per_step, segs) -> np.ndarray:
 class Context:
     """One device context holding the frozen model tables (kp_ctx)."""
 
-    def __init__(self, model_name, entity, relation, conve=None, device=0):
+    def __init__(self, model_name, entity, relation, conve=None, device=0, norm_p=0):
         L = lib()
         self._keep = []
         E = np.ascontiguousarray(entity, dtype=np.float32)
         R = np.ascontiguousarray(relation, dtype=np.float32)
         d = ModelDesc(KP_MODEL[model_name], E.shape[0], R.shape[0], E.shape[1], _ptr(E), _ptr(R))
+        d.norm_p = int(norm_p)
         self._keep += [E, R]
         if conve is not None:
             for k in ("conv_w", "conv_b", "fc_w", "fc_b", "bn_alpha", "bn_beta"):

@@ -78,6 +78,9 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     c->n_ent = m->n_ent;
     c->n_rel2 = m->n_rel2;
     c->dim = m->dim;
+    KP_REQUIRE(m->norm_p == 0 || (m->model == KP_MODEL_TRANSE && (m->norm_p == 1 || m->norm_p == 2)),
+               "kp_ctx_create: norm_p must be 1 or 2 (TransE) or 0");
+    c->te_norm = m->norm_p == 1 ? 1 : 2;
     KP_HIP(hipSetDevice(device));
     KP_HIP(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
     (void)kp_time_base(device, nullptr);

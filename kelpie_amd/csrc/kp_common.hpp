@@ -122,6 +122,7 @@ struct kp_ctx {
   bool eT_ready = false;
   int cv_fused = 1;        // ConvE d = 200: fused encoder kernels (kp_cv_fused.hpp), KP_CV_FUSED
   int cv_rank64 = 1;       // ConvE post-training rank on fp64 logits (KP_CV_RANK=f32: fp32 sigmoid scores)
+  int te_norm = 2;         // TransE score norm p (kp_model_desc.norm_p): 2 or 1
   int te_rank64 = 1;       // TransE post-training rank on fp64 squared distances (KP_TE_RANK=f32: fp32 norms)
   DevBuf cvf_fw3, cvf_bw3;  // their permuted split images of the FC weight (built once)
   bool cvf_ready = false;
@@ -240,7 +241,7 @@ enum { RANK_TRIPLE_RESULTS = 0, RANK_PREDICT_TAILS = 1, RANK_SORT_POSITION = 2 }
 // over the frozen entities (scores q . E_e summed in fp64, sequentially over d) plus the
 // kelpie column.  The target itself counts unless filtered.
 // launch_rank_f64's score kinds
-enum { RANK64_DOT = 0, RANK64_SIGMOID = 1, RANK64_DIST = 2 };
+enum { RANK64_DOT = 0, RANK64_SIGMOID = 1, RANK64_DIST = 2, RANK64_DIST1 = 3 };
 void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* d_t64, const double* d_kcol64,
                      const int32_t* d_pred_o, const int32_t* d_filt_off, const int32_t* d_filt, float* d_target,
                      int64_t* d_rank, int act = 0);

@@ -212,7 +212,8 @@ __global__ __launch_bounds__(256) void kp_rank_filter_bits(int n_slots, int nwor
 // act RANK64_DOT: the scores are the fp64 values (ComplEx); RANK64_SIGMOID: the scores
 // are sigmoid(logit) and the rank compares the monotone logits (ConvE); RANK64_DIST: a
 // minimizer whose scores are L2 distances and the rank compares their squares (TransE:
-// get_triple_results' minimizer branch, the target counting itself even when filtered)
+// get_triple_results' minimizer branch, the target counting itself even when filtered);
+// RANK64_DIST1: the same minimizer on L1 distances (TransE norm p = 1)
 __global__ void kp_rank_f64_kelpie(int n_slots, int n_ent, int nwords, const uint32_t* __restrict__ bits,
                                    const int32_t* __restrict__ pred_o, const double* __restrict__ t64,
                                    const double* __restrict__ kcol64, int act, float* __restrict__ target_out,
@@ -220,16 +221,17 @@ __global__ void kp_rank_f64_kelpie(int n_slots, int n_ent, int nwords, const uin
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_slots) return;
   const bool filtered = (bits[(size_t)s * nwords + (n_ent >> 5)] >> (n_ent & 31)) & 1u;
-  if (act == RANK64_DIST)
+  if (act == RANK64_DIST || act == RANK64_DIST1)
     rank[s] = (pred_o[s] == n_ent || (!filtered && kcol64[s] <= t64[s])) ? 1ull : 0ull;
   else
     rank[s] = (!filtered && kcol64[s] >= t64[s]) ? 1ull : 0ull;
   target_out[s] = act == RANK64_SIGMOID ? (float)(1.0 / (1.0 + exp(-t64[s])))
                   : act == RANK64_DIST  ? (float)sqrt(t64[s])
-                                        : (float)t64[s];
+                                        : (float)t64[s];  // DOT, DIST1
 }
 
-template <bool DIST>
+// MODE: RANK64_DOT (dot products, maximizer), RANK64_DIST (squared L2), RANK64_DIST1 (L1)
+template <int MODE>
 __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent, int dp, const double* __restrict__ Q,
                                                          const double* __restrict__ t64,
                                                          const int32_t* __restrict__ pred_o, const float* __restrict__ ET,
@@ -249,9 +251,11 @@ __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent,
 #pragma unroll
     for (int j = 0; j < RQ; ++j)
       if (j < ns) {
-        if constexpr (DIST) {
+        if constexpr (MODE == RANK64_DIST) {
           const double df = q[(size_t)j * dp + d] - v;  // exact: fp32 operands, fp64 difference
           acc[j] = __fma_rn(df, df, acc[j]);
+        } else if constexpr (MODE == RANK64_DIST1) {
+          acc[j] += fabs(q[(size_t)j * dp + d] - v);
         } else {
           acc[j] = __fma_rn(q[(size_t)j * dp + d], v, acc[j]);
         }
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent,
       const bool filtered = (bits[(size_t)s * nwords + (e >> 5)] >> (e & 31)) & 1u;
       // the target counts itself whatever the rounding of its own score (a maximizer's
       // only if unfiltered: its filtered score is set back after the count)
-      if constexpr (DIST)
+      if constexpr (MODE != RANK64_DOT)
         hit = e == pred_o[s] || (!filtered && acc[j] <= t64[s]);
       else
         hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s]);
@@ -304,12 +308,16 @@ void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* 
   hipLaunchKernelGGL(kp_rank_f64_kelpie, dim3((n_slots + 63) / 64), dim3(64), 0, c->stream, n_slots, c->n_ent, nwords,
                      bits, d_pred_o, d_t64, d_kcol64, act, d_target, rank);
   KP_HIP(hipGetLastError());
+  const dim3 grid(ldt / 256, (n_slots + RQ - 1) / RQ);
   if (act == RANK64_DIST)
-    hipLaunchKernelGGL(kp_rank_f64_count<true>, dim3(ldt / 256, (n_slots + RQ - 1) / RQ), dim3(256), 0, c->stream,
-                       n_slots, c->n_ent, c->dp, d_q64, d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
+    hipLaunchKernelGGL(kp_rank_f64_count<RANK64_DIST>, grid, dim3(256), 0, c->stream, n_slots, c->n_ent, c->dp, d_q64,
+                       d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
+  else if (act == RANK64_DIST1)
+    hipLaunchKernelGGL(kp_rank_f64_count<RANK64_DIST1>, grid, dim3(256), 0, c->stream, n_slots, c->n_ent, c->dp, d_q64,
+                       d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
   else
-    hipLaunchKernelGGL(kp_rank_f64_count<false>, dim3(ldt / 256, (n_slots + RQ - 1) / RQ), dim3(256), 0, c->stream,
-                       n_slots, c->n_ent, c->dp, d_q64, d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
+    hipLaunchKernelGGL(kp_rank_f64_count<RANK64_DOT>, grid, dim3(256), 0, c->stream, n_slots, c->n_ent, c->dp, d_q64,
+                       d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
   KP_HIP(hipGetLastError());
 }
 

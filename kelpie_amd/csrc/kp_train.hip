@@ -188,9 +188,10 @@ __global__ void kp_tr_opt(float* __restrict__ X, float* __restrict__ S1, float* 
 // negative factors): roles 0..2 = positive lhs, rel, rhs; 3..5 = negative ones.
 //   score = ||lhs + rel - rhs||,  hinge_i = score_pos - score_neg + margin > 0
 //   d lhs = (+-1 / B) (lhs + rel - rhs) / score [hinge] + (w / (3 B d)) lhs, etc.
+// l1 (norm p = 1): score = sum |lhs + rel - rhs|, d lhs = (+-1 / B) sgn(lhs + rel - rhs) [hinge] + ...
 __global__ void kp_tr_te_rowgrads(const float* __restrict__ E, const float* __restrict__ R, int dp, int dim,
                                   const int32_t* __restrict__ pos, const int32_t* __restrict__ neg, int B,
-                                  float margin, float inv_b, float wl, float* __restrict__ grads) {
+                                  float margin, float inv_b, float wl, int l1, float* __restrict__ grads) {
   const int i = blockIdx.x;
   if (i >= B) return;
   const int lane = threadIdx.x;  // one wave per row
@@ -201,19 +202,23 @@ __global__ void kp_tr_te_rowgrads(const float* __restrict__ E, const float* __re
   float sp = 0.f, sn = 0.f;
   for (int d = lane; d < dim; d += 64) {
     const float a = (ph[d] + pr[d]) - pt[d], b = (nh[d] + nr[d]) - nt[d];
-    sp += a * a;
-    sn += b * b;
+    sp += l1 ? fabsf(a) : a * a;
+    sn += l1 ? fabsf(b) : b * b;
   }
   sp = wave_sum(sp);
   sn = wave_sum(sn);
-  const float np_ = sqrtf(sp), nn = sqrtf(sn);
+  const float np_ = l1 ? sp : sqrtf(sp), nn = l1 ? sn : sqrtf(sn);
   const bool hinge = (np_ - nn) + margin > 0.f;
-  const float cp = hinge ? inv_b / np_ : 0.f, cn = hinge ? -inv_b / nn : 0.f;
+  const float cp = hinge ? (l1 ? inv_b : inv_b / np_) : 0.f, cn = hinge ? (l1 ? -inv_b : -inv_b / nn) : 0.f;
   float* g = grads + (size_t)i * 6 * dp;
   for (int d = lane; d < dp; d += 64) {
     float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (d < dim) {
-      const float a = (ph[d] + pr[d]) - pt[d], b = (nh[d] + nr[d]) - nt[d];
+      float a = (ph[d] + pr[d]) - pt[d], b = (nh[d] + nr[d]) - nt[d];
+      if (l1) {
+        a = a > 0.f ? 1.f : (a < 0.f ? -1.f : 0.f);
+        b = b > 0.f ? 1.f : (b < 0.f ? -1.f : 0.f);
+      }
       v[0] = cp * a + wl * ph[d];
       v[1] = cp * a + wl * pr[d];
       v[2] = -cp * a + wl * pt[d];
@@ -509,7 +514,8 @@ void transe_train_epoch(kp_ctx* c, const kp_hp* hp, int n, const int32_t* pos, c
     const float inv_b = 1.0f / (float)B;
     const float wl = hp->reg_weight / (3.0f * (float)B * (float)dim);
     hipLaunchKernelGGL(kp_tr_te_rowgrads, dim3(B), dim3(64), 0, c->stream, c->dE, c->dR, dp, dim,
-                       dpos + 3 * (size_t)start, dneg + 3 * (size_t)start, B, hp->margin, inv_b, wl, grads);
+                       dpos + 3 * (size_t)start, dneg + 3 * (size_t)start, B, hp->margin, inv_b, wl,
+                       c->te_norm == 1 ? 1 : 0, grads);
     KP_HIP(hipGetLastError());
     KP_HIP(hipMemsetAsync(gE, 0, 4 * nE, c->stream));
     KP_HIP(hipMemsetAsync(gR, 0, 4 * nR, c->stream));

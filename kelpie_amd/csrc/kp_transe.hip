@@ -8,7 +8,8 @@
 //   of batch_size; negatives corrupt the head (head_or_tail == 1) or the tail
 //   with a random entity in [0, |E|] (the kelpie id included, A-Q3);
 //   loss = mean(max(0, f+ - f- + margin)) + lambda * (L2(pos) + L2(neg)) / 2,
-//   f = ||lhs + rel - rhs||_2, L2 = (mean lhs^2 + mean rel^2 + mean rhs^2) / 3;
+//   f = ||lhs + rel - rhs||_p (p = 2, or 1: transe.py:46, tune.py:19),
+//   L2 = (mean lhs^2 + mean rel^2 + mean rhs^2) / 3;
 //   Adam(lr) on the kelpie row only.
 //
 // One workgroup per slot runs every epoch on chip (x and the Adam moments in
@@ -122,7 +123,11 @@ __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlan
 // dropped from the norms; their gradient lanes are never stored).  The kernel is
 // bound by VALU issue (tools/te_times.py): the selects below are per-lane with
 // wave-uniform masks; forcing them into scalar branches was measured 1.9x slower.
-template <int VPL>
+__device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
+
+// L1 (norm p = 1): f = sum |v| and d f / d v = sgn(v) with sgn(0) = 0 (torch's p = 1 norm
+// backward); the per-pair coefficient is then +-1 instead of +-1 / f
+template <int VPL, bool L1>
 __device__ __forceinline__ void te_item(const int4* rec, const float* __restrict__ E, const float* __restrict__ Rt,
                                         const float4* x4, const int* fo, const bool* on, float margin, float4* g,
                                         int& cnt) {
@@ -150,7 +155,8 @@ __device__ __forceinline__ void te_item(const int4* rec, const float* __restrict
     const float4 b = bb[u];
     lb[u] = make_float4(lp.x + b.x, lp.y + b.y, lp.z + b.z, lp.w + b.w);
     vp[u] = make_float4(lb[u].x - rp[u].x, lb[u].y - rp[u].y, lb[u].z - rp[u].z, lb[u].w - rp[u].w);
-    const float s = fmaf(vp[u].x, vp[u].x, fmaf(vp[u].y, vp[u].y, fmaf(vp[u].z, vp[u].z, vp[u].w * vp[u].w)));
+    const float s = L1 ? (fabsf(vp[u].x) + fabsf(vp[u].y)) + (fabsf(vp[u].z) + fabsf(vp[u].w))
+                       : fmaf(vp[u].x, vp[u].x, fmaf(vp[u].y, vp[u].y, fmaf(vp[u].z, vp[u].z, vp[u].w * vp[u].w)));
     sp += on[u] ? s : 0.f;
   }
   float4 vn[TE_NB][VPL];
@@ -169,8 +175,9 @@ __device__ __forceinline__ void te_item(const int4* rec, const float* __restrict
         v = make_float4((bq.x + b.x) - rp[u].x, (bq.y + b.y) - rp[u].y, (bq.z + b.z) - rp[u].z, (bq.w + b.w) - rp[u].w);
       else  // corrupted tail: (lhs + rel) - e_n
         v = make_float4(lb[u].x - bq.x, lb[u].y - bq.y, lb[u].z - bq.z, lb[u].w - bq.w);
-      vn[q][u] = v;
-      const float s = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+      const float s = L1 ? (fabsf(v.x) + fabsf(v.y)) + (fabsf(v.z) + fabsf(v.w))
+                         : fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+      vn[q][u] = L1 ? make_float4(sgnf(v.x), sgnf(v.y), sgnf(v.z), sgnf(v.w)) : v;
       sn[q] += on[u] ? s : 0.f;
     }
   }
@@ -178,17 +185,17 @@ __device__ __forceinline__ void te_item(const int4* rec, const float* __restrict
   sp = row16_sum_f(sp);
 #pragma unroll
   for (int q = 0; q < TE_NB; ++q) sn[q] = row16_sum_f(sn[q]);
-  const float fp = sqrtf(wave_fold_u(sp));
+  const float fp = L1 ? wave_fold_u(sp) : sqrtf(wave_fold_u(sp));
   int n_act = 0;
 #pragma unroll
   for (int q = 0; q < TE_NB; ++q) {
-    const float fn = sqrtf(wave_fold_u(sn[q]));
+    const float fn = L1 ? wave_fold_u(sn[q]) : sqrtf(wave_fold_u(sn[q]));
     if (q >= nb) continue;
     const bool act = (fp - fn) + margin >= 0.f;  // clamp_min backward passes grad where self >= min
     n_act += act ? 1 : 0;
     const int sgn_n = ((sgnb >> (2 * q)) & 3) - 1;
     if (act && sgn_n != 0 && fn > 0.f) {  // negatives without the kelpie entity: hinge only
-      const float cn = -(float)sgn_n / fn;
+      const float cn = L1 ? -(float)sgn_n : -(float)sgn_n / fn;
 #pragma unroll
       for (int u = 0; u < VPL; ++u) {
         g[u].x = fmaf(cn, vn[q][u].x, g[u].x);
@@ -200,13 +207,14 @@ __device__ __forceinline__ void te_item(const int4* rec, const float* __restrict
   }
   const int sgn_p = (hk ? 1 : 0) - (tk ? 1 : 0);
   if (n_act > 0 && sgn_p != 0 && fp > 0.f) {
-    const float cps = (float)n_act * ((float)sgn_p / fp);
+    const float cps = L1 ? (float)(n_act * sgn_p) : (float)n_act * ((float)sgn_p / fp);
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
-      g[u].x = fmaf(cps, vp[u].x, g[u].x);
-      g[u].y = fmaf(cps, vp[u].y, g[u].y);
-      g[u].z = fmaf(cps, vp[u].z, g[u].z);
-      g[u].w = fmaf(cps, vp[u].w, g[u].w);
+      const float4 w = L1 ? make_float4(sgnf(vp[u].x), sgnf(vp[u].y), sgnf(vp[u].z), sgnf(vp[u].w)) : vp[u];
+      g[u].x = fmaf(cps, w.x, g[u].x);
+      g[u].y = fmaf(cps, w.y, g[u].y);
+      g[u].z = fmaf(cps, w.z, g[u].z);
+      g[u].w = fmaf(cps, w.w, g[u].w);
     }
   }
   cnt += rfl(r0.w);
@@ -233,7 +241,7 @@ __device__ __forceinline__ void te_item(const int4* rec, const float* __restrict
 // row-gather round per bundle, two barriers and the Adam step per epoch.  NT = 1024
 // threads per workgroup (1024: one per CU; 512 for diagnostics).
 // STAGED = false (slots too long for the LDS buffers) reads the descriptors from memory.
-template <int VPL, int NT, bool STAGED>  // VPL float4 per lane: dp <= 256 * VPL
+template <int VPL, int NT, bool STAGED, bool L1>  // VPL float4 per lane: dp <= 256 * VPL
 __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, const float* __restrict__ E,
                                                           const float* __restrict__ Rt,
                                                           const TeSlot* __restrict__ slots,
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
 #ifdef KP_TE_STAMPS
           const long long c1 = __builtin_amdgcn_s_memtime();
 #endif
-          te_item<VPL>(recs + 3 * k, E, Rt, x4, fo, on, hp.margin, g, cnt);
+          te_item<VPL, L1>(recs + 3 * k, E, Rt, x4, fo, on, hp.margin, g, cnt);
 #ifdef KP_TE_STAMPS
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           st_comp += __builtin_amdgcn_s_memtime() - c1;
@@ -397,15 +405,15 @@ __global__ __launch_bounds__(NT) void kp_te_posttrain(int n_ent, int dp, int d, 
 #endif
 }
 
-// scores[q][e] = || (lhs_q + rel_q) - E_e ||_2 for e < n_ent (transe.py:48-65);
-// lhs_q is a frozen row (heads[q] >= 0) or the slot's kelpie row X[q].
+// scores[q][e] = || (lhs_q + rel_q) - E_e ||_p for e < n_ent (transe.py:48-65), p = 2
+// or 1 (l1); lhs_q is a frozen row (heads[q] >= 0) or the slot's kelpie row X[q].
 #define TS_Q 8
 __global__ __launch_bounds__(256) void kp_te_scores(int n_ent, int dp, const float* __restrict__ E,
                                                     const float* __restrict__ R, int nq,
                                                     const int32_t* __restrict__ heads,
                                                     const int32_t* __restrict__ rels,
                                                     const float* __restrict__ X, float* __restrict__ out, int ld,
-                                                    int kcol) {
+                                                    int kcol, int l1) {
   extern __shared__ __attribute__((aligned(16))) float tq[];  // [TS_Q][dp]
   const int q0 = blockIdx.y * TS_Q;
   for (int i = threadIdx.x; i < TS_Q * dp; i += blockDim.x) {
@@ -431,12 +439,12 @@ __global__ __launch_bounds__(256) void kp_te_scores(int n_ent, int dp, const flo
       for (int q = 0; q < TS_Q; ++q) {
         const float4 t = *reinterpret_cast<const float4*>(tq + q * dp + k);
         const float a = t.x - v.x, b = t.y - v.y, c = t.z - v.z, w = t.w - v.w;
-        acc[q] += a * a + b * b + c * c + w * w;
+        acc[q] += l1 ? (fabsf(a) + fabsf(b)) + (fabsf(c) + fabsf(w)) : a * a + b * b + c * c + w * w;
       }
     }
 #pragma unroll
     for (int q = 0; q < TS_Q; ++q)
-      if (q0 + q < nq) out[(size_t)(q0 + q) * ld + e] = sqrtf(acc[q]);
+      if (q0 + q < nq) out[(size_t)(q0 + q) * ld + e] = l1 ? acc[q] : sqrtf(acc[q]);
   }
   // kelpie column: || (x + r) - x ||
   if (kcol >= 0 && blockIdx.x == 0 && threadIdx.x < TS_Q) {
@@ -445,9 +453,9 @@ __global__ __launch_bounds__(256) void kp_te_scores(int n_ent, int dp, const flo
       float acc = 0.f;
       for (int k = 0; k < dp; ++k) {
         const float dlt = tq[threadIdx.x * dp + k] - X[(size_t)q * dp + k];
-        acc += dlt * dlt;
+        acc += l1 ? fabsf(dlt) : dlt * dlt;
       }
-      out[(size_t)q * ld + kcol] = sqrtf(acc);
+      out[(size_t)q * ld + kcol] = l1 ? acc : sqrtf(acc);
     }
   }
 }
@@ -458,19 +466,20 @@ void launch_te_scores(kp_ctx* c, int nq, const int32_t* dh, const int32_t* dr, c
   dim3 grid((c->n_ent + 255) / 256, (nq + TS_Q - 1) / TS_Q);
   const size_t shm = sizeof(float) * TS_Q * c->dp;
   hipLaunchKernelGGL(kp_te_scores, grid, dim3(256), shm, c->stream, c->n_ent, c->dp, c->dE, c->dR, nq, dh, dr, dX,
-                     dOut, ld, kcol);
+                     dOut, ld, kcol, c->te_norm == 1 ? 1 : 0);
   KP_HIP(hipGetLastError());
 }
 
-// fp64 ranking queries (launch_rank_f64, RANK64_DIST): the translation q = x + R_p of
-// the post-trained row in fp64 (exact: two fp32 operands), its squared distance to the
-// target and to the kelpie row as one sequential fp64 FMA chain over d, the order
+// fp64 ranking queries (launch_rank_f64, RANK64_DIST / RANK64_DIST1): the translation
+// q = x + R_p of the post-trained row in fp64 (exact: two fp32 operands), its squared
+// distance (L1: its |.| sum) to the target and to the kelpie row as one sequential fp64
+// chain over d, the order
 // kp_rank_f64_count scores every entity in.  An fp32 norm over 200 terms is ~1e-7
 // relative off, enough to swap near-tied entities (FB15k-237 necessary fixtures).
 __global__ void kp_te_rankq64(const float* __restrict__ X, const float* __restrict__ R,
                               const float* __restrict__ E, int n_ent, int dp, const int32_t* __restrict__ pred,
                               int n_slots, double* __restrict__ Q, double* __restrict__ t64,
-                              double* __restrict__ kcol64) {
+                              double* __restrict__ kcol64, int l1) {
   const int s = blockIdx.x;
   if (s >= n_slots) return;
   const float* x = X + (size_t)s * dp;
@@ -483,13 +492,13 @@ __global__ void kp_te_rankq64(const float* __restrict__ X, const float* __restri
     double z = 0.0, t = 0.0;
     for (int d = 0; d < dp; ++d) {
       const double df = q[d] - (double)x[d];
-      z = __fma_rn(df, df, z);
+      z = l1 ? z + fabs(df) : __fma_rn(df, df, z);
     }
     if (o < n_ent) {
       const float* eo = E + (size_t)o * dp;
       for (int d = 0; d < dp; ++d) {
         const double df = q[d] - (double)eo[d];
-        t = __fma_rn(df, df, t);
+        t = l1 ? t + fabs(df) : __fma_rn(df, df, t);
       }
     } else {
       t = z;  // the kelpie entity is its own object
@@ -504,6 +513,7 @@ __global__ void kp_te_rankq64(const float* __restrict__ X, const float* __restri
 void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   const int ns = bt->n_slots;
   const int DP = c->dp;
+  const bool l1 = c->te_norm == 1;
   KP_REQUIRE(hp->neg_ratio >= 1 && hp->batch_size >= 1 && hp->epochs >= 0, "TransE: bad hyper-parameters");
   std::vector<TeSlot> slots(ns);
   for (int s = 0; s < ns; ++s) {
@@ -559,14 +569,20 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   hipEvent_t ea = c->event(0), eb = c->event(1);
   KP_HIP(hipEventRecord(ea, c->stream));
   const int vpl = (DP + 255) / 256;
-#define TE_LAUNCH(V, T, ST)                                                                                    \
-  hipLaunchKernelGGL((kp_te_posttrain<V, T, ST>), dim3(ns), dim3(T), shm, c->stream, c->n_ent, DP, c->dim, c->dE, \
+#define TE_LAUNCH(V, T, ST, L)                                                                                   \
+  hipLaunchKernelGGL((kp_te_posttrain<V, T, ST, L>), dim3(ns), dim3(T), shm, c->stream, c->n_ent, DP, c->dim, c->dE, \
                      c->dR, dSlots, dOrder, dRows, dRng, h, dX)
-#define TE_STAGE(V, T) \
-  if (staged)          \
-    TE_LAUNCH(V, T, true); \
-  else                 \
-    TE_LAUNCH(V, T, false)
+#define TE_NORM(V, T, ST)     \
+  if (l1)                     \
+    TE_LAUNCH(V, T, ST, true); \
+  else                        \
+    TE_LAUNCH(V, T, ST, false)
+#define TE_STAGE(V, T)      \
+  if (staged) {             \
+    TE_NORM(V, T, true);    \
+  } else {                  \
+    TE_NORM(V, T, false);   \
+  }
   if (vpl == 1) {
     if (nt == 1024) {
       TE_STAGE(1, 1024);
@@ -577,11 +593,12 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     TE_STAGE(2, 512);
   }
 #undef TE_STAGE
+#undef TE_NORM
 #undef TE_LAUNCH
   KP_HIP(hipGetLastError());
   KP_HIP(hipEventRecord(eb, c->stream));
 
-  // ---- rank: scores of (kelpie, p, .) = ||(x + R_p) - E_e||, minimizer
+  // ---- rank: scores of (kelpie, p, .) = ||(x + R_p) - E_e||_p, minimizer
   const int ld = round_up(c->n_ent + 1, 4);
   std::vector<int32_t> heads(ns, -1), rels(ns), po(ns);
   for (int s = 0; s < ns; ++s) {
@@ -601,9 +618,9 @@ void transe_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
     double* dQ64 = reinterpret_cast<double*>(c->ws[29].ensure(sizeof(double) * (size_t)ns * DP));
     double* dT64 = reinterpret_cast<double*>(c->ws[30].ensure(sizeof(double) * 2 * (size_t)ns));
     hipLaunchKernelGGL(kp_te_rankq64, dim3(ns), dim3(64), 0, c->stream, dX, c->dR, c->dE, c->n_ent, DP, dPred, ns,
-                       dQ64, dT64, dT64 + ns);
+                       dQ64, dT64, dT64 + ns, l1 ? 1 : 0);
     KP_HIP(hipGetLastError());
-    launch_rank_f64(c, ns, dQ64, dT64, dT64 + ns, dPo, dFo, dF, dTarget, dRank, RANK64_DIST);
+    launch_rank_f64(c, ns, dQ64, dT64, dT64 + ns, dPo, dFo, dF, dTarget, dRank, l1 ? RANK64_DIST1 : RANK64_DIST);
   } else {
     float* dScores = reinterpret_cast<float*>(c->ws[9].ensure(sizeof(float) * (size_t)ns * ld));
     launch_te_scores(c, ns, dH, dRl, dX, dScores, ld, c->n_ent);

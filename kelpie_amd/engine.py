@@ -649,11 +649,24 @@ class PostTrainingEngine(RelevanceEngine):
 
         from . import rng as _rng_mod
 
+        # KELPIE_PIPELINE_TRACE=<path>: a JSON list of (seconds, event, batch) per pipeline
+        # stage, for host timelines (diagnostics; tools/pipeline_trace.py)
+        trace_path = os.environ.get("KELPIE_PIPELINE_TRACE")
+        trace = [] if trace_path else None
+
+        def tr(ev, b):
+            if trace is not None:
+                trace.append((time.perf_counter(), ev, b))
+
         def run(state):
             try:
+                b = state["b"]
+                tr("run", b)
                 # this batch's deferred draws (the scheduling thread did not wait for them)
                 _rng_mod.wait_ticket(state.get("ticket"))
+                tr("draws", b)
                 state["stats"] = dict(self._run(state["slots"], ctx=state["ctx"]))
+                tr("ran", b)
             except BaseException as e:  # re-raised on the scheduling thread
                 state["error"] = e
 
@@ -663,6 +676,7 @@ class PostTrainingEngine(RelevanceEngine):
 
         def finish(state):
             state["thread"].join()
+            tr("finish", state["b"])
             if state.get("error") is not None:
                 raise state["error"]
             self.base_pt_results = {}
@@ -673,12 +687,14 @@ class PostTrainingEngine(RelevanceEngine):
             stats.append(st)
             outs.append(o)
             self._deferred_error = state.get("deferred")
+            tr("finished", state["b"])
             self._raise_deferred(state["slots"], state["pending"])
 
         try:
             for b, items in enumerate(batches):
                 self.set_cache()
                 t0 = time.perf_counter()
+                tr("schedule", b)
                 self._deferred_error = None
                 # detached: the next batch is scheduled while the workers still make this
                 # one's draws (TransE: the sequential numpy chain); the batch thread waits
@@ -688,6 +704,7 @@ class PostTrainingEngine(RelevanceEngine):
                 ticket = drng.last_ticket
                 err, self._deferred_error = self._deferred_error, None
                 t_sched = time.perf_counter() - t0
+                tr("scheduled", b)
                 # batch b uses context b % depth: the batch before it on that context is done.
                 # Its device work is waited for first and batch b started on the freed context,
                 # then its results are collected: the collection (and the gather, sharded) runs
@@ -696,13 +713,14 @@ class PostTrainingEngine(RelevanceEngine):
                 while len(inflight) >= len(ctxs):
                     old = inflight.popleft()
                     old["thread"].join()
+                    tr("joined", old["b"])
                     done.append(old)
                 if late_collect or any(d.get("error") is not None for d in done):
                     for d in done:
                         finish(d)  # raises the first device failure before batch b starts
                     done = []
                 state = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched, "error": None,
-                         "deferred": err, "ctx": ctxs[b % len(ctxs)], "ticket": ticket}
+                         "deferred": err, "ctx": ctxs[b % len(ctxs)], "ticket": ticket, "b": b}
                 state["thread"] = threading.Thread(target=run, args=(state,), daemon=True)
                 state["thread"].start()
                 inflight.append(state)
@@ -718,6 +736,10 @@ class PostTrainingEngine(RelevanceEngine):
             sys.setswitchinterval(old_switch)
             if nogc:
                 gc.enable()
+            if trace is not None:
+                import json
+                with open(trace_path, "a") as f:
+                    f.write(json.dumps(trace) + "\n")
             if sys.exc_info()[0] is None:
                 _rng_mod.sync()  # the generators are current again when the call returns
             else:

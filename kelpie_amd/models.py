@@ -152,15 +152,20 @@ class ComplEx(FrozenModel):
 
 
 class TransE(FrozenModel):
-    """TransE (transe.py:17-82): L2 distance, minimizer."""
+    """TransE (transe.py:17-82): L_p distance (p = ``norm``, 2 or 1: transe.py:46,
+    tune.py:19), minimizer."""
 
     name = "TransE"
 
     def __init__(self, dataset, entity_embeddings, relation_embeddings, norm=2, device=0):
         super().__init__(dataset, entity_embeddings, relation_embeddings, device)
-        if norm != 2:
-            raise NotImplementedError("TransE: only the L2 norm (all reference configs) is supported")
-        self.norm = norm
+        if int(norm) not in (1, 2):
+            raise ValueError(f"TransE: norm must be 1 or 2, got {norm!r}")
+        self.norm = int(norm)
+
+    def _make_ctx(self):
+        return _lib.Context(self.name, self.entity_embeddings, self.relation_embeddings, device=self.device,
+                            norm_p=self.norm)
 
     def is_minimizer(self):
         return True

@@ -201,6 +201,8 @@ class OracleModel:
             self.init_scale = float(self.params.get("init_scale", 1e-3))
         else:
             self.dimension = dim
+        # TransE score norm p (transe.py:46; tune.py:19 searches p in {1, 2})
+        self.norm = int(self.params.get("norm", 2)) if name == "TransE" else 2
         if name == "ConvE":
             self.hidden_dropout = float(self.params.get("hidden_dropout_rate", 0.0))
             self.input_dropout = float(self.params.get("input_dropout_rate", 0.0))
@@ -302,8 +304,10 @@ class OracleModel:
         rel = self.R[t[:, 1]]
         if self.name == "TransE":
             tr = (lhs + rel).astype(F32)
-            diff = tr[:, None, :] - E[None, :, :]
-            return np.sqrt((diff.astype(np.float64) ** 2).sum(-1)).astype(F32)
+            diff = (tr[:, None, :] - E[None, :, :]).astype(np.float64)
+            if self.norm == 1:
+                return np.abs(diff).sum(-1).astype(F32)
+            return np.sqrt((diff ** 2).sum(-1)).astype(F32)
         if self.name == "ComplEx":
             q = self.complex_query(lhs, rel)
             return (q @ E.T).astype(F32)
@@ -452,10 +456,11 @@ class TransETrainer:
     regularizers.py), numpy float32 over the whole tables, Adam.  ``epoch`` takes the
     epoch's positive and corrupted rows in order."""
 
-    def __init__(self, E, R, hp: dict):
+    def __init__(self, E, R, hp: dict, norm=2):
         self.E = np.array(E, dtype=F32)
         self.R = np.array(R, dtype=F32)
         self.hp = hp
+        self.norm = int(norm)
         self.oE, self.oR = AdamState(self.E.size, hp["lr"]), AdamState(self.R.size, hp["lr"])
 
     def _step(self, pos, neg):
@@ -464,11 +469,18 @@ class TransETrainer:
         rows = [E[pos[:, 0]], R[pos[:, 1]], E[pos[:, 2]], E[neg[:, 0]], R[neg[:, 1]], E[neg[:, 2]]]
         a = ((rows[0] + rows[1]) - rows[2]).astype(F32)
         b = ((rows[3] + rows[4]) - rows[5]).astype(F32)
-        sp = np.sqrt((a * a).sum(1)).astype(F32)
-        sn = np.sqrt((b * b).sum(1)).astype(F32)
-        hinge = ((sp - sn) + F32(self.hp["margin"])) > 0
-        cp = np.where(hinge, F32(1.0 / B) / sp, F32(0))[:, None].astype(F32)
-        cn = np.where(hinge, -F32(1.0 / B) / sn, F32(0))[:, None].astype(F32)
+        if self.norm == 1:  # transe.py:72 with p = 1: sum |v|, gradient sgn(v)
+            sp, sn = np.abs(a).sum(1).astype(F32), np.abs(b).sum(1).astype(F32)
+            hinge = ((sp - sn) + F32(self.hp["margin"])) > 0
+            cp = np.where(hinge, F32(1.0 / B), F32(0))[:, None].astype(F32)
+            cn = np.where(hinge, -F32(1.0 / B), F32(0))[:, None].astype(F32)
+            a, b = np.sign(a).astype(F32), np.sign(b).astype(F32)
+        else:
+            sp = np.sqrt((a * a).sum(1)).astype(F32)
+            sn = np.sqrt((b * b).sum(1)).astype(F32)
+            hinge = ((sp - sn) + F32(self.hp["margin"])) > 0
+            cp = np.where(hinge, F32(1.0 / B) / sp, F32(0))[:, None].astype(F32)
+            cn = np.where(hinge, -F32(1.0 / B) / sn, F32(0))[:, None].astype(F32)
         wl = F32(self.hp.get("regularizer_weight", 0.0)) / (F32(3) * F32(B) * F32(d))
         g = [cp * a + wl * rows[0], cp * a + wl * rows[1], -cp * a + wl * rows[2],
              cn * b + wl * rows[3], cn * b + wl * rows[4], -cn * b + wl * rows[5]]
@@ -635,6 +647,7 @@ def posttrain_transe(model: OracleModel, ds, triples, x0, hp, rng):
     lam = float(hp["regularizer_weight"])
     x = x0.astype(F32).copy()
     d = model.dimension
+    l1 = model.norm == 1
     opt = AdamState(d, hp["lr"])
     for _ in range(int(hp["epochs"])):
         # in-place shuffle (compounding across epochs) + ratio*R negatives
@@ -654,13 +667,19 @@ def posttrain_transe(model: OracleModel, ds, triples, x0, hp, rng):
             vs = []
             for tri in (pos, ng):
                 v = (E[tri[:, 0]] + model.R[tri[:, 1]] - E[tri[:, 2]]).astype(F32)
-                f = np.sqrt((v.astype(np.float64) ** 2).sum(1))
+                if l1:
+                    f = np.abs(v.astype(np.float64)).sum(1)
+                else:
+                    f = np.sqrt((v.astype(np.float64) ** 2).sum(1))
                 vs.append((v, f, tri))
             # clamp_min backward passes the gradient where z >= 0
             act = (vs[0][1] - vs[1][1] + float(margin)) >= 0
             for sign, (v, f, tri) in ((1.0, vs[0]), (-1.0, vs[1])):
-                with np.errstate(invalid="ignore", divide="ignore"):
-                    u = np.where(f[:, None] > 0, v / f[:, None], 0.0)
+                if l1:  # d|v|_1/dv = sgn(v), sgn(0) = 0 (torch's norm backward, p = 1)
+                    u = np.sign(v).astype(np.float64)
+                else:
+                    with np.errstate(invalid="ignore", divide="ignore"):
+                        u = np.where(f[:, None] > 0, v / f[:, None], 0.0)
                 coef = sign * act / B
                 g += ((coef * (tri[:, 0] == k))[:, None] * u).sum(0)
                 g -= ((coef * (tri[:, 2] == k))[:, None] * u).sum(0)

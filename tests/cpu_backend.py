@@ -99,6 +99,7 @@ class OracleBackedContext:
             params["feature_map_dropout_rate"] = model.feature_map_dropout_rate
         else:
             dim = model.dimension
+            params["norm"] = model.norm
         self.om = ko.OracleModel(name, w, dim, params)
         if name == "ConvE":
             off = 0
@@ -174,7 +175,7 @@ class OracleBackedContext:
         if epoch == 0 or getattr(self, "_trainer", None) is None:
             hpd = self._hp(hp)
             if self.model.name == "TransE":
-                self._trainer = ko.TransETrainer(self.om.E, self.om.R, hpd)
+                self._trainer = ko.TransETrainer(self.om.E, self.om.R, hpd, norm=self.om.norm)
             else:
                 hpd["optimizer_name"] = {0: "Adagrad", 1: "Adam", 2: "SGD"}[hp.optimizer]
                 self._trainer = ko.ComplExTrainer(self.om.E, self.om.R, hpd)

@@ -99,6 +99,11 @@ CASES = {
                               hp={"batch_size": 512, "label_smoothing": 0.1, "lr": 0.0427, "decay": 0.995,
                                   "epochs": 40},
                               xsi=5.0, suff_xsi=0.9, conve_random_bn=True),
+    # TransE with the L1 score norm (TransEHyperParams.norm = 1; tune.py:19 searches {1, 2})
+    "transe_l1_tiny": dict(model="TransE", shape="tiny", dim=16, model_params={"dimension": 16, "norm": 1},
+                           hp={"batch_size": 2048, "epochs": 65, "lr": 0.01, "margin": 5,
+                               "negative_triples_ratio": 5, "regularizer_weight": 1.0},
+                           xsi=5.0, suff_xsi=0.9, skip_builder=True),
     # the two multiclass-NLL regularisers with a non-zero weight in post-training
     # (multiclass_nll_optimizer.py:45-48, regularizers.py:25-46)
     "complex_n3_tiny": dict(model="ComplEx", shape="tiny", dim=8, model_params={"dimension": 8, "init_scale": 1e-3},

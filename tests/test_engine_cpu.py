@@ -11,7 +11,7 @@ from engine_cases import check_builder, check_necessary, check_pipeline, check_p
 from golden_io import CASES
 
 FAST = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve60_tiny", "conve60_drop_tiny", "complex_n3_tiny",
-        "complex_n2_tiny"]
+        "complex_n2_tiny", "transe_l1_tiny"]
 
 
 @pytest.mark.parametrize("name", FAST)

@@ -14,7 +14,7 @@ import kelpie_amd as ka
 pytestmark = pytest.mark.gpu
 
 GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny", "conve60_tiny", "conve_tiny", "conve_drop_tiny",
-             "conve60_drop_tiny", "complex_n3_tiny", "complex_n2_tiny"]
+             "conve60_drop_tiny", "complex_n3_tiny", "complex_n2_tiny", "transe_l1_tiny"]
 
 
 @pytest.mark.parametrize("name", GPU_CASES + ["complex200_small", "transe200_small"])

@@ -64,6 +64,11 @@ def test_oracle_necessary(name):
 def test_oracle_sufficient(name):
     rec, ds, model = _setup(name)
     seed_all(rec["seed"])
+    if name == "conve_drop_tiny":
+        # d = 200, 150 epochs, three dropouts: one sufficient call is k post-trainings,
+        # minutes in numpy; the dropout path of the oracle is pinned by the necessary calls
+        # above and conve60_drop_tiny, every sufficient call by the GPU tests
+        pytest.skip("CPU time: covered by test_oracle_necessary and tests/test_gpu_parity.py")
     eng = ko.OracleEngine(model, ds, rec["hp"])
     for block in rec["sufficient"]:
         eng.set_cache()

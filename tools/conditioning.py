@@ -226,7 +226,10 @@ def main():
         with open(out_path) as f:
             out["runs"] = json.load(f).get("runs", {})
     for v in args.variants:
-        if v in out["runs"] or (v == "fp32_perm" and wl["model"] == "TransE"):
+        # no permuted variant for TransE (nothing to permute) or under feature-map dropout:
+        # its per-channel masks (conve.py:147) would land on other filters, another model
+        if v in out["runs"] or (v == "fp32_perm" and (wl["model"] == "TransE"
+                                                      or wl.get("fmap_dropout", 0) > 0)):
             continue
         w, cols = (permuted_weights(wl, w0) if v == "fp32_perm" else (w0, None))
         dataset, model = noise_floor.reference_model(src, wl, g, w)

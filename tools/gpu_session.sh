@@ -36,6 +36,12 @@ run_step() {
       local rc=$?
       grep -E "passed|failed|error" $O/tests_${a[1]:-all}.txt | tail -2
       return $rc ;;
+    hostprof)  # host scheduling cost of one workload's batches (CPU only)
+      timeout -k 10 300 python -u tools/host_profile.py --workload ${a[1]:-transe-fb15k237-necessary} --preds 16 \
+        --repeats ${a[2]:-6} > $O/host_profile_${a[1]:-transe-fb15k237-necessary}.txt 2>&1
+      local rc=$?
+      grep -E "^batch" $O/host_profile_${a[1]:-transe-fb15k237-necessary}.txt || true
+      return $rc ;;
     micro|microfb|microdb)
       local v=${a[1]} reps=${a[2]:-2} envs=() tagx=""
       if [ -n "${a[3]}" ]; then IFS=',' read -r -a envs <<< "${a[3]}"; tagx="_$(echo ${a[3]} | tr ',=' '__')"; fi
