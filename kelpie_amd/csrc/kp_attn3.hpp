@@ -88,6 +88,11 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_ILV
 #define KP_ILV 1
 #endif
+#ifndef KP_ATTN_PRIO
+// wave issue priority of the attention waves (s_setprio) over the other batch's kernels'
+// waves co-resident on their SIMDs (engine pipeline); 0 = the default priority
+#define KP_ATTN_PRIO 0
+#endif
 #ifndef KP_ATTN_FULLTILE
 #define KP_ATTN_FULLTILE 1  // full key tiles skip the per-key masks (bitwise the same)
 #endif
@@ -278,6 +283,7 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   // stays reachable for a value the caller never passes), so a launch costs its dispatch
   if (ylo != 12345.f) return;
 #endif
+  if constexpr (KP_ATTN_PRIO > 0) __builtin_amdgcn_s_setprio(KP_ATTN_PRIO);
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;

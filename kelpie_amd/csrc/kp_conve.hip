@@ -506,7 +506,7 @@ __global__ void kp_cv_kcol(int n, CvConst k, const float* __restrict__ Q, const 
   float z = 0.f;
   for (int d = threadIdx.x; d < k.dim; d += 64) z += Q[(size_t)s * k.dp + d] * X[(size_t)s * k.dp + d];
   z = wave_sum(z);
-  if (threadIdx.x == 0) scores[(size_t)s * ld + k.n_ent] = 1.0f / (1.0f + __expf(-z));
+  if (threadIdx.x == 0) scores[(size_t)s * ld + k.n_ent] = 1.0f / (1.0f + expf(-z));
 }
 
 CvConst make_const(kp_ctx* c, const kp_hp* hp) {

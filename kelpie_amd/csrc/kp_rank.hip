@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void kp_gemm_abt(const float* __restrict__ A, 
       if (q < M && e < N) {
         float v = acc[n][r];
         if (bias && blockIdx.z == 0) v += bias[e];
-        if (act == 1) v = 1.0f / (1.0f + __expf(-v));
+        if (act == 1) v = 1.0f / (1.0f + expf(-v));  // torch.sigmoid in float32 (accurate exp)
         out[(size_t)q * ldo + e] = v;
       }
     }
@@ -207,10 +207,17 @@ __global__ __launch_bounds__(256) void kp_rank_filter_bits(int n_slots, int nwor
   }
 }
 
+// torch.sigmoid on a float32 logit (conve.py:157): 1 / (1 + exp(-x)) in float32; near 1
+// its values step by 2^-23 and reach 1.0 at x ~ 16.64, so the reference's fp32 scores
+// tie where the fp64 logits still differ (saturated targets above all)
+__device__ __forceinline__ float sigmoid_f32(double x) { return 1.0f / (1.0f + expf(-(float)x)); }
+
 // kelpie column and target: one thread per slot (counts the kelpie column, writes the
 // fp32 target score)
 // act RANK64_DOT: the scores are the fp64 values (ComplEx); RANK64_SIGMOID: the scores
-// are sigmoid(logit) and the rank compares the monotone logits (ConvE); RANK64_DIST: a
+// are sigmoid(logit) and the rank compares the monotone logits, an entity whose float32
+// sigmoid equals the target's counting as the tie the reference's fp32 scores make
+// (ConvE); RANK64_DIST: a
 // minimizer whose scores are L2 distances and the rank compares their squares (TransE:
 // get_triple_results' minimizer branch, the target counting itself even when filtered);
 // RANK64_DIST1: the same minimizer on L1 distances (TransE norm p = 1)
@@ -223,14 +230,17 @@ __global__ void kp_rank_f64_kelpie(int n_slots, int n_ent, int nwords, const uin
   const bool filtered = (bits[(size_t)s * nwords + (n_ent >> 5)] >> (n_ent & 31)) & 1u;
   if (act == RANK64_DIST || act == RANK64_DIST1)
     rank[s] = (pred_o[s] == n_ent || (!filtered && kcol64[s] <= t64[s])) ? 1ull : 0ull;
+  else if (act == RANK64_SIGMOID)
+    rank[s] = (!filtered && (kcol64[s] >= t64[s] || sigmoid_f32(kcol64[s]) == sigmoid_f32(t64[s]))) ? 1ull : 0ull;
   else
     rank[s] = (!filtered && kcol64[s] >= t64[s]) ? 1ull : 0ull;
-  target_out[s] = act == RANK64_SIGMOID ? (float)(1.0 / (1.0 + exp(-t64[s])))
+  target_out[s] = act == RANK64_SIGMOID ? sigmoid_f32(t64[s])
                   : act == RANK64_DIST  ? (float)sqrt(t64[s])
                                         : (float)t64[s];  // DOT, DIST1
 }
 
-// MODE: RANK64_DOT (dot products, maximizer), RANK64_DIST (squared L2), RANK64_DIST1 (L1)
+// MODE: RANK64_DOT (dot products, maximizer), RANK64_SIGMOID (dot products = logits, with
+// the float32 sigmoid ties), RANK64_DIST (squared L2), RANK64_DIST1 (L1)
 template <int MODE>
 __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent, int dp, const double* __restrict__ Q,
                                                          const double* __restrict__ t64,
@@ -270,8 +280,10 @@ __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent,
       const bool filtered = (bits[(size_t)s * nwords + (e >> 5)] >> (e & 31)) & 1u;
       // the target counts itself whatever the rounding of its own score (a maximizer's
       // only if unfiltered: its filtered score is set back after the count)
-      if constexpr (MODE != RANK64_DOT)
+      if constexpr (MODE == RANK64_DIST || MODE == RANK64_DIST1)
         hit = e == pred_o[s] || (!filtered && acc[j] <= t64[s]);
+      else if constexpr (MODE == RANK64_SIGMOID)
+        hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s] || sigmoid_f32(acc[j]) == sigmoid_f32(t64[s]));
       else
         hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s]);
     }
@@ -315,6 +327,9 @@ void launch_rank_f64(kp_ctx* c, int n_slots, const double* d_q64, const double* 
   else if (act == RANK64_DIST1)
     hipLaunchKernelGGL(kp_rank_f64_count<RANK64_DIST1>, grid, dim3(256), 0, c->stream, n_slots, c->n_ent, c->dp, d_q64,
                        d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
+  else if (act == RANK64_SIGMOID)
+    hipLaunchKernelGGL(kp_rank_f64_count<RANK64_SIGMOID>, grid, dim3(256), 0, c->stream, n_slots, c->n_ent, c->dp,
+                       d_q64, d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);
   else
     hipLaunchKernelGGL(kp_rank_f64_count<RANK64_DOT>, grid, dim3(256), 0, c->stream, n_slots, c->n_ent, c->dp, d_q64,
                        d_t64, d_pred_o, c->eT.as<float>(), ldt, nwords, bits, rank);

@@ -670,6 +670,7 @@ class PostTrainingEngine(RelevanceEngine):
             except BaseException as e:  # re-raised on the scheduling thread
                 state["error"] = e
 
+        tr("enter", -1)
         outs, stats, inflight = [], [], collections.deque()
         late_collect = os.environ.get("KELPIE_PIPELINE_EARLY_START", "1") == "0"  # A/B: collect, then start
         detach = os.environ.get("KELPIE_PIPELINE_DETACH", "1") == "1"
@@ -736,6 +737,7 @@ class PostTrainingEngine(RelevanceEngine):
             sys.setswitchinterval(old_switch)
             if nogc:
                 gc.enable()
+            tr("exit", -1)
             if trace is not None:
                 import json
                 with open(trace_path, "a") as f:

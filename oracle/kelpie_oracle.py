@@ -313,7 +313,17 @@ class OracleModel:
             return (q @ E.T).astype(F32)
         x, _ = self.conve_encode(lhs, rel)
         s = (x @ E.T).astype(F32)
-        return (1.0 / (1.0 + np.exp(-s.astype(np.float64)))).astype(F32)
+        return sigmoid_f32(s)
+
+
+def sigmoid_f32(s):
+    """torch.sigmoid on a float32 tensor (conve.py:157): 1 / (1 + exp(-x)) in float32
+    arithmetic.  Near 1 its outputs step by 2^-23 and reach 1.0 at x ~ 16.64 (a float64
+    sigmoid rounded once to float32 stays below 1.0 up to x ~ 17.33): the saturated ties
+    the reference's rank counts (post_training_engine.py:117-121)."""
+    s = np.asarray(s, dtype=F32)
+    with np.errstate(over="ignore"):
+        return (F32(1.0) / (F32(1.0) + np.exp(-s))).astype(F32)
 
 
 def predict_tails(om, dataset, triples):

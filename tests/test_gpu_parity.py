@@ -188,6 +188,52 @@ def test_conve_vs_oracle_full_width(dim, p_drop, part, monkeypatch):
     assert match == len(out["cpu"]), f"rank match {match}/{len(out['cpu'])}: {out}"
 
 
+def test_conve_saturated_sigmoid_ties():
+    """Targets whose float32 sigmoid is 1.0 (logit above ~16.64): the reference's fp32
+    scores tie every saturated entity with the target, and its rank counts them
+    (post_training_engine.py:117-121); the device ranks on fp64 logits and must count
+    the same ties (kp_rank_f64_count<RANK64_SIGMOID>).  BN3 scaled x30 on the d = 60
+    model saturates ~400 entities per row; the oracle scores with torch's float32
+    sigmoid (kelpie_oracle.sigmoid_f32)."""
+    from cpu_backend import OracleBackedContext
+    from kelpie_amd import synth
+    dim = 60
+    g = synth.make_graph("small", seed=9)
+    ds = ka.Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    w = synth.make_weights("ConvE", g.num_entities, g.num_relations, dim, seed=9, conve_random_bn=True,
+                           trained_scale=0.5)
+    w["bn3_weight"] = w["bn3_weight"] * 30
+    w["bn3_bias"] = w["bn3_bias"] * 30
+    bn = {i: {"weight": w[f"bn{i}_weight"], "bias": w[f"bn{i}_bias"], "running_mean": w[f"bn{i}_mean"],
+              "running_var": w[f"bn{i}_var"]} for i in (1, 2, 3)}
+    hp = dict(CV_HP, epochs=5)
+    test = [tuple(int(v) for v in t) for t in g.test][:50]
+    out = {}
+    for backend in ("gpu", "cpu"):
+        model = ka.ConvE(ds, w["entity_embeddings"], w["relation_embeddings"], w["conv_weight"].reshape(32, 3, 3),
+                         w["conv_bias"], w["fc_weight"], w["fc_bias"], bn=bn)
+        if backend == "cpu":
+            model._ctx = OracleBackedContext(model)
+        sc = model.ctx.all_scores(np.array([t[0] for t in test]), np.array([t[1] for t in test]))
+        preds = [t for i, t in enumerate(test) if sc[i][t[2]] == 1.0][:3]
+        assert len(preds) == 3, "no saturated targets"
+        seed_all(42)
+        eng = ka.NecessaryPostTrainingEngine(model, ds, hp)
+        res = []
+        for pred in preds:
+            eng.set_cache()
+            cands = sorted(ds.entity_to_training_triples[pred[0]])[:3]
+            eng.compute_relevance_batch(pred, [[c] for c in cands])
+            res += [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
+                    for pt, b in eng.last_results]
+        out[backend] = (preds, res)
+    assert out["gpu"][0] == out["cpu"][0]
+    assert any(r[1] == 1.0 or r[3] == 1.0 for r in out["cpu"][1]), "no saturated post-trained target"
+    assert [(r[0], r[2]) for r in out["gpu"][1]] == [(r[0], r[2]) for r in out["cpu"][1]], out
+    for a, b in zip(out["gpu"][1], out["cpu"][1]):
+        assert abs(a[1] - b[1]) <= 1e-4 and abs(a[3] - b[3]) <= 1e-4, (a, b)
+
+
 def test_complex_all_scores_matches_fp32_reference():
     g, ds, w = _small_complex(dim=200)
     model = ka.ComplEx(ds, w["entity_embeddings"], w["relation_embeddings"])

@@ -72,7 +72,7 @@ run_step() {
       cat $O/pmc_$v.txt ;;
     bench)
       local w=${a[1]} st=${a[2]:-3} wu=${a[3]:-1} envs=() tagx=""
-      if [ -n "${a[4]}" ]; then IFS=',' read -r -a envs <<< "${a[4]}"; tagx="_$(echo ${a[4]} | tr ',=' '__')"; fi
+      if [ -n "${a[4]}" ]; then IFS=',' read -r -a envs <<< "${a[4]}"; tagx="_$(echo ${a[4]} | tr ',=/' '___')"; fi
       env "${envs[@]}" timeout -k 10 600 python bench.py --workload $w --steps $st --warmup $wu --no-cpu-baseline \
         > $O/bench_$w$tagx.json 2> $O/bench_$w$tagx.err || { tail -5 $O/bench_$w$tagx.err; return 1; }
       python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], round(d['value'],1), 'cand/s', round(d['ms_per_step'],2), 'ms', 'frac', d['roofline']['frac'], 'fp64', d.get('rank_delta_match_rate_ref_fp64'))" $O/bench_$w$tagx.json "$w$tagx" ;;
@@ -111,6 +111,18 @@ run_step() {
         for v in "${vals[@]}"; do
           run_step "bench:$w:$st:1:$var=$v" || return 1
           mv $O/bench_${w}_${var}_$v.json $O/ab_${w}_${var}_${v}_$rep.json
+        done
+      done ;;
+    libab)  # libab:<wl>:<base|variant,...>[:reps[:steps]]: variants/lib_<variant>.so against the product library
+      local w=${a[1]} reps=${a[3]:-2} st=${a[4]:-3}
+      IFS=',' read -r -a vals <<< "${a[2]}"
+      for rep in $(seq 1 $reps); do
+        for v in "${vals[@]}"; do
+          local lib=$R/kelpie_amd/libkelpie_hip.so
+          [ $v != base ] && lib=$R/variants/lib_$v.so
+          KELPIE_HIP_LIB=$lib timeout -k 10 600 python bench.py --workload $w --steps $st --warmup 1 --no-cpu-baseline \
+            > $O/libab_${w}_${v}_$rep.json 2> $O/libab_${w}_${v}_$rep.err || { tail -5 $O/libab_${w}_${v}_$rep.err; return 1; }
+          python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], round(d['value'],1), 'cand/s', round(d['ms_per_step'],2), 'ms', 'frac', d['roofline']['frac'], 'fp64', d.get('rank_delta_match_rate_ref_fp64'))" $O/libab_${w}_${v}_$rep.json "$w $v"
         done
       done ;;
     fullsize)

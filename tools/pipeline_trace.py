@@ -18,7 +18,7 @@ def summarise(events):
     by = {}
     for t, ev, b in events:
         by.setdefault(b, {})[ev] = t
-    bs = sorted(by)
+    bs = sorted(k for k in by if k >= 0)
     if len(bs) < 4:
         return None
     steady = bs[2:]
@@ -28,6 +28,8 @@ def summarise(events):
         v = [by[k][b] - by[k][a] for k in steady if a in by[k] and b in by[k]]
         return 1e3 * st.median(v) if v else float("nan")
 
+    ends = by.pop(-1, {})
+    bs = sorted(by)
     starts = [by[k]["schedule"] for k in steady]
     period = 1e3 * (starts[-1] - starts[0]) / max(1, len(starts) - 1)
     rows = {
@@ -47,6 +49,10 @@ def summarise(events):
         lines.append("  b%-3d " % k + "  ".join(f"{ev}={1e3 * (e[ev] - t0):8.2f}" for ev in
                                                  ("schedule", "scheduled", "run", "draws", "ran", "joined",
                                                   "finish", "finished") if ev in e))
+    if "enter" in ends and "exit" in ends:
+        rows["call span"] = 1e3 * (ends["exit"] - ends["enter"])
+        rows["enter -> first schedule"] = 1e3 * (by[bs[0]]["schedule"] - ends["enter"])
+        rows["last finished -> exit"] = 1e3 * (ends["exit"] - max(e.get("finished", 0) for e in by.values()))
     return rows, lines, len(bs)
 
 
