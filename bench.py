@@ -399,10 +399,12 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     outs = eng.compute_relevance_pipeline([items_of(jobs[i]) for i in range(args.warmup, n_steps)], depth=depth)
+    t_call = time.perf_counter() - t0
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     kd.barrier()
     elapsed = time.perf_counter() - t0
+    log(f"[rank {rank}] timed region {elapsed * 1e3:.1f} ms, of which the pipeline call {t_call * 1e3:.1f} ms")
     recs = [[r, 0, 0, 0, 0] for o in outs for out in o for r in out]
     hot = [0.0, 0.0, 0]
     ivs = []

@@ -207,17 +207,22 @@ __global__ __launch_bounds__(256) void kp_rank_filter_bits(int n_slots, int nwor
   }
 }
 
-// torch.sigmoid on a float32 logit (conve.py:157): 1 / (1 + exp(-x)) in float32; near 1
-// its values step by 2^-23 and reach 1.0 at x ~ 16.64, so the reference's fp32 scores
-// tie where the fp64 logits still differ (saturated targets above all)
+// torch.sigmoid on a float32 logit (conve.py:157): 1 / (1 + exp(-x)) in float32.  It
+// reaches 1.0 at x ~ 16.64, so when the target's fp32 score is 1.0 the reference's rank
+// counts every saturated entity as a tie, however far apart the logits are; the device
+// ranks on fp64 logits and counts those ties explicitly (saturated: the float32 sigmoid
+// is 1.0).  Below saturation, equal float32 scores are rounding coincidences of either
+// side's logits and are not counted (the full-size fixtures: counting them moved the
+// rank deltas out of the reference's own spread).
+__device__ __forceinline__ bool sigmoid_f32_saturated(double x) { return 1.0f / (1.0f + expf(-(float)x)) == 1.0f; }
 __device__ __forceinline__ float sigmoid_f32(double x) { return 1.0f / (1.0f + expf(-(float)x)); }
 
 // kelpie column and target: one thread per slot (counts the kelpie column, writes the
 // fp32 target score)
 // act RANK64_DOT: the scores are the fp64 values (ComplEx); RANK64_SIGMOID: the scores
-// are sigmoid(logit) and the rank compares the monotone logits, an entity whose float32
-// sigmoid equals the target's counting as the tie the reference's fp32 scores make
-// (ConvE); RANK64_DIST: a
+// are sigmoid(logit) and the rank compares the monotone logits, with a saturated target
+// (float32 score 1.0) tied by every saturated entity as the reference's fp32 scores tie
+// them (ConvE); RANK64_DIST: a
 // minimizer whose scores are L2 distances and the rank compares their squares (TransE:
 // get_triple_results' minimizer branch, the target counting itself even when filtered);
 // RANK64_DIST1: the same minimizer on L1 distances (TransE norm p = 1)
@@ -231,7 +236,9 @@ __global__ void kp_rank_f64_kelpie(int n_slots, int n_ent, int nwords, const uin
   if (act == RANK64_DIST || act == RANK64_DIST1)
     rank[s] = (pred_o[s] == n_ent || (!filtered && kcol64[s] <= t64[s])) ? 1ull : 0ull;
   else if (act == RANK64_SIGMOID)
-    rank[s] = (!filtered && (kcol64[s] >= t64[s] || sigmoid_f32(kcol64[s]) == sigmoid_f32(t64[s]))) ? 1ull : 0ull;
+    rank[s] = (!filtered && (kcol64[s] >= t64[s] || (sigmoid_f32_saturated(t64[s]) && sigmoid_f32_saturated(kcol64[s]))))
+                  ? 1ull
+                  : 0ull;
   else
     rank[s] = (!filtered && kcol64[s] >= t64[s]) ? 1ull : 0ull;
   target_out[s] = act == RANK64_SIGMOID ? sigmoid_f32(t64[s])
@@ -240,7 +247,7 @@ __global__ void kp_rank_f64_kelpie(int n_slots, int n_ent, int nwords, const uin
 }
 
 // MODE: RANK64_DOT (dot products, maximizer), RANK64_SIGMOID (dot products = logits, with
-// the float32 sigmoid ties), RANK64_DIST (squared L2), RANK64_DIST1 (L1)
+// the saturated float32 sigmoid ties), RANK64_DIST (squared L2), RANK64_DIST1 (L1)
 template <int MODE>
 __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent, int dp, const double* __restrict__ Q,
                                                          const double* __restrict__ t64,
@@ -283,7 +290,8 @@ __global__ __launch_bounds__(256) void kp_rank_f64_count(int n_slots, int n_ent,
       if constexpr (MODE == RANK64_DIST || MODE == RANK64_DIST1)
         hit = e == pred_o[s] || (!filtered && acc[j] <= t64[s]);
       else if constexpr (MODE == RANK64_SIGMOID)
-        hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s] || sigmoid_f32(acc[j]) == sigmoid_f32(t64[s]));
+        hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s] ||
+                            (sigmoid_f32_saturated(t64[s]) && sigmoid_f32_saturated(acc[j])));
       else
         hit = !filtered && (e == pred_o[s] || acc[j] >= t64[s]);
     }

@@ -737,11 +737,7 @@ class PostTrainingEngine(RelevanceEngine):
             sys.setswitchinterval(old_switch)
             if nogc:
                 gc.enable()
-            tr("exit", -1)
-            if trace is not None:
-                import json
-                with open(trace_path, "a") as f:
-                    f.write(json.dumps(trace) + "\n")
+            tr("unwound", -1)
             if sys.exc_info()[0] is None:
                 _rng_mod.sync()  # the generators are current again when the call returns
             else:
@@ -749,6 +745,11 @@ class PostTrainingEngine(RelevanceEngine):
                     _rng_mod.sync()
                 except Exception:  # noqa: BLE001 -- the error in flight is the one to report
                     pass
+            tr("exit", -1)
+            if trace is not None:
+                import json
+                with open(trace_path, "a") as f:
+                    f.write(json.dumps(trace) + "\n")
         self.last_batch_stats = stats
         return outs
 

@@ -52,7 +52,9 @@ def summarise(events):
     if "enter" in ends and "exit" in ends:
         rows["call span"] = 1e3 * (ends["exit"] - ends["enter"])
         rows["enter -> first schedule"] = 1e3 * (by[bs[0]]["schedule"] - ends["enter"])
-        rows["last finished -> exit"] = 1e3 * (ends["exit"] - max(e.get("finished", 0) for e in by.values()))
+        rows["last finished -> unwound"] = 1e3 * (ends.get("unwound", ends["exit"])
+                                                  - max(e.get("finished", 0) for e in by.values()))
+        rows["unwound -> exit (rng sync)"] = 1e3 * (ends["exit"] - ends.get("unwound", ends["exit"]))
     return rows, lines, len(bs)
 
 
