@@ -601,7 +601,7 @@ class SchedBatch:
 # Page-locked memory is committed and locked, so the pool is small (KP_PINNED_ARENAS).
 _PINNED = []       # the pool's arrays
 _PINNED_IDLE = []  # per pool array: no lease of it is alive
-_PINNED_MAX = int(os.environ.get("KP_PINNED_ARENAS", "4"))
+_PINNED_MAX = int(os.environ.get("KP_PINNED_ARENAS", "6"))
 _PINNED_OK = None
 
 

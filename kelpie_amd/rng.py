@@ -31,6 +31,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+import threading
 
 import numpy as np
 import torch
@@ -95,6 +96,16 @@ _torch_async = False
 _poisoned = None
 
 
+# ticket -> the arrays a detached block's workers write (its arena, the walk's outputs):
+# kept alive until the ticket is waited for or a full sync, then released, so that a
+# pipeline's arenas go back to the page-locked pool batch by batch instead of all at the
+# end of the call (with every arena held, the pool ran dry after 4 batches and each later
+# batch took a fresh 64 MiB pageable arena: first-touch faults in the draw workers and a
+# ~50 ms release at the call's end, TransE FB15k-237 on the box)
+_detached = {}
+_detached_lock = threading.Lock()  # batch threads release while the scheduling thread adds
+
+
 def wait_ticket(ticket):
     """Wait for the draws of a detached deferred block (ReferenceRNG.deferred(detach=True))
     and of every block before it; a failed draw marks the stream lost."""
@@ -106,6 +117,10 @@ def wait_ticket(ticket):
     except Exception as exc:
         _poisoned = repr(exc)
         raise
+    # this block's and every earlier block's draws are complete
+    with _detached_lock:
+        for t in [t for t in _detached if t <= ticket]:
+            del _detached[t]
 
 
 def clear_poison():
@@ -158,9 +173,13 @@ def sync():
             _torch_async = False
             _skip = 0
             _inflight.clear()
+            with _detached_lock:
+                _detached.clear()
             _poisoned = repr(exc)
             raise
     _inflight.clear()
+    with _detached_lock:
+        _detached.clear()
     _flush_skip()  # also takes the torch stream back from an asynchronous walk
 
 
@@ -195,6 +214,10 @@ class ReferenceRNG:
                 self._arena = None
                 if detach and _outstanding and not _skip:
                     self.last_ticket = _lib.rng_batch_close()
+                    # the block's arrays now belong to its ticket (wait_ticket releases them)
+                    with _detached_lock:
+                        _detached[self.last_ticket] = list(_inflight)
+                    _inflight.clear()
                 else:
                     sync()
 
@@ -203,8 +226,8 @@ class ReferenceRNG:
     # arena per block: the arrays of an earlier batch may still be in flight.
     # int32 words of a fresh arena: one TransE FB15k-237 batch's draws (~6 M words) fit, so
     # they stay one contiguous span.  A pooled page-locked arena (_lib.pinned_i32) is
-    # committed and locked when allocated: the pool holds at most KP_PINNED_ARENAS (4) of
-    # them, 256 MiB per process; a pageable one commits only the pages written.
+    # committed and locked when allocated: the pool holds at most KP_PINNED_ARENAS (6) of
+    # them, 384 MiB per process; a pageable one commits only the pages written.
     _ARENA = 1 << 24
 
     def _take(self, n: int) -> np.ndarray:
