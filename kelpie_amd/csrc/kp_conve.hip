@@ -188,6 +188,113 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return sh[0] + sh[1] + sh[2] + sh[3];
 }
 
+// kp_cv_dx's dot products in its summation order: a 256-thread block_sum of per-thread
+// partials over d = tid + 256 m, i.e. four wave sums (old wave w: d mod 256 in [64 w,
+// 64 w + 64)) added in wave order.  Two waves holding d = t + 128 j (t < 128) keep one
+// partial per parity of j: wave h, parity q covers old wave h + 2 q.  Their wave sums
+// meet in LDS and are added in old-wave order: bitwise the block's result.
+template <int NJ>
+__device__ __forceinline__ float dot256_order2(const float* a, const float* b, float* sh) {
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (j & 1)
+      p1 += a[j] * b[j];
+    else
+      p0 += a[j] * b[j];
+  }
+  p0 = wave_sum(p0);
+  p1 = wave_sum(p1);
+  const int h = threadIdx.x >> 6;
+  __syncthreads();  // the previous sum's readers are done with sh
+  if ((threadIdx.x & 63) == 0) {
+    sh[h] = p0;
+    sh[h + 2] = p1;
+  }
+  __syncthreads();
+  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+// kp_cv_dx on two waves per pair with 16 bytes of LDS (NJ = ceil(dp / 128) row values per
+// lane, in registers): bitwise the same as the 256-thread form below, and small enough
+// (<= 32 VGPRs, 16 B of LDS) to run beside the other batch's attention workgroups, whose
+// two waves per SIMD leave 32 registers and 4 KiB of LDS per CU (kp_attn3<13>); the block
+// form (5 KiB of LDS, 35 VGPRs) could not, and waited for whole CUs under overlap
+template <int NJ>
+__global__ __launch_bounds__(128) void kp_cv_dx2(int M, CvConst k, const CvInst* __restrict__ inst,
+                                                 const float* __restrict__ Q, const float* __restrict__ O, int n_split,
+                                                 const int32_t* __restrict__ tails, const float* __restrict__ E,
+                                                 const float* __restrict__ X, const int32_t* __restrict__ bits,
+                                                 const float* __restrict__ bna, float* __restrict__ dfc,
+                                                 float* __restrict__ gk, __bf16* __restrict__ g3) {
+  __shared__ float sh[4];
+  const int i = blockIdx.x;
+  if (i >= M) return;
+  const int t = threadIdx.x;
+  const CvInst I = inst[i];
+  float xi[NJ], xk[NJ], dx[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int d = t + 128 * j;
+    const bool in = d < k.dim;
+    xi[j] = in ? Q[(size_t)i * k.dp + d] : 0.f;
+    xk[j] = in ? X[(size_t)I.slot * k.dp + d] : 0.f;
+  }
+  const float gs = 1.0f / (float)((long long)I.b * (long long)(k.n_ent + 1));
+  const float sk = dot256_order2<NJ>(xi, xk, sh);  // kelpie column
+  bool k_is_tail = false;
+  for (int u = 0; u < I.tail_count; ++u) k_is_tail |= (tails[I.tail_begin + u] == k.n_ent);
+  const float Gk = bce_g(sk, k_is_tail ? k.yhi : k.ylo, gs);
+  if (t == 0) gk[i] = Gk;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int d = t + 128 * j;
+    float v = 0.f;
+    if (d < k.dim)
+      for (int sp = 0; sp < n_split; ++sp) v += O[((size_t)sp * M + i) * k.dp + d];
+    dx[j] = v + Gk * xk[j];
+  }
+  // target corrections: G(s, yhi) - G(s, ylo) for the frozen tails
+  for (int u = 0; u < I.tail_count; ++u) {
+    const int e = tails[I.tail_begin + u];
+    if (e == k.n_ent) continue;
+    float er[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int d = t + 128 * j;
+      er[j] = d < k.dim ? E[(size_t)e * k.dp + d] : 0.f;
+    }
+    const float st = dot256_order2<NJ>(xi, er, sh);
+    const float corr = bce_g(st, k.yhi, gs) - bce_g(st, k.ylo, gs);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) dx[j] += corr * er[j];
+  }
+  const float* a3 = bna + 33;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int d = t + 128 * j;
+    if (d < k.dim) {
+      const float nz = k.has_mask ? noise_at(bits, I.mb.hid, d, k.scale) : 1.0f;
+      const float relu = xi[j] > 0.f ? 1.0f : 0.0f;
+      const float v = dx[j] * relu * a3[d] * nz;
+      dfc[(size_t)i * k.dim + d] = v;
+      if (g3) {  // kp_cv_bwd_fused's A operand: [3][M][KB] bf16 pieces
+        __bf16 h, m, l;
+        split3(v, h, m, l);
+        const size_t o = (size_t)i * kpcvf::KB + d, ps = (size_t)M * kpcvf::KB;
+        g3[o] = h;
+        g3[ps + o] = m;
+        g3[2 * ps + o] = l;
+      }
+    }
+  }
+  if (g3)
+    for (int d = k.dim + t; d < kpcvf::KB; d += 128) {
+      const size_t o = (size_t)i * kpcvf::KB + d, ps = (size_t)M * kpcvf::KB;
+      g3[o] = g3[ps + o] = g3[2 * ps + o] = (__bf16)0.f;
+    }
+}
+
 // dL/dx_i (encoder output) -> dL/dfc_i; also G at the kelpie column
 __global__ __launch_bounds__(256) void kp_cv_dx(int M, CvConst k, const CvInst* __restrict__ inst,
                                                 const float* __restrict__ Q, const float* __restrict__ O, int n_split,
@@ -1019,8 +1126,25 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
         c->hot_pairs.push_back({(double)nk, 0.0});
       }
       ++launches;
-      hipLaunchKernelGGL(kp_cv_dx, dim3(nk), dim3(256), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE, dX,
-                         dBits, c->d_bn_a, ddfc, dgk, shared ? nullptr : dG3);
+      {
+        __bf16* g3p = shared ? nullptr : dG3;
+        const int nj = (c->dp + 127) / 128;
+#define CV_DX2(J)                                                                                                   \
+  hipLaunchKernelGGL(kp_cv_dx2<J>, dim3(nk), dim3(128), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE, dX, \
+                     dBits, c->d_bn_a, ddfc, dgk, g3p)
+        if (!c->cv_dx_block && nj == 2)
+          CV_DX2(2);
+        else if (!c->cv_dx_block && nj == 1)
+          CV_DX2(1);
+        else if (!c->cv_dx_block && nj == 3)
+          CV_DX2(3);
+        else if (!c->cv_dx_block && nj == 4)
+          CV_DX2(4);
+        else
+          hipLaunchKernelGGL(kp_cv_dx, dim3(nk), dim3(256), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE,
+                             dX, dBits, c->d_bn_a, ddfc, dgk, g3p);
+#undef CV_DX2
+      }
       KP_HIP(hipGetLastError());
       if (shared) {
         // map rows 0-17 once per kelpie row (the sum of its pairs' dfc; rows 18-19 of its
