@@ -36,6 +36,10 @@ run_step() {
       local rc=$?
       grep -E "passed|failed|error" $O/tests_${a[1]:-all}.txt | tail -2
       return $rc ;;
+    rngbench)  # the TransE draw chains timed apart on the box's CPU (tools/rng_bench.cpp)
+      g++ -O3 -std=c++17 -mavx2 -mfma -ffp-contract=off -pthread -Iinclude tools/rng_bench.cpp -o /tmp/rng_bench_$TAG || return 1
+      timeout -k 10 120 /tmp/rng_bench_$TAG ${a[1]:-5} > $O/rng_bench.txt 2>&1 || return 1
+      tail -6 $O/rng_bench.txt ;;
     hostprof)  # host scheduling cost of one workload's batches (CPU only)
       timeout -k 10 300 python -u tools/host_profile.py --workload ${a[1]:-transe-fb15k237-necessary} --preds 16 \
         --repeats ${a[2]:-6} > $O/host_profile_${a[1]:-transe-fb15k237-necessary}.txt 2>&1
