@@ -979,14 +979,21 @@ int te_enqueue(TorchMt& mt, uint32_t* np_key, int32_t* np_pos, int32_t R, int32_
       te_shuffles(np_key, np_pos, R, epochs, out, sc.np, sc.idx, sc.jv);
       return;
     }
-    // the draws go to a buffer of their own in ordinary memory (`out` may be page-locked
-    // memory, where the scattered stores of the draw loop ran ~1.5x slower on the box) and
-    // the permutation chain, which streams whole rows into `out`, leaves the sequential
-    // worker for the pool
-    auto jv = std::make_shared<std::vector<int32_t>>((size_t)R * (size_t)epochs);
-    te_draws(np_key, np_pos, R, epochs, jv->data(), (size_t)R, sc.np);
-    if (!DrawQueue::get().enqueue(Task(), [=](Scratch& s2) { te_perms(R, epochs, jv->data(), (size_t)R, out, s2.idx); }))
-      te_perms(R, epochs, jv->data(), (size_t)R, out, sc.idx);
+    // The sequential worker only walks the chain (no stores: 2.4 vs 3.7-4.2 ms per bench
+    // batch on the box, tools/rng_bench.cpp, profiles/r05/rng_bench_box.txt), from a
+    // snapshot of the numpy state taken here; a pool task replays the same chain from the
+    // snapshot with the draws stored (in ordinary memory: `out` may be page-locked, where
+    // the scattered stores ran ~1.5x slower) and then runs the permutation chain into out
+    auto snap = std::make_shared<std::vector<uint32_t>>(np_key, np_key + kN);
+    const int32_t pos0 = *np_pos;
+    te_draws(np_key, np_pos, R, epochs, nullptr, 0, sc.np);
+    auto replay = [=](Scratch& s2) {
+      int32_t p = pos0;
+      s2.jv.resize((size_t)R * (size_t)epochs);
+      te_draws(snap->data(), &p, R, epochs, s2.jv.data(), (size_t)R, s2.np);
+      te_perms(R, epochs, s2.jv.data(), (size_t)R, out, s2.idx);
+    };
+    if (!DrawQueue::get().enqueue(Task(), replay)) replay(sc);
   };
   Task fill;
   if (out)
