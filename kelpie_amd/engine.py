@@ -21,6 +21,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+from . import _lib
 from .data import MANY_TO_ONE, ONE_TO_ONE, Dataset, KelpieView
 from .models import FrozenModel
 from .rng import ReferenceRNG, StateCheckpoint
@@ -63,7 +64,6 @@ def _contiguous_draws(slots, total, ctx=None):
     if total == 0:
         return np.zeros(1, np.int32)
     arrays = [s.rng.reshape(-1) for s in slots]
-    from . import _lib
     live = [a for a in arrays if a.size]
     lease = _lib.arena_of(live[0]) if live else None
     if lease is not None:
@@ -368,7 +368,6 @@ class PostTrainingEngine(RelevanceEngine):
         calls, self._fused = self._fused, []
         if not calls:
             return
-        from . import _lib
         m, hp = self.model, self.hp
         if self._sched is None:
             self._sched = _lib.SchedBatch()
