@@ -381,20 +381,23 @@ class PostTrainingEngine(RelevanceEngine):
                                                    [t for c in calls for t in c["triples"]])
         if fc >= 0:
             calls = calls[:fc + 1]  # the reference stops at the failing call
-        r_base = [int(rows[i, 0]) if c["flags"] & 1 else -1 for i, c in enumerate(calls)]
-        r_pt = [int(rows[i, 1]) if i != fc else -1 for i in range(len(calls))]
+        # plain ints once per flush (numpy scalar indexing per element costs ~0.2 us each)
+        idx, rows, nf = idx.tolist(), rows.tolist(), nf.tolist()
+        r_base = [rows[i][0] if c["flags"] & 1 else -1 for i, c in enumerate(calls)]
+        r_pt = [rows[i][1] if i != fc else -1 for i in range(len(calls))]
         want = [(c["flags"] >> 1) & 3 for c in calls] if self._sharded() else None
         xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, r_base, r_pt, int(hp["epochs"]),
                                               int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1,
                                               want=want)
         for i, c in enumerate(calls):
             db, dp = draws[i]
+            ii, ri, ni = idx[i], rows[i], nf[i]
             if c["base"] is not None:
                 c["base"].x0, c["base"].rng = xb[i], db
-                c["base"].native = (sb, int(idx[i, 0]), int(rows[i, 0]), int(nf[i, 0]))
+                c["base"].native = (sb, ii[0], ri[0], ni[0])
             if i != fc:
                 c["pt"].x0, c["pt"].rng = xp[i], dp
-                c["pt"].native = (sb, int(idx[i, 1]), int(rows[i, 1]), int(nf[i, 1]))
+                c["pt"].native = (sb, ii[1], ri[1], ni[1])
         if fc >= 0:
             raise self._edit_error(calls[fc], code, k)
 
