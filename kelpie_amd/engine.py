@@ -693,44 +693,74 @@ class PostTrainingEngine(RelevanceEngine):
             tr("finished", state["b"])
             self._raise_deferred(state["slots"], state["pending"])
 
-        try:
-            for b, items in enumerate(batches):
-                self.set_cache()
-                t0 = time.perf_counter()
-                tr("schedule", b)
-                self._deferred_error = None
-                # detached: the next batch is scheduled while the workers still make this
-                # one's draws (TransE: the sequential numpy chain); the batch thread waits
-                # for them before packing (KELPIE_PIPELINE_DETACH=0: wait here, A/B)
-                with self.rng.deferred(detach=detach) as drng:
-                    slots, pending, jobs = self._schedule_all(items, None)
-                ticket = drng.last_ticket
-                err, self._deferred_error = self._deferred_error, None
-                t_sched = time.perf_counter() - t0
-                tr("scheduled", b)
-                # batch b uses context b % depth: the batch before it on that context is done.
-                # Its device work is waited for first and batch b started on the freed context,
-                # then its results are collected: the collection (and the gather, sharded) runs
-                # while batch b packs and launches instead of ahead of it
-                done = []
-                while len(inflight) >= len(ctxs):
-                    old = inflight.popleft()
-                    old["thread"].join()
-                    tr("joined", old["b"])
-                    done.append(old)
-                if late_collect or any(d.get("error") is not None for d in done):
-                    for d in done:
-                        finish(d)  # raises the first device failure before batch b starts
-                    done = []
-                state = {"slots": slots, "pending": pending, "jobs": jobs, "schedule_s": t_sched, "error": None,
-                         "deferred": err, "ctx": ctxs[b % len(ctxs)], "ticket": ticket, "b": b}
-                state["thread"] = threading.Thread(target=run, args=(state,), daemon=True)
-                state["thread"].start()
-                inflight.append(state)
+        # KELPIE_PIPELINE_LOOKAHEAD (default 1): batches scheduled ahead of the contexts.  A
+        # freed context starts the next batch at once instead of after that batch's schedule
+        # (headline trace r05n: a context idled ~3 ms while the next batch was scheduled, with
+        # one batch left on the device); 0 schedules each batch only when it can start
+        lookahead = max(0, int(os.environ.get("KELPIE_PIPELINE_LOOKAHEAD", "1")))
+        ready = collections.deque()
+        todo = iter(enumerate(batches))
+        stop = False
+
+        def schedule_next():
+            """Schedule the next batch into `ready`; False when there is none."""
+            nonlocal stop
+            nxt = next(todo, None)
+            if nxt is None:
+                stop = True
+                return False
+            b, items = nxt
+            self.set_cache()
+            t0 = time.perf_counter()
+            tr("schedule", b)
+            self._deferred_error = None
+            # detached: the next batch is scheduled while the workers still make this
+            # one's draws (TransE: the sequential numpy chain); the batch thread waits
+            # for them before packing (KELPIE_PIPELINE_DETACH=0: wait here, A/B)
+            with self.rng.deferred(detach=detach) as drng:
+                slots, pending, jobs = self._schedule_all(items, None)
+            err, self._deferred_error = self._deferred_error, None
+            tr("scheduled", b)
+            ready.append({"slots": slots, "pending": pending, "jobs": jobs,
+                          "schedule_s": time.perf_counter() - t0, "error": None, "deferred": err,
+                          "ticket": drng.last_ticket, "b": b})
+            if err is not None:
+                stop = True  # the sequential reference stops at the failing call
+            return True
+
+        def start_next(done):
+            """Start the oldest ready batch on its context (batch b uses context b % depth:
+            the batch before it there is in `done` or was finished earlier), then collect
+            the finished ones: their collection (and the gather, sharded) runs while the
+            new batch packs and launches instead of ahead of it."""
+            if late_collect or any(d.get("error") is not None for d in done):
                 for d in done:
-                    finish(d)
-                if err is not None:
-                    break  # the sequential reference stops at the failing call
+                    finish(d)  # raises the first device failure before the next batch starts
+                done = []
+            state = ready.popleft()
+            state["ctx"] = ctxs[state["b"] % len(ctxs)]
+            state["thread"] = threading.Thread(target=run, args=(state,), daemon=True)
+            state["thread"].start()
+            inflight.append(state)
+            for d in done:
+                finish(d)
+
+        def join_oldest():
+            old = inflight.popleft()
+            old["thread"].join()
+            tr("joined", old["b"])
+            return old
+
+        try:
+            while True:
+                if ready and (len(inflight) < len(ctxs) or not inflight[0]["thread"].is_alive()):
+                    start_next([join_oldest()] if len(inflight) >= len(ctxs) else [])
+                elif not stop and len(ready) <= lookahead:
+                    schedule_next()
+                elif ready:
+                    start_next([join_oldest()])  # scheduled far enough ahead: wait for a context
+                else:
+                    break
             while inflight:
                 finish(inflight.popleft())
         finally:
