@@ -693,11 +693,13 @@ class PostTrainingEngine(RelevanceEngine):
             tr("finished", state["b"])
             self._raise_deferred(state["slots"], state["pending"])
 
-        # KELPIE_PIPELINE_LOOKAHEAD (default 1): batches scheduled ahead of the contexts.  A
-        # freed context starts the next batch at once instead of after that batch's schedule
-        # (headline trace r05n: a context idled ~3 ms while the next batch was scheduled, with
-        # one batch left on the device); 0 schedules each batch only when it can start
-        lookahead = max(0, int(os.environ.get("KELPIE_PIPELINE_LOOKAHEAD", "1")))
+        # KELPIE_PIPELINE_LOOKAHEAD=N: batches scheduled ahead of the contexts, so that a freed
+        # context starts the next batch at once instead of after that batch's schedule (the
+        # headline trace r05n shows a context idle ~3 ms while the next batch was scheduled).
+        # Measured, alternating on one box (profiles/r05/r05w/): 1 against 0, headline
+        # 868 / 878 / 875 vs 884 / 894 / 891 cand/s, ConvE 454 / 456 vs 456 / 457; default 0
+        # (each batch scheduled when the previous one has started)
+        lookahead = max(0, int(os.environ.get("KELPIE_PIPELINE_LOOKAHEAD", "0")))
         ready = collections.deque()
         todo = iter(enumerate(batches))
         stop = False
