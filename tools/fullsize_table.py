@@ -25,8 +25,9 @@ def main():
     import bench
     from test_fullsize_reference import elementwise_misses
     from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine
-    names = sys.argv[1:] or sorted(os.path.basename(p)[:-5]
-                                   for p in glob.glob(os.path.join(ROOT, "tests", "golden", "fullsize", "*.json")))
+    args = [a for a in sys.argv[1:] if a != "all"]  # "all" (or nothing): every fixture
+    names = args or sorted(os.path.basename(p)[:-5]
+                           for p in glob.glob(os.path.join(ROOT, "tests", "golden", "fullsize", "*.json")))
     built = {}
     for name in names:
         with open(os.path.join(ROOT, "tests", "golden", "fullsize", name + ".json")) as f:
