@@ -209,14 +209,17 @@ def seed_all(seed=42):
 
 
 def load_fixture(workload):
-    """tests/golden/fullsize/<workload>.json: the reference itself (fp32 as it runs, and
-    fp64 / permuted-reduction-order variants) on one prediction of this workload
-    (tools/conditioning.py, development container).  Data only."""
-    path = os.path.join(ROOT, "tests", "golden", "fullsize", workload + ".json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        return json.load(f)
+    """tests/golden/fullsize/<workload>.json (else its first other prediction, __p0): the
+    reference itself (fp32 as it runs, and fp64 / permuted-reduction-order variants) on one
+    prediction of this workload (tools/conditioning.py, development container).  Data only."""
+    for name in (workload, workload + "__p0"):
+        path = os.path.join(ROOT, "tests", "golden", "fullsize", name + ".json")
+        if os.path.exists(path):
+            with open(path) as f:
+                fx = json.load(f)
+            fx["_file"] = os.path.relpath(path, ROOT)
+            return fx
+    return None
 
 
 def _cores():
@@ -517,7 +520,8 @@ def main():
                                           f"the rest), one all-gather per batch"},
                 "rank_delta_match_rate": (parity.get("fp32") or {}).get("match_rate"),
                 "rank_delta_max_abs_diff": (parity.get("fp32") or {}).get("max_abs_diff"),
-                "rank_delta_vs": "the reference (fp32, CPU) on the fixture tests/golden/fullsize/<workload>.json",
+                "rank_delta_vs": "the reference (fp32, CPU) on the fixture "
+                                 + ((fixture or {}).get("_file") or "tests/golden/fullsize/<workload>.json (absent)"),
                 "rank_delta_match_rate_ref_fp64": (parity.get("fp64") or {}).get("match_rate"),
                 "rank_delta_max_abs_diff_ref_fp64": (parity.get("fp64") or {}).get("max_abs_diff"),
                 "reference_fp32_vs_fp64_max_abs_diff": parity.get("reference_fp32_vs_fp64_max_abs_diff"),
