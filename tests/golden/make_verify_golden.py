@@ -60,6 +60,15 @@ CASES_VERIFY = {
                         "regularizer_weight": 1.0},
         },
     },
+    # the L1 score norm (TransEHyperParams.norm = 1, transe.py:46; tune.py:19 searches {1, 2})
+    "transe_l1_tiny": {
+        "model": "TransE",
+        "model_params": {"dimension": 16, "norm": 1},
+        "training": {
+            "adam_l1": {"batch_size": 512, "epochs": 3, "lr": 0.01, "margin": 5, "negative_triples_ratio": 5,
+                        "regularizer_weight": 1.0},
+        },
+    },
 }
 
 
