@@ -881,20 +881,26 @@ class NecessaryPostTrainingEngine(PostTrainingEngine):
         minimizer = self.model.is_minimizer()
         outs = []
         self.last_results = []
+        rank_w, sig_w, lens = [], [], []
         for pj in jobs:
-            out = []
+            lens.append(len(pj))
             for pt_idx, key in pj:
                 base = self._base_result(key, slots, pending)
                 pt = slots[pt_idx].result
-                rank_worsening = pt["target_rank"] - base["target_rank"]
+                rank_w.append(pt["target_rank"] - base["target_rank"])
                 if minimizer:
                     score_worsening = pt["target_score"] - base["target_score"]
                 else:
                     score_worsening = base["target_score"] - pt["target_score"]
-                # int64 tensor + python float -> float32 tensor (A-Q5)
-                out.append(float(np.float32(np.float32(rank_worsening) + np.float32(_sigmoid(score_worsening)))))
+                sig_w.append(_sigmoid(score_worsening))
                 self.last_results.append((pt, base))
-            outs.append(out)
+        # int64 tensor + python float -> float32 tensor (A-Q5): one float32 add per call,
+        # element-wise over the batch (the same bits as the scalar form)
+        rel = (np.asarray(rank_w, np.int64).astype(np.float32) + np.asarray(sig_w, np.float64).astype(np.float32)).tolist()
+        k = 0
+        for n in lens:
+            outs.append(rel[k:k + n])
+            k += n
         return outs
 
 
