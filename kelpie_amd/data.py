@@ -307,9 +307,14 @@ class KelpieView:
         """This view in the library's host scheduler (kp_view_create, csrc/kp_sched.cpp)."""
         if self._native is None:
             from . import _lib
-            extra = np.asarray(self._other_triples(), dtype=np.int32).reshape(-1, 3)
-            self._native = _lib.NativeView(self.kelpie_entity, self.dataset.num_relations, self.original_entity,
-                                           self.base_arr, extra)
+            # _other_triples() as an array: the replacement done on the array (same triples,
+            # same order) instead of one Python tuple per triple
+            ds, k, s = self.dataset, self.kelpie_entity, self.original_entity
+            oth = ds.entity_to_validation_triples.get(s, []) + ds.entity_to_testing_triples.get(s, [])
+            extra = np.array(oth, dtype=np.int32).reshape(-1, 3)
+            extra[extra[:, 0] == s, 0] = k
+            extra[extra[:, 2] == s, 2] = k
+            self._native = _lib.NativeView(k, ds.num_relations, s, self.base_arr, extra)
         return self._native
 
     def _rows(self, t):
