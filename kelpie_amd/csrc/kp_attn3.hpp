@@ -88,6 +88,12 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_ILV
 #define KP_ILV 1
 #endif
+#ifndef KP_DMA_GROUP
+// buffer-descriptor LDS-DMA in groups of four consecutive pieces per wave: one M0 write and
+// four buffer_load ... lds with offset:0/1024/2048/3072 in one asm statement (instead of an
+// M0 write, an s_nop and one load per piece, each M0 write waiting on the previous load)
+#define KP_DMA_GROUP 1
+#endif
 #ifndef KP_ATTN_PRIO
 // wave issue priority of the attention waves (s_setprio) over the other batch's kernels'
 // waves co-resident on their SIMDs (engine pipeline); 0 = the default priority
@@ -310,8 +316,56 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         e3rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)(lds0 + (uint32_t)(buf * BUF_B + 1024 * p)), 16,
         16 * lane, (key_begin + tile * KT) * ROW_B + 1024 * p, 0, 0);
   };
+  // KP_DMA_GROUP (BUFDMA): wave w issues the consecutive pieces w NPW .. w NPW + NPW - 1,
+  // group g = pieces 4 g .. 4 g + 3 of them in one statement (the last group may be short)
+  typedef int i32x4_t __attribute__((ext_vector_type(4)));
+  const i32x4_t e3rs = {(int)(uint32_t)(uintptr_t)E3,
+                        (int)(uint32_t)((uintptr_t)E3 >> 32) & 0xFFFF,
+                        (int)((n_ent + 31) / 32 * 32 * ROW_B + 1024), 0x00020000};
+  auto dma_group = [&](int tile, int buf, int g) {
+    const int pb = w * ((PIECES + 3) / 4) + 4 * g;
+    const uint32_t m0v = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(buf * BUF_B + 1024 * pb)));
+    const uint32_t so = (uint32_t)__builtin_amdgcn_readfirstlane((key_begin + tile * KT) * ROW_B + 1024 * pb);
+    const int nleft = (PIECES + 3) / 4 - 4 * g;
+    if (nleft >= 4)
+      asm volatile(
+          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen offset:1024 lds\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen offset:2048 lds\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen offset:3072 lds" ::"s"(m0v),
+          "v"(16 * lane), "s"(e3rs), "s"(so)
+          : "memory");
+    else if (nleft == 3)
+      asm volatile(
+          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen offset:1024 lds\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen offset:2048 lds" ::"s"(m0v),
+          "v"(16 * lane), "s"(e3rs), "s"(so)
+          : "memory");
+    else if (nleft == 2)
+      asm volatile(
+          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen offset:1024 lds" ::"s"(m0v),
+          "v"(16 * lane), "s"(e3rs), "s"(so)
+          : "memory");
+    else if (nleft == 1)
+      asm volatile(
+          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
+          "v"(16 * lane), "s"(e3rs), "s"(so)
+          : "memory");
+  };
+  constexpr bool DGROUP = KP_DMA_GROUP && BUFDMA;
   auto issue = [&](int tile, int buf) {
     const uint8_t* src = E3 + (size_t)(key_begin + tile * KT) * ROW_B + 16 * lane;
+    if constexpr (KP_DMA_GROUP && BUFDMA) {
+#pragma unroll
+      for (int g = 0; g < ((PIECES + 3) / 4 + 3) / 4; ++g) dma_group(tile, buf, g);
+      return;
+    }
 #pragma unroll
     for (int p0 = 0; p0 < PIECES; p0 += 4) {
       const int p = p0 + w;
@@ -687,7 +741,11 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
 #pragma unroll
           for (int m = 0; m < DB; ++m) {
 #if !defined(KP_ATTN_NODMA) && !defined(KP_DMA_EARLY)
-            if (SPREAD && !SPREAD2 && dma_on) {
+            if (DGROUP && SPREAD && !SPREAD2 && dma_on) {
+              if (m % 4 == 0 && m < NPW) dma_group(tn, (t + 1) & 1, m / 4);
+              if (m == DB - 1)
+                for (int g = (DB + 3) / 4; 4 * g < NPW; ++g) dma_group(tn, (t + 1) & 1, g);
+            } else if (SPREAD && !SPREAD2 && dma_on) {
               if (m < NPW) {
                 issue_piece(tn, (t + 1) & 1, m);
 #ifdef KP_DIAG_DMA_LGKM0
