@@ -44,5 +44,18 @@ def test_pipeline_two_contexts(name):
 
 
 @pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
+@pytest.mark.parametrize("lookahead,workers,detach", [("1", "1", "1"), ("0", "0", "1"), ("1", "0", "0")])
+def test_pipeline_switches(name, lookahead, workers, detach, monkeypatch):
+    """The pipeline's A/B switches (KELPIE_PIPELINE_LOOKAHEAD: batches scheduled ahead of
+    the contexts; KELPIE_PIPELINE_WORKERS=0: a thread per batch; KELPIE_PIPELINE_DETACH=0:
+    the scheduling thread waits for each batch's draws) keep the reference's sequential
+    results, in order, with two batches in flight."""
+    monkeypatch.setenv("KELPIE_PIPELINE_LOOKAHEAD", lookahead)
+    monkeypatch.setenv("KELPIE_PIPELINE_WORKERS", workers)
+    monkeypatch.setenv("KELPIE_PIPELINE_DETACH", detach)
+    check_pipeline(name, "cpu", two_contexts=True)
+
+
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
 def test_explain_pipeline_and_output_json(name, tmp_path):
     check_pipeline_explain(name, "cpu", str(tmp_path))
