@@ -349,7 +349,9 @@ class PostTrainingEngine(RelevanceEngine):
                 fused, flush_at = self._fused, self._FUSED_FLUSH
         return out
 
-    _FUSED_FLUSH = 24  # queued TransE calls per library call
+    # queued TransE calls per library call (KELPIE_TE_FLUSH: A/B of the per-flush overhead
+    # against how early the draws reach the workers)
+    _FUSED_FLUSH = int(os.environ.get("KELPIE_TE_FLUSH", "24"))
     _FUSED_FIRST = 4  # ... for a batch's first one
 
     @staticmethod
