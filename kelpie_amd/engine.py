@@ -350,8 +350,10 @@ class PostTrainingEngine(RelevanceEngine):
         return out
 
     # queued TransE calls per library call (KELPIE_TE_FLUSH: A/B of the per-flush overhead
-    # against how early the draws reach the workers)
-    _FUSED_FLUSH = int(os.environ.get("KELPIE_TE_FLUSH", "24"))
+    # against how early the draws reach the workers).  Alternating on two boxes, 30 steps
+    # (profiles/r05/r05aj/, r05ak/): 64 averaged 57.9k cand/s over seven runs, 24 50.9k, 48
+    # 55.6k over four
+    _FUSED_FLUSH = int(os.environ.get("KELPIE_TE_FLUSH", "64"))
     _FUSED_FIRST = 4  # ... for a batch's first one
 
     @staticmethod
