@@ -296,9 +296,10 @@ class PostTrainingEngine(RelevanceEngine):
             slots.append(base)
         pt = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_pt, owner=pt_owner)
         slots.append(pt)
-        self._fused.append({"view": view, "kp": kp, "triples": [(int(a), int(b), int(c)) for a, b, c in triples],
-                            "flags": (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
-                            | (8 if mode == "sufficient" else 0), "base": base, "pt": pt})
+        # a queued call: (view, kelpie triple, rule triples, flags, base slot, pt slot)
+        self._fused.append((view, kp, [(int(a), int(b), int(c)) for a, b, c in triples],
+                            (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
+                            | (8 if mode == "sufficient" else 0), base, pt))
         if len(self._fused) >= (self._FUSED_FLUSH if self._sched is not None else self._FUSED_FIRST):
             # hand the draws to the library's workers early: their numpy shuffles then run
             # while this thread queues the next calls (the batch's first flush sooner, so
@@ -340,9 +341,9 @@ class PostTrainingEngine(RelevanceEngine):
                 slots.append(base)
             pt = _Slot(None, None, None, kp, None, None, own_pt, pt_owner)
             slots.append(pt)
-            fused.append({"view": view, "kp": kp, "triples": triples,
-                          "flags": (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
-                          | (8 if sufficient else 0), "base": base, "pt": pt})
+            fused.append((view, kp, triples,
+                          (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
+                          | (8 if sufficient else 0), base, pt))
             out.append((len(slots) - 1, pred))
             if len(fused) >= flush_at:
                 self._flush_fused()
@@ -362,9 +363,9 @@ class PostTrainingEngine(RelevanceEngine):
         if code == 1:
             return AssertionError()
         if code == 2:
-            v = call["view"]
+            v = call[0]
             o, kel = v.original_entity, v.kelpie_entity
-            t = call["triples"][k]
+            t = call[2][k]
             return KeyError((kel if t[0] == o else t[0], t[1], kel if t[2] == o else t[2]))
         return ValueError("list.remove(x): x not in list")
 
@@ -376,32 +377,33 @@ class PostTrainingEngine(RelevanceEngine):
         if self._sched is None:
             self._sched = _lib.SchedBatch()
         sb = self._sched
-        nviews = [c["view"].native for c in calls]
+        nviews = [c[0].native for c in calls]
         sb.views.extend(nviews)  # its C++ slots point into these views: they live as long as the batch
         off = np.zeros(len(calls) + 1, np.int32)
-        off[1:] = np.cumsum([len(c["triples"]) for c in calls])
-        idx, rows, nf, (fc, code, k) = sb.add_calls([v.h for v in nviews], [c["kp"][1] for c in calls],
-                                                   [c["flags"] for c in calls], off,
-                                                   [t for c in calls for t in c["triples"]])
+        off[1:] = np.cumsum([len(c[2]) for c in calls])
+        idx, rows, nf, (fc, code, k) = sb.add_calls([v.h for v in nviews], [c[1][1] for c in calls],
+                                                   [c[3] for c in calls], off,
+                                                   [t for c in calls for t in c[2]])
         if fc >= 0:
             calls = calls[:fc + 1]  # the reference stops at the failing call
         # plain ints once per flush (numpy scalar indexing per element costs ~0.2 us each)
         idx, rows, nf = idx.tolist(), rows.tolist(), nf.tolist()
-        r_base = [rows[i][0] if c["flags"] & 1 else -1 for i, c in enumerate(calls)]
+        r_base = [rows[i][0] if c[3] & 1 else -1 for i, c in enumerate(calls)]
         r_pt = [rows[i][1] if i != fc else -1 for i in range(len(calls))]
-        want = [(c["flags"] >> 1) & 3 for c in calls] if self._sharded() else None
+        want = [(c[3] >> 1) & 3 for c in calls] if self._sharded() else None
         xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, r_base, r_pt, int(hp["epochs"]),
                                               int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1,
                                               want=want)
         for i, c in enumerate(calls):
             db, dp = draws[i]
             ii, ri, ni = idx[i], rows[i], nf[i]
-            if c["base"] is not None:
-                c["base"].x0, c["base"].rng = xb[i], db
-                c["base"].native = (sb, ii[0], ri[0], ni[0])
+            base, pt = c[4], c[5]
+            if base is not None:
+                base.x0, base.rng = xb[i], db
+                base.native = (sb, ii[0], ri[0], ni[0])
             if i != fc:
-                c["pt"].x0, c["pt"].rng = xp[i], dp
-                c["pt"].native = (sb, ii[1], ri[1], ni[1])
+                pt.x0, pt.rng = xp[i], dp
+                pt.native = (sb, ii[1], ri[1], ni[1])
         if fc >= 0:
             raise self._edit_error(calls[fc], code, k)
 
