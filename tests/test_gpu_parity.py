@@ -111,8 +111,10 @@ TE_HP = {"batch_size": 2048, "epochs": 30, "lr": 0.01, "margin": 5, "negative_tr
          "regularizer_weight": 1.0}
 
 
-@pytest.mark.parametrize("dim", [200, 16])
-def test_transe_vs_oracle_full_width(dim):
+@pytest.mark.parametrize("dim,norm", [(200, 2), (16, 2), (200, 1)])
+def test_transe_vs_oracle_full_width(dim, norm):
+    """d = 200 (the production instantiation) and d = 16, with the L2 and (d = 200) the L1
+    score norm (transe.py:46)."""
     from cpu_backend import OracleBackedContext
     from kelpie_amd import synth
     g = synth.make_graph("small", seed=5)
@@ -123,7 +125,7 @@ def test_transe_vs_oracle_full_width(dim):
     preds = [t for t in test if 8 <= deg.get(t[0], 0) <= 40][:2] + [max(test, key=lambda t: deg.get(t[0], 0))]
     out = {}
     for backend in ("gpu", "cpu"):
-        model = ka.TransE(ds, w["entity_embeddings"], w["relation_embeddings"])
+        model = ka.TransE(ds, w["entity_embeddings"], w["relation_embeddings"], norm=norm)
         if backend == "cpu":
             model._ctx = OracleBackedContext(model)
         seed_all(42)
