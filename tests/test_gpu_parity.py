@@ -59,9 +59,11 @@ HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 20, "lr": 0.043,
 PARTS = ["streamk", "ranges"]
 
 
-@pytest.mark.parametrize("dim,hot,part", [(200, False, "streamk"), (200, False, "ranges"), (8, False, "auto"),
-                                          (200, True, "streamk"), (200, True, "ranges")])
-def test_complex_vs_oracle_full_width(dim, hot, part, monkeypatch):
+@pytest.mark.parametrize("dim,hot,part,reg", [(200, False, "streamk", None), (200, False, "ranges", None),
+                                              (8, False, "auto", None), (200, True, "streamk", None),
+                                              (200, True, "ranges", None), (200, False, "auto", "N3"),
+                                              (200, False, "auto", "N2")])
+def test_complex_vs_oracle_full_width(dim, hot, part, reg, monkeypatch):
     """D = 400 (the production kernel instantiation) and D = 16 on a 2,000-entity
     graph, including a hub subject with more rows than one minibatch.
 
@@ -69,7 +71,8 @@ def test_complex_vs_oracle_full_width(dim, hot, part, monkeypatch):
     first-tile maximum by far more than kpattn::kMargin, which exercises the
     attention kernel's exact-max second pass (step and frozen-pair queries).
     ``part``: the attention's work partition, forced (KP_ATTN_PART): stream-K or the
-    XCD-grouped key ranges (multi-tile ranges of the 63 key tiles)."""
+    XCD-grouped key ranges (multi-tile ranges of the 63 key tiles).  ``reg``: the N3 or N2
+    regulariser at weight 0.05 in post-training (regularizers.py:25-46; else weight 0)."""
     from cpu_backend import OracleBackedContext
     monkeypatch.setenv("KP_ATTN_PART", part)
     g, ds, w = _small_complex(dim=dim)
@@ -88,7 +91,8 @@ def test_complex_vs_oracle_full_width(dim, hot, part, monkeypatch):
         if backend == "cpu":
             model._ctx = OracleBackedContext(model)
         seed_all(42)
-        eng = ka.NecessaryPostTrainingEngine(model, ds, HP)
+        hp = dict(HP, regularizer_name=reg, regularizer_weight=0.05) if reg else HP
+        eng = ka.NecessaryPostTrainingEngine(model, ds, hp)
         res = []
         for pred in preds:
             eng.set_cache()
