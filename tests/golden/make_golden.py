@@ -124,6 +124,16 @@ CASES = {
                                  "decay1": 0.9, "decay2": 0.999, "regularizer_name": "N3",
                                  "regularizer_weight": 0},
                              xsi=5.0, suff_xsi=0.9, trained_scale=0.3, skip_builder=True, skip_sufficient=True),
+    # N3 at a non-zero weight at the production width (ComplEx D = 400, hub subject with
+    # multi-step epochs): pins the regulariser term of kp_cx_update where Adagrad can
+    # amplify its rounding
+    "complex200_n3_small": dict(model="ComplEx", shape="small", dim=200,
+                                model_params={"dimension": 200, "init_scale": 1e-3},
+                                hp={"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 20, "lr": 0.043,
+                                    "decay1": 0.9, "decay2": 0.999, "regularizer_name": "N3",
+                                    "regularizer_weight": 0.05},
+                                xsi=5.0, suff_xsi=0.9, trained_scale=0.3, skip_builder=True,
+                                skip_sufficient=True),
     "transe200_small": dict(model="TransE", shape="small", dim=200, model_params={"dimension": 200, "norm": 2},
                             hp={"batch_size": 2048, "epochs": 65, "lr": 0.01, "margin": 5,
                                 "negative_triples_ratio": 5, "regularizer_weight": 1.0},

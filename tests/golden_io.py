@@ -8,7 +8,7 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["transe_tiny", "complex_tiny", "complex_adam_tiny", "conve_tiny", "conve60_tiny", "complex200_small",
          "transe200_small", "conve_drop_tiny", "conve60_drop_tiny", "complex_n3_tiny", "complex_n2_tiny",
-         "transe_l1_tiny"]
+         "transe_l1_tiny", "complex200_n3_small"]
 
 
 def load_case(name):

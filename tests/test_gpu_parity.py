@@ -17,7 +17,7 @@ GPU_CASES = ["complex_tiny", "complex_adam_tiny", "transe_tiny", "conve60_tiny",
              "conve60_drop_tiny", "complex_n3_tiny", "complex_n2_tiny", "transe_l1_tiny"]
 
 
-@pytest.mark.parametrize("name", GPU_CASES + ["complex200_small", "transe200_small"])
+@pytest.mark.parametrize("name", GPU_CASES + ["complex200_small", "transe200_small", "complex200_n3_small"])
 @pytest.mark.parametrize("batched", [False, True])
 def test_necessary_vs_reference_goldens(name, batched):
     check_necessary(name, "gpu", batched)
