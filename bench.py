@@ -18,7 +18,9 @@ reference's random init, the ComplEx DBpedia50 explanation hp (Adagrad 0.043,
 43 epochs, batch 512), 20 candidates per prediction, 10 conversion entities
 (pipeline.py:36-39, degree cap 200).
 
-For N > 1 the driver launches one rank per GPU with torchrun.  A step then holds
+For N > 1 the driver launches one rank per GPU with torchrun; a plain
+``python bench.py --gpus N`` starts the N local ranks itself (torchrun as a child
+process), and a WORLD_SIZE other than N is refused.  A step then holds
 N times the predictions (weak scaling: the per-GPU work is fixed); every rank walks
 every batch's draws -- the reference's one global random stream, in the same order on
 every rank -- but schedules in full and post-trains only the slots it claims (for the
@@ -326,6 +328,26 @@ def parity_sample(eng, wl, fixture, fallback):
     return pred, cands, ents, out
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_local_ranks(n):
+    """``--gpus N`` without a launcher: run this same script under torchrun with N local
+    ranks (127.0.0.1 rendezvous, the driver's own command shape) as a child process --
+    never an exec, and nothing here has touched the GPU -- and return its exit status.
+    Rank 0 of the child prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(sys.argv[0])]
+    cmd += sys.argv[1:]
+    log(f"[bench] launching {n} local ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -335,6 +357,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--preds-per-step", type=int, default=None, help="override the workload's predictions per step")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # a plain `python bench.py --gpus N`: start the N local ranks ourselves, before
+        # anything touches the GPU, and exit with their status
+        sys.exit(launch_local_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"[bench] WORLD_SIZE={env_world} but --gpus {args.gpus}: launch one rank per GPU with --gpus N")
+        sys.exit(2)
     _heartbeat()
 
     import torch

@@ -37,6 +37,30 @@ static void upload_padded(kp_ctx* c, float** dst, const float* src, int rows, in
   KP_HIP(hipMemcpy(*dst, tmp.data(), sizeof(float) * tmp.size(), hipMemcpyHostToDevice));
 }
 
+// One private stream-ordered pool per device for the contexts' workspaces, created on
+// first use and kept for the process (never destroyed: contexts on several threads share
+// it).  Its release threshold is unbounded, so freed workspace stays with the pool.
+static hipMemPool_t device_pool(int device) {
+  static std::mutex mu;
+  static std::vector<hipMemPool_t> pools;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)pools.size() <= device) pools.resize(device + 1, nullptr);
+  if (!pools[device]) {
+    hipMemPoolProps props;
+    std::memset(&props, 0, sizeof(props));
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
+    hipMemPool_t pool = nullptr;
+    KP_HIP(hipMemPoolCreate(&pool, &props));
+    uint64_t keep = UINT64_MAX;
+    KP_HIP(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
+    pools[device] = pool;
+  }
+  return pools[device];
+}
+
 static void upload_plain(float** dst, const float* src, size_t n) {
   KP_HIP(hipMalloc(dst, sizeof(float) * n + 64));
   KP_HIP(hipMemcpy(*dst, src, sizeof(float) * n, hipMemcpyHostToDevice));
@@ -116,14 +140,15 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     if (const char* a = std::getenv("KP_ATTN_PART"))
       c->attn_part = std::strcmp(a, "streamk") == 0 ? 1 : std::strcmp(a, "ranges") == 0 ? 2 : 0;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    // the context's own workspaces grow stream-ordered on its stream (DevBuf); the
-    // default pool keeps what they give back instead of returning it to the driver
+    // the context's own workspaces grow stream-ordered on its stream (DevBuf), from the
+    // library's private pool of the device, which keeps what they give back instead of
+    // returning it to the driver; the device's default pool (torch, RCCL) is left alone
     {
-      hipMemPool_t pool;
-      KP_HIP(hipDeviceGetDefaultMemPool(&pool, device));
-      uint64_t keep = UINT64_MAX;
-      KP_HIP(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
-      for (DevBuf* d : c->bound_buffers()) d->s = c->stream;
+      hipMemPool_t pool = device_pool(device);
+      for (DevBuf* d : c->bound_buffers()) {
+        d->s = c->stream;
+        d->pool = pool;
+      }
     }
     KP_HIP(hipEventCreate(&c->ev0));
     KP_HIP(hipEventCreate(&c->ev1));

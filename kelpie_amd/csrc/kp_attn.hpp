@@ -59,16 +59,13 @@ __device__ __forceinline__ void glds16(const float* gp, uint32_t lds_base) {
   if constexpr (BUILTIN) {
     __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(uintptr_t)lds_base, 16, 0, 0);
   } else {
-#ifdef KP_DIAG_M0SAVE
-    // diagnostic: M0 saved and restored around the DMA (the compiler's M0 preserved)
+    // M0 is reserved to the compiler (a clobber of it is not honoured), so the DMA saves
+    // it and puts it back: any M0 the compiler set stays valid across the statement
     unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "s"(lds_base), "v"(gp)
                  : "memory");
-#else
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_base), "v"(gp) : "memory");
-#endif
   }
 }
 

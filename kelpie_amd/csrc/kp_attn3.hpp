@@ -327,34 +327,37 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
     const uint32_t m0v = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(buf * BUF_B + 1024 * pb)));
     const uint32_t so = (uint32_t)__builtin_amdgcn_readfirstlane((key_begin + tile * KT) * ROW_B + 1024 * pb);
     const int nleft = (PIECES + 3) / 4 - 4 * g;
+    // M0 is reserved to the compiler (a clobber of it is not honoured): the group saves it
+    // and puts it back, so a compiler-set M0 (the builtin LDS-DMA of bdma) stays valid
+    uint32_t keep;
     if (nleft >= 4)
       asm volatile(
-          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen offset:1024 lds\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen offset:2048 lds\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen offset:3072 lds" ::"s"(m0v),
+          "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen offset:1024 lds\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen offset:2048 lds\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen offset:3072 lds\n\ts_mov_b32 m0, %0" : "=&s"(keep) : "s"(m0v),
           "v"(16 * lane), "s"(e3rs), "s"(so)
           : "memory");
     else if (nleft == 3)
       asm volatile(
-          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen offset:1024 lds\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen offset:2048 lds" ::"s"(m0v),
+          "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen offset:1024 lds\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen offset:2048 lds\n\ts_mov_b32 m0, %0" : "=&s"(keep) : "s"(m0v),
           "v"(16 * lane), "s"(e3rs), "s"(so)
           : "memory");
     else if (nleft == 2)
       asm volatile(
-          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen offset:1024 lds" ::"s"(m0v),
+          "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen offset:1024 lds\n\ts_mov_b32 m0, %0" : "=&s"(keep) : "s"(m0v),
           "v"(16 * lane), "s"(e3rs), "s"(so)
           : "memory");
     else if (nleft == 1)
       asm volatile(
-          "s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\t"
-          "buffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v),
+          "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0" : "=&s"(keep) : "s"(m0v),
           "v"(16 * lane), "s"(e3rs), "s"(so)
           : "memory");
   };

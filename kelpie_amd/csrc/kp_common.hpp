@@ -48,6 +48,7 @@ struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
   hipStream_t s = nullptr;
+  hipMemPool_t pool = nullptr;  // the library's own pool of the device (kp_device_pool)
   std::vector<void*> old;
   void* ensure(size_t bytes) {
     if (bytes == 0) bytes = 16;
@@ -55,7 +56,10 @@ struct DevBuf {
       const size_t want = bytes + bytes / 4;
       void* q = nullptr;
       if (s) {
-        KP_HIP(hipMallocAsync(&q, want, s));
+        if (pool)
+          KP_HIP(hipMallocFromPoolAsync(&q, want, pool, s));
+        else
+          KP_HIP(hipMallocAsync(&q, want, s));
         if (p) KP_HIP(hipFreeAsync(p, s));
       } else {
         KP_HIP(hipMalloc(&q, want));

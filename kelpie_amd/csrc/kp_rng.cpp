@@ -1414,10 +1414,18 @@ int kp_rng_normal(uint8_t* ts, size_t tlen, int64_t n, float mean, float std_, i
 
 int kp_mt19937_discard(uint8_t* st, size_t len, uint64_t n) {
   if (!st || len < 24 + kN * 8) return KP_EINVAL;
-  TorchMt mt;
-  mt.load(st);
-  mt.skip(n);
-  mt.store(st);
+  // the jump-ahead (mt_charpoly / mt_jump_poly) can throw; no exception crosses the C ABI,
+  // and the caller's state blob is written only after a successful skip
+  try {
+    TorchMt mt;
+    mt.load(st);
+    mt.skip(n);
+    mt.store(st);
+  } catch (const std::bad_alloc&) {
+    return KP_ENOMEM;
+  } catch (...) {
+    return KP_EINVAL;
+  }
   return KP_OK;
 }
 

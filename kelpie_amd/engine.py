@@ -22,6 +22,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
+from .hparams import optimizer_hp
 from .data import MANY_TO_ONE, ONE_TO_ONE, Dataset, KelpieView
 from .models import FrozenModel
 from .rng import ReferenceRNG, StateCheckpoint
@@ -160,7 +161,9 @@ class PostTrainingEngine(RelevanceEngine):
 
     def __init__(self, model: FrozenModel, dataset: Dataset, hp: dict, rng: ReferenceRNG | None = None):
         RelevanceEngine.__init__(self, model=model, dataset=dataset)
-        self.hp = hp
+        # the reference's optimizer hp class (post_training_engine.py:71): a missing or
+        # mistyped field raises pydantic.ValidationError here, before any device work
+        self.hp = optimizer_hp(model.name, hp)
         self.rng = rng or ReferenceRNG()
         self._fused = []  # TransE calls whose edits and draws _flush_fused makes in two library calls
         self._sched = None

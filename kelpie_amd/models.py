@@ -284,6 +284,8 @@ def from_state_dict(name, dataset, state, model_params, device=0):
         v = state[k]
         return v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
 
+    from .hparams import model_params as _validated
+    model_params = _validated(name, model_params)  # explain.py:169-170, the reference's hp class
     E, R = arr("entity_embeddings"), arr("relation_embeddings")
     if name == "ComplEx":
         return ComplEx(dataset, E, R, init_scale=model_params.get("init_scale", 1e-3), device=device)

@@ -1,0 +1,111 @@
+"""Reference runs of the regularised full-width ComplEx case (development container only;
+TEST INFRASTRUCTURE: imports /root/reference through ``ref_harness``).
+
+``tests/test_gpu_parity.py::test_complex_vs_oracle_full_width`` runs D = 400 (d = 200)
+on the 2,000-entity synthetic graph (``synth.make_graph("small", seed=3)``, trained-scale
+0.3 weights), two ordinary predictions and a hub subject with more than one minibatch of
+rows, the first 4 training triples of each subject as singleton candidates, Adagrad 0.043
+for 20 epochs, and -- the cases this file exists for -- the N3 or N2 regulariser at
+weight 0.05 (ref ``regularizers.py:25-46``, ``multiclass_nll_optimizer.py:45-48``).
+This script runs the *reference itself* on exactly those inputs (seeds 42 once, then
+``set_cache()`` and the sequential ``compute_relevance`` calls of each prediction) in the
+two ``tools/conditioning.py`` variants, fp32 (as it runs) and fp64 (tables, optimizer
+state and arithmetic in float64, the random draws made in float32 as the fp32 run makes
+them), and records every post-training's target rank and score.
+
+    python tests/golden/make_reg_fullwidth_golden.py
+writes tests/golden/complex200_reg_fullwidth.json (data only)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import ref_harness  # noqa: E402
+from kelpie_amd import Dataset, synth  # noqa: E402
+
+HP = {"optimizer_name": "Adagrad", "batch_size": 512, "epochs": 20, "lr": 0.043, "decay1": 0.9, "decay2": 0.999,
+      "regularizer_name": "N3", "regularizer_weight": 0}
+DIM, SCALE, SEED = 200, 0.3, 3
+
+
+def case():
+    """The graph, weights, predictions and candidates of the full-width test."""
+    g = synth.make_graph("small", seed=SEED)
+    ds = Dataset(g.num_entities, g.num_relations, g.train, g.valid, g.test)
+    w = synth.make_weights("ComplEx", g.num_entities, g.num_relations, DIM, seed=SEED, trained_scale=SCALE)
+    deg = ds.entity_to_degree
+    test = [tuple(int(v) for v in t) for t in g.test]
+    preds = [t for t in test if 8 <= deg.get(t[0], 0) <= 40][:2]
+    preds.append(max(test, key=lambda t: deg.get(t[0], 0)))
+    cands = [sorted(ds.entity_to_training_triples[p[0]])[:4] for p in preds]
+    return g, ds, w, preds, cands
+
+
+def run(src, g, w, preds, cands, hp, fp64):
+    from conditioning import _Patches, to_double
+    from noise_floor import reference_model
+    from src.relevance_engines import NecessaryPostTrainingEngine
+    wl = {"model": "ComplEx", "shape": "small", "dim": DIM}
+    dataset, model = reference_model(src, wl, g, w)
+    patches = _Patches(fp64=True, dim=2 * DIM).__enter__() if fp64 else None
+    try:
+        if fp64:
+            to_double(model)
+        ref_harness.seed_all(42)
+        eng = NecessaryPostTrainingEngine(model, dataset, hp)
+        log = []
+        orig = eng.get_triple_results
+
+        def logged(m, triple):
+            r = orig(m, triple)
+            log.append({"rank": int(r["target_rank"]), "score": float(r["target_score"])})
+            return r
+
+        eng.get_triple_results = logged
+        out = []
+        for pred, cs in zip(preds, cands):
+            eng.set_cache()
+            blk = {"pred": list(pred), "calls": []}
+            for c in cs:
+                log.clear()
+                rel = float(eng.compute_relevance(pred, [c]))
+                blk["calls"].append({"rule": [list(c)], "relevance": rel, "results": list(log)})
+            out.append(blk)
+        return out
+    finally:
+        if patches is not None:
+            patches.__exit__(None, None, None)
+
+
+def main():
+    src = ref_harness.load_reference()
+    torch.set_num_threads(8)
+    g, ds, w, preds, cands = case()
+    rec = {"case": "tests/test_gpu_parity.py::test_complex_vs_oracle_full_width (D = 400, 2,000 entities, hub)",
+           "graph": {"shape": "small", "seed": SEED}, "weights": {"dim": DIM, "seed": SEED, "trained_scale": SCALE},
+           "init_scale": 1e-3, "hp": HP, "seed": 42, "preds": [list(p) for p in preds],
+           "candidates": [[list(c) for c in cs] for cs in cands], "runs": {}}
+    for reg in ("none", "N3", "N2"):
+        hp = dict(HP) if reg == "none" else dict(HP, regularizer_name=reg, regularizer_weight=0.05)
+        for variant in ("fp32", "fp64"):
+            t0 = time.time()
+            rec["runs"][f"{reg}_{variant}"] = run(src, g, w, preds, cands, hp, variant == "fp64")
+            print(reg, variant, f"{time.time() - t0:.0f}s",
+                  [[c["relevance"] for c in b["calls"]] for b in rec["runs"][f"{reg}_{variant}"]], flush=True)
+    with open(os.path.join(HERE, "complex200_reg_fullwidth.json"), "w") as f:
+        json.dump(rec, f, indent=0)
+
+
+if __name__ == "__main__":
+    main()
