@@ -348,6 +348,68 @@ def launch_local_ranks(n):
     return subprocess.call(cmd)
 
 
+def load_builder_fixture(workload):
+    """tests/golden/builder/<workload>__{fp32,fp64}.json: the reference's own pipeline
+    (prefilter k = 20, StochasticBuilder at the default xsi) on the bench's predictions,
+    seeds 42 once (tools/builder_fixture.py, development container).  Data only."""
+    out = {}
+    for v in ("fp32", "fp64"):
+        path = os.path.join(ROOT, "tests", "golden", "builder", f"{workload}__{v}.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                rec = json.load(f)
+            out[v] = rec["runs"][v]["explanations"]
+            out["_file"] = os.path.relpath(path, ROOT).replace(f"__{v}.json", "__<variant>.json")
+    return out
+
+
+def builder_leg(model, ds, wl, n_preds, sharding=None):
+    """The whole explanation builder (the reference's own recorded metric, #relevances /
+    execution_time over StochasticBuilder.build_explanations, stochastic_builder.py:33-107;
+    explain.py:196): topology prefilter k = 20, singleton rules in one batch, compound
+    rules in speculative windows of 32 with generator rewinds -- the evaluations past a
+    window's stop are device work the metric does not count (``wasted``).  Seeds 42 once,
+    then the bench's first ``n_preds`` predictions in order, so the first one is the
+    prediction of the reference's builder fixture."""
+    import random
+    import torch
+    from kelpie_amd.pipeline import build_pipeline
+    random.seed(42)
+    np.random.seed(42)
+    torch.manual_seed(42)
+    pipe = build_pipeline(model, ds, wl["hp"], wl["mode"])
+    pipe.engine.sharding = sharding
+    preds = pick_preds(ds, n_preds, seed=1234)
+    exs = []
+    for pred in preds:
+        exs.append(pipe.explain(pred=pred, prefilter_k=20))
+    st = pipe.builder.stats
+    n_rel = sum(ex["#relevances"] for ex in exs)
+    t = sum(ex["execution_time"] for ex in exs)
+    out = {"metric": "#relevances / execution_time (the reference's recorded builder metric)",
+           "value": n_rel / t if t > 0 else None, "unit": "relevances/s", "predictions": len(exs),
+           "relevances": n_rel, "execution_time_s": t, "evaluated": st["evaluated"], "wasted": st["wasted"],
+           "engine_batches": st["batches"], "xsi": pipe.builder.xsi, "prefilter_k": 20,
+           "speculative_window": pipe.builder.spec_window,
+           "per_prediction": [{"#relevances": ex["#relevances"], "execution_time_s": ex["execution_time"]}
+                              for ex in exs]}
+    fx = load_builder_fixture(wl["_name"])
+    if fx and exs:
+        got = exs[0]
+        top = [[list(t) for t in rule] for rule, _ in got["rule_to_relevance"]]
+        m = {"fixture": fx["_file"]}
+        for v in ("fp32", "fp64"):
+            if v in fx:
+                ref = fx[v][0]
+                m[v] = {"#relevances_equal": got["#relevances"] == ref["#relevances"],
+                        "top10_rules_equal": top == [[list(t) for t in rule] for rule, _ in ref["rule_to_relevance"]],
+                        "max_abs_relevance_diff_top10": max(
+                            [abs(a[1] - b[1]) for a, b in zip(got["rule_to_relevance"], ref["rule_to_relevance"])]
+                            or [0.0])}
+        out["reference_match_first_prediction"] = m
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -356,6 +418,8 @@ def main():
     ap.add_argument("--workload", default="complex-fb15k237-sufficient", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--preds-per-step", type=int, default=None, help="override the workload's predictions per step")
+    ap.add_argument("--builder-preds", type=int, default=4,
+                    help="predictions explained end to end by the builder leg after the timed region (0: none)")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
@@ -371,7 +435,7 @@ def main():
     from kelpie_amd import distributed as kd
     from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine
     rank, world, local = kd.init_from_env()
-    wl = WORKLOADS[args.workload]
+    wl = dict(WORKLOADS[args.workload], _name=args.workload)
     # one GPU per rank; on a box with fewer GPUs than ranks (gloo rehearsal) they share
     device = local % max(1, torch.cuda.device_count()) if torch.cuda.is_available() else 0
     ds, model, weights = build(wl, device, rank)
@@ -506,6 +570,13 @@ def main():
     roof["timing"] = ("achieved = algorithmic work / union of the launches' intervals (HIP events on a shared "
                       "time base); avg_launch_ms = mean launch duration")
 
+    builder = None
+    if args.builder_preds > 0:
+        # the whole builder over the workload's first predictions (every rank, the slots of
+        # each engine batch sharded as above), after the timed singleton region
+        builder = builder_leg(model, ds, wl, args.builder_preds, kd.SlotSharding() if world > 1 else None)
+        log(f"[rank {rank}] builder leg: {json.dumps(builder)}")
+
     cpu = None
     parity = None
     if rank == 0:
@@ -557,7 +628,7 @@ def main():
                 "reference_fp32_vs_fp64_max_abs_diff": parity.get("reference_fp32_vs_fp64_max_abs_diff"),
                 # the timed steps' relevances, bit for bit (A/B runs of two builds compare it)
                 "results_sha16": hashlib.sha256(np.asarray([r[0] for r in recs], np.float64).tobytes()).hexdigest()[:16],
-                "roofline": roof, "cpu_baseline": cpu}
+                "roofline": roof, "cpu_baseline": cpu, "builder": builder}
         print(json.dumps(line), flush=True)
 
 

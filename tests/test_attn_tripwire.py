@@ -1,0 +1,57 @@
+"""Tripwire for the LDS-DMA hazard of the attention kernels.
+
+Two non-shipped variants of the compiler-visible read form of ``kp_attn3`` (the one the
+ConvE instantiation ``kp_attn3<13, ATT_BCE_O>`` ships in) gave wrong partials that
+changed from run to run.  The shipped form passes, but nothing else would notice the
+hazard returning after a compiler or layout change, so this test reruns the ConvE
+post-training batch at the YAGO3-10 shape (123,182 entities: 3,850 key tiles, the
+bench's own ConvE workload, 20 candidates of one prediction, 109 Adam steps each) and
+asserts that every relevance, rank and post-trained score is bitwise equal across
+reruns on fresh contexts, and -- the fp64 check -- equal to the same batch with the
+fp32 attention (``KP_ATTN=f32``, ``kp_attn``, no LDS-DMA of the split image) within the
+accumulation-order spread of the two contractions.  The ComplEx instantiation
+(``kp_attn3<25>``, inline-asm reads) gets the same rerun check on the headline workload.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(workload, n_cands):
+    import bench
+    from golden_io import seed_all
+    from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine
+    wl = bench.WORKLOADS[workload]
+    ds, model, _ = bench.build(wl, 0, 0)
+    pred = bench.pick_preds(ds, 1, seed=1234)[0]
+    cands = bench.candidates_of(ds, pred, n_cands)
+    cls = SufficientPostTrainingEngine if wl["mode"] == "sufficient" else NecessaryPostTrainingEngine
+    seed_all(42)
+    eng = cls(model, ds, wl["hp"])
+    if wl["mode"] == "sufficient":
+        eng.select_entities_to_convert(pred, wl["convert"], 200)
+    rels = eng.compute_relevance_batch(pred, [[c] for c in cands])
+    res = eng.last_results if wl["mode"] == "necessary" else [pb for rj in eng.last_results for pb in rj]
+    return (np.asarray(rels, np.float64),
+            np.asarray([(pt["target_rank"], b["target_rank"]) for pt, b in res], np.int64),
+            np.asarray([(pt["target_score"], b["target_score"]) for pt, b in res], np.float64))
+
+
+@pytest.mark.parametrize("workload,n_cands", [("conve-yago310-necessary", 20), ("complex-fb15k237-sufficient", 6)])
+def test_attention_rerun_bitwise(workload, n_cands):
+    a = _run(workload, n_cands)
+    b = _run(workload, n_cands)
+    for x, y in zip(a, b):
+        assert x.tobytes() == y.tobytes()
+
+
+def test_conve_attention_matches_fp32_contraction(monkeypatch):
+    got = _run("conve-yago310-necessary", 20)
+    monkeypatch.setenv("KP_ATTN", "f32")
+    ref = _run("conve-yago310-necessary", 20)
+    # scores: the two contractions differ in accumulation order only (1e-5 relative);
+    # ranks come from the fp64 logit rank on both paths and agree but for near-ties
+    assert np.allclose(got[2], ref[2], rtol=1e-5, atol=0)
+    assert np.abs(got[1] - ref[1]).max() <= 1
+    assert np.mean(got[1] == ref[1]) >= 0.9

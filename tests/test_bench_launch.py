@@ -14,7 +14,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 RUNNER = os.path.join(HERE, "bench_standin.py")
-ARGS = ["--workload", "transe-fb15k237-necessary", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+ARGS = ["--workload", "transe-fb15k237-necessary", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+        "--builder-preds", "1"]
 
 
 def _env():
@@ -41,6 +42,9 @@ def test_bench_gpus2_launches_two_ranks_and_matches_one():
     assert two["config"]["predictions_per_step"] == one["config"]["predictions_per_step"] == 2
     assert two["config"]["candidates_per_step"] == one["config"]["candidates_per_step"]
     assert two["results_sha16"] == one["results_sha16"]
+    # the builder leg (one prediction end to end) on two ranks equals the one-rank leg
+    assert two["builder"]["relevances"] == one["builder"]["relevances"] > 0
+    assert two["builder"]["evaluated"] == one["builder"]["evaluated"]
 
 
 def test_bench_world_size_mismatch_refused():

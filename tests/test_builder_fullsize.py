@@ -1,0 +1,169 @@
+"""The whole explanation builder at full size against the reference itself.
+
+The north star asks for identical explanation rankings, and the reference's recorded
+metric counts the whole ``StochasticBuilder`` (ref ``stochastic_builder.py:33-107``):
+singleton rules, then compound rules of length 2..4 in prescore order with the early
+exit on ``xsi`` and the stochastic stop (``:140-175``: a sliding window of 10 relevances
+and one ``random.random()`` per rule below the best).  ``tools/builder_fixture.py`` ran
+the reference's own pipeline (``explain.py:49-89,196``: topology prefilter k = 20, the
+builder, seeds 42 once before the first prediction) on the bench workloads' synthetic
+graphs and weights, as it runs (fp32) and in float64, and recorded every
+``compute_relevance`` call, every ``random.random()`` value and the ``output.json``
+record (tests/golden/builder/<name>__<variant>.json).
+
+The GPU run (``kelpie_amd.pipeline.build_pipeline`` over the HIP engine, speculative
+windows of 32 rules with generator rewinds) must reproduce, per prediction:
+
+* the prefiltered candidates and the sequence of evaluated rules, call for call, of a
+  reference variant (so the same early exits and stochastic stops);
+* the same ``random.random()`` values, and the same ``#relevances``;
+* every relevance where the reference variants agree, within 1e-4 (relative above 1),
+  else between them (rank deltas near a tie resolve differently in fp32 and fp64,
+  DESIGN.md section 3);
+* the same top-10 ``rule_to_relevance`` rules in the same order.
+"""
+import glob
+import json
+import os
+import random
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DIR = os.path.join(HERE, "golden", "builder")
+NAMES = sorted({os.path.basename(p).rsplit("__", 1)[0] for p in glob.glob(os.path.join(DIR, "*__fp32.json"))})
+TOL = 1e-4
+
+
+def load(name):
+    out = {}
+    for v in ("fp32", "fp64"):
+        if not os.path.exists(os.path.join(DIR, f"{name}__{v}.json")):
+            continue
+        with open(os.path.join(DIR, f"{name}__{v}.json")) as f:
+            rec = json.load(f)
+        run = rec["runs"][v]
+        assert not run.get("truncated"), (name, v)
+        for ex in run["explanations"]:
+            # labels -> ids (the synthetic datasets' e%06d / r%04d labels, kelpie_amd.data.Dataset)
+            ex["rule_to_relevance"] = [([[int(t[0][1:]), int(t[1][1:]), int(t[2][1:])] for t in rule], rel)
+                                       for rule, rel in ex["rule_to_relevance"]]
+        out[v] = (rec, run["explanations"])
+    return out
+
+
+def calls_of(ex):
+    return [(tuple(tuple(t) for t in c["rule"]), c["relevance"]) for c in ex["calls"]]
+
+
+def _close(a, b):
+    return abs(a - b) <= TOL * max(1.0, abs(b))
+
+
+def check_prediction(got_calls, got_draws, got_ex, refs):
+    """``refs``: {variant: reference explanation record} of one prediction.  Returns the
+    variants whose whole call sequence the GPU reproduced (at least one, or it fails)."""
+    seqs = {v: calls_of(ex) for v, ex in refs.items()}
+    rules = [r for r, _ in got_calls]
+    same = [v for v, s in seqs.items() if [r for r, _ in s] == rules]
+    assert same, ("evaluated rule sequence differs from every reference variant",
+                  {v: len(s) for v, s in seqs.items()}, len(rules))
+    for i, (rule, rel) in enumerate(got_calls):
+        # every variant that evaluated the same rules up to and including call i
+        vals = [s[i][1] for v, s in seqs.items() if len(s) > i and [r for r, _ in s[:i + 1]] == rules[:i + 1]]
+        lo, hi = min(vals), max(vals)
+        if all(_close(x, vals[0]) for x in vals):
+            assert _close(rel, vals[0]), (i, rule, rel, vals)
+        else:
+            tol = TOL * max(1.0, abs(lo), abs(hi))
+            assert lo - tol <= rel <= hi + tol, (i, rule, rel, vals)
+    for v in same:
+        ex = refs[v]
+        assert got_draws == pytest.approx(ex["random_draws"], abs=0), v
+        assert got_ex["#relevances"] == ex["#relevances"], (v, got_ex["#relevances"], ex["#relevances"])
+    # the top-10 rules, in order, as one of the variants that evaluated the same rules
+    got_top = [[tuple(t) for t in rule] for rule, _ in got_ex["rule_to_relevance"]]
+    tops = {v: [[tuple(t) for t in rule] for rule, _ in refs[v]["rule_to_relevance"]] for v in same}
+    assert any(got_top == t for t in tops.values()), (got_top, tops)
+    return same
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_builder_fixture_well_formed(name):
+    """Both reference runs explain the same predictions from the same prefiltered
+    candidates; each run's #relevances equals its calls, and its random draws are the
+    builder's (one per compound rule below the running best, after the first 10)."""
+    refs = load(name)
+    assert set(refs) == {"fp32", "fp64"}, sorted(refs)
+    (r32, e32), (r64, e64) = refs["fp32"], refs["fp64"]
+    assert r32["preds"] == r64["preds"] and len(e32) == len(e64) == len(r32["preds"])
+    for a, b in zip(e32, e64):
+        assert a["pred"] == b["pred"] and a["candidates"] == b["candidates"]
+        assert 0 < len(a["candidates"]) <= r32["prefilter_k"]
+        for ex in (a, b):
+            assert ex["#relevances"] == len(ex["calls"])
+            assert len(ex["rule_to_relevance"]) == min(10, len(ex["calls"]))
+
+
+def run_gpu(name):
+    """The GPU pipeline over the fixture's predictions: per prediction the evaluated
+    (rule, relevance) sequence, the random.random() values and the output record."""
+    import bench
+    from golden_io import seed_all
+    from kelpie_amd.pipeline import build_pipeline
+    refs = load(name)
+    rec = refs["fp32"][0]
+    wl = bench.WORKLOADS[rec["workload"]]
+    ds, model, _ = bench.build(wl, 0, 0)
+    seed_all(42)
+    pipe = build_pipeline(model, ds, wl["hp"], wl["mode"], xsi=rec["xsi"])
+    b = pipe.builder
+    calls, draws = [], []
+    orig_single, orig_comp = b.explore_singleton_rules, b.explore_compound_rules
+
+    def single(pred, triples):
+        out = orig_single(pred, triples)
+        calls.extend(((t,), r) for t, r in out.items())
+        return out
+
+    def comp(pred, triples, length, t2r):
+        out, n = orig_comp(pred, triples, length, t2r)
+        calls.extend((tuple(r), v) for r, v in out.items())
+        return out, n
+
+    b.explore_singleton_rules, b.explore_compound_rules = single, comp
+    orig_random = random.random
+
+    def rnd():
+        v = orig_random()
+        draws.append(v)
+        return v
+
+    random.random = rnd
+    results = []
+    try:
+        for pred in rec["preds"]:
+            calls.clear()
+            draws.clear()
+            ex = pipe.explain(pred=tuple(pred), prefilter_k=rec["prefilter_k"])
+            rules = [(tuple(tuple(ds.ids_triple(t)) for t in rule), r) for rule, r in ex["rule_to_relevance"]]
+            ex = dict(ex, rule_to_relevance=[([list(t) for t in rule], r) for rule, r in rules])
+            results.append((list(calls), list(draws), ex))
+    finally:
+        random.random = orig_random
+    return refs, results, b.stats
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_builder_vs_reference(name):
+    refs, results, stats = run_gpu(name)
+    n = len(refs["fp32"][1])
+    assert len(results) == n
+    for k in range(n):
+        got_calls, got_draws, got_ex = results[k]
+        ref_k = {v: refs[v][1][k] for v in refs}
+        cands = [tuple(r[0]) for r, _ in got_calls if len(r) == 1]
+        assert [list(c) for c in cands] == ref_k["fp32"]["candidates"]
+        check_prediction(got_calls, got_draws, got_ex, ref_k)
+    assert stats["evaluated"] - stats["wasted"] == sum(ex["#relevances"] for _, _, ex in results)
