@@ -377,7 +377,9 @@ def builder_leg(model, ds, wl, n_preds, sharding=None):
     random.seed(42)
     np.random.seed(42)
     torch.manual_seed(42)
-    pipe = build_pipeline(model, ds, wl["hp"], wl["mode"])
+    # speculative windows: "auto" (kelpie_amd.builder) or a fixed size (KELPIE_BUILDER_WINDOW, A/B)
+    win = os.environ.get("KELPIE_BUILDER_WINDOW", "auto")
+    pipe = build_pipeline(model, ds, wl["hp"], wl["mode"], window=win if win == "auto" else int(win))
     pipe.engine.sharding = sharding
     preds = pick_preds(ds, n_preds, seed=1234)
     exs = []
@@ -390,7 +392,7 @@ def builder_leg(model, ds, wl, n_preds, sharding=None):
            "value": n_rel / t if t > 0 else None, "unit": "relevances/s", "predictions": len(exs),
            "relevances": n_rel, "execution_time_s": t, "evaluated": st["evaluated"], "wasted": st["wasted"],
            "engine_batches": st["batches"], "xsi": pipe.builder.xsi, "prefilter_k": 20,
-           "speculative_window": pipe.builder.spec_window,
+           "speculative_window": "auto" if pipe.builder.auto else pipe.builder.spec_window,
            "per_prediction": [{"#relevances": ex["#relevances"], "execution_time_s": ex["execution_time"]}
                               for ex in exs]}
     fx = load_builder_fixture(wl["_name"])

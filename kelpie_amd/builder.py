@@ -6,12 +6,21 @@ summarisation), restructured for a batched engine:
 
 * all singleton rules of a prediction are evaluated in ONE engine batch
   (the reference's hot loop A, ``:110-124``);
-* compound rules are evaluated in speculative windows of ``window`` rules in
-  prescore order (hot loop B, ``:126-175``).  The accept / early-return /
+* compound rules are evaluated in speculative windows of rules in prescore
+  order (hot loop B, ``:126-175``).  The accept / early-return /
   ``random.random()`` termination logic is then replayed sequentially over the
   window's relevances; if the search stops inside the window, the torch /
   numpy generators are rewound to the state right after the last rule the
   reference would have evaluated, so every later draw is unchanged.
+
+Window sizes: a fixed ``window``, or ``window="auto"``: the rules before index 10
+of a length (the sliding window's size: no stochastic stop can happen there, only
+the early exit on ``xsi``) go as one window, and after that each window holds about
+as many rules as the search is expected to run before it stops, from the stop
+probability the replay has reached (1 - average / best of the sliding window),
+between ``AUTO_MIN`` and ``AUTO_MAX`` rules.  Either way the results, the draws and
+``#relevances`` are those of the sequential reference; only the device work spent
+past a stop (``stats["wasted"]``) and the number of engine batches change.
 """
 from __future__ import annotations
 
@@ -21,7 +30,9 @@ import time
 
 
 class StochasticBuilder:
-    def __init__(self, xsi, engine, summarization: str = None, max_explanation_length: int = 4, window: int = 32):
+    AUTO_MIN, AUTO_MAX = 4, 32
+
+    def __init__(self, xsi, engine, summarization: str = None, max_explanation_length: int = 4, window=32):
         if summarization is not None:
             raise NotImplementedError("summarisation (simulation / bisimulation) is out of scope")
         self.xsi = xsi
@@ -29,7 +40,8 @@ class StochasticBuilder:
         self.dataset = engine.dataset
         self.length_cap = max_explanation_length
         self.window_size = 10  # the reference's sliding window (stochastic_builder.py:24)
-        self.spec_window = max(1, int(window))
+        self.auto = window == "auto"
+        self.spec_window = self.AUTO_MAX if self.auto else max(1, int(window))
         self.summarization = None
         self.stats = {"batches": 0, "evaluated": 0, "wasted": 0}
 
@@ -80,7 +92,7 @@ class StochasticBuilder:
         computed = 0
         i = 0
         while i < len(rules) and not terminate:
-            chunk = [r for r, _ in rules[i:i + self.spec_window]]
+            chunk = [r for r, _ in rules[i:i + self._window(i, window, best)]]
             cps = []
             rels = self.engine.compute_relevance_batch(pred, [list(r) for r in chunk], checkpoints=cps)
             self.stats["batches"] += 1
@@ -108,3 +120,17 @@ class StochasticBuilder:
                 self.stats["wasted"] += len(chunk) - stop_at - 1
             i += len(chunk)
         return rule_to_relevance, computed
+
+    def _window(self, i, window, best):
+        """Rules in the next speculative window (see the module docstring)."""
+        if not self.auto:
+            return self.spec_window
+        if i < self.window_size:
+            return self.window_size - i
+        if best == 0:
+            return self.AUTO_MIN
+        thr = (sum(window) / self.window_size) / best
+        p_stop = min(1.0, max(0.0, 1.0 - thr))  # P(random.random() > thr) per rule below the best
+        if p_stop <= 1.0 / self.AUTO_MAX:
+            return self.AUTO_MAX
+        return int(min(self.AUTO_MAX, max(self.AUTO_MIN, round(1.0 / p_stop))))

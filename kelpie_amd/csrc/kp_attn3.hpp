@@ -105,6 +105,12 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_ATTN_FULLTILE_ALL
 #define KP_ATTN_FULLTILE_ALL 0  // ... on the compiler-visible read form (ConvE) as well
 #endif
+#ifndef KP_CV_EXACT_BCE
+// ConvE BCE-through-sigmoid weight (kp_attn3 ATT_BCE_O and kp_conve.hip bce_g): bit 0 the
+// accurate sigmoid (expf, IEEE division), bit 1 (p - y) * gs where p(1 - p) >= 1e-12 (the
+// value the reference's ((p - y) / p(1 - p) * gs) * p(1 - p) rounds to in exact arithmetic)
+#define KP_CV_EXACT_BCE 0
+#endif
 #ifndef KP_ASM_ALL
 #define KP_ASM_ALL 0  // 1: the asm read form for every DB (ConvE included)
 #endif
@@ -673,9 +679,19 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
+#if KP_CV_EXACT_BCE & 1
+              const float x0 = 1.0f / (1.0f + expf(-sc[u][r]));
+#else
               const float x0 = __builtin_amdgcn_rcpf(1.0f + __expf(-sc[u][r]));
+#endif
               const float w0 = (1.0f - x0) * x0;
+#if KP_CV_EXACT_BCE & 2
+              const float gw = w0 >= 1e-12f ? (x0 - ylo) * gsc
+                                            : (((x0 - ylo) * __builtin_amdgcn_rcpf(1e-12f)) * gsc) * w0;
+              pw[u][r] = keep(u, r) ? gw : 0.f;
+#else
               pw[u][r] = keep(u, r) ? (((x0 - ylo) * __builtin_amdgcn_rcpf(fmaxf(w0, 1e-12f))) * gsc) * w0 : 0.f;
+#endif
             }
         } else {
           float v[2][4];

@@ -204,6 +204,9 @@ __global__ __launch_bounds__(256) void kp_cx_contrib(int half, const int4* __res
   }
 }
 
+#ifndef KP_CX_UPD64
+#define KP_CX_UPD64 0
+#endif
 // Sum a slot's contributions, add the N3 term, apply the optimizer (torch op order).
 template <int DP>
 __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __restrict__ act,
@@ -226,11 +229,18 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
   // load latency: ~90 us per step at FB15k-237 sizes); a slot with at most UPD_WIDE
   // rows keeps the sequential chain (the choice is block-uniform).
   constexpr int UPD_WIDE = 4;
-  __shared__ float red[4][DP];
+#if KP_CX_UPD64
+  // diagnostic / A-B: the slot's gradient assembled in fp64 (sums, 1/B, regulariser term),
+  // rounded once to fp32 before the optimizer (12.8 KiB of LDS at D = 400 instead of 6.4)
+  typedef double acc_t;
+#else
+  typedef float acc_t;
+#endif
+  __shared__ acc_t red[4][DP];
   if (nc > UPD_WIDE) {
     const int w = tid >> 6, lane = tid & 63;
     for (int d = lane; d < 2 * half; d += 64) {
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      acc_t acc[4] = {0.f, 0.f, 0.f, 0.f};
       int j = w;
       for (; j + 12 < nc; j += 16) {
 #pragma unroll
@@ -264,7 +274,7 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
   for (int u = 0; u < (DP / 2 + 255) / 256; ++u) {
     const int i = tid + 256 * u;
     if (i >= half) continue;
-    float gv[2] = {0.f, 0.f};
+    acc_t gv[2] = {0.f, 0.f};
     if (nc > UPD_WIDE) {
       gv[0] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
       gv[1] = (red[0][i + half] + red[1][i + half]) + (red[2][i + half] + red[3][i + half]);
@@ -275,19 +285,29 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
         gv[1] += c[i + half];
       }
     }
+#if KP_CX_UPD64
+    gv[0] /= (double)P.b;
+    gv[1] /= (double)P.b;
+#else
     gv[0] *= inv_b;
     gv[1] *= inv_b;
+#endif
     const float a = x[i], b = x[i + half];
     if (opt.reg_w != 0.f) {
+#if KP_CX_UPD64
+      const double mod = opt.reg_n2 ? (double)n2 : sqrt((double)a * a + (double)b * b);
+      const double k3 = 3.0 * (double)opt.reg_w / (double)P.b * (double)(P.cnt_l + P.cnt_r) * mod;
+#else
       const float mod = opt.reg_n2 ? n2 : sqrtf(a * a + b * b);
       const float k3 = 3.0f * opt.reg_w * inv_b * (float)(P.cnt_l + P.cnt_r) * mod;
+#endif
       gv[0] += k3 * a;
       gv[1] += k3 * b;
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int d = i + h * half;
-      const float gd = gv[h];
+      const float gd = (float)gv[h];
       float xd = h ? b : a;
       const size_t o = (size_t)slot * DP + d;
       if (opt.kind == KP_OPT_ADAGRAD) {

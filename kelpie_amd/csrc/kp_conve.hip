@@ -60,8 +60,15 @@ struct CvConst {
 
 __device__ __forceinline__ float bce_g(float s, float y, float gs) {
   // BCELoss backward (grad = gs) followed by sigmoid backward, torch op order
+#if KP_CV_EXACT_BCE & 1
+  const float p = 1.0f / (1.0f + expf(-s));
+#else
   const float p = 1.0f / (1.0f + __expf(-s));
+#endif
   const float w = (1.0f - p) * p;
+#if KP_CV_EXACT_BCE & 2
+  if (w >= 1e-12f) return (p - y) * gs;
+#endif
   return ((p - y) / fmaxf(w, 1e-12f) * gs) * w;
 }
 

@@ -51,7 +51,7 @@ class SufficientPipeline(Pipeline):
         return result
 
 
-def build_pipeline(model, dataset, hp, mode, prefilter=None, xsi=None, window=32, entity_classes=None):
+def build_pipeline(model, dataset, hp, mode, prefilter=None, xsi=None, window="auto", entity_classes=None):
     """explain.py:49-89 for the post-training engines (baseline=None, no summarisation)."""
     if prefilter == TYPE_PREFILTER:
         raise NotImplementedError("type_based prefilter: out of scope (kelpie_amd/prefilters.py)")

@@ -90,7 +90,7 @@ def run(src, g, w, preds, cands, hp, fp64):
 
 def main():
     src = ref_harness.load_reference()
-    torch.set_num_threads(8)
+    torch.set_num_threads(int(os.environ.get("REF_THREADS", "2")))
     g, ds, w, preds, cands = case()
     rec = {"case": "tests/test_gpu_parity.py::test_complex_vs_oracle_full_width (D = 400, 2,000 entities, hub)",
            "graph": {"shape": "small", "seed": SEED}, "weights": {"dim": DIM, "seed": SEED, "trained_scale": SCALE},

@@ -44,6 +44,8 @@ def load(name):
             rec = json.load(f)
         run = rec["runs"][v]
         assert not run.get("truncated"), (name, v)
+        if len(run["explanations"]) < len(rec["preds"]):
+            continue  # a run still being written
         for ex in run["explanations"]:
             # labels -> ids (the synthetic datasets' e%06d / r%04d labels, kelpie_amd.data.Dataset)
             ex["rule_to_relevance"] = [([[int(t[0][1:]), int(t[1][1:]), int(t[2][1:])] for t in rule], rel)

@@ -26,7 +26,7 @@ def test_sufficient_host_protocol(name):
 
 
 @pytest.mark.parametrize("name", ["transe_tiny", "complex_tiny", "conve60_tiny", "conve60_drop_tiny"])
-@pytest.mark.parametrize("window", [1, 4, 32])
+@pytest.mark.parametrize("window", [1, 4, 32, "auto"])
 def test_builder_speculative_windows(name, window):
     check_builder(name, "cpu", window=window)
 

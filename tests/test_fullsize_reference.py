@@ -79,6 +79,22 @@ def elementwise_misses(fx, got):
     return out
 
 
+def mirror_only(fx, got):
+    """Indices of the elements of ``got`` that the element-wise rule accepts only through
+    its mirror clause (outside every reference variant's range, but no farther from the
+    fp64 run than the fp32 run is), reported apart from the in-spread ones."""
+    runs = [run["rank_deltas"] for run in fx["runs"].values()]
+    f32 = fx["runs"].get("fp32", {}).get("rank_deltas")
+    f64 = fx["runs"].get("fp64", {}).get("rank_deltas")
+    out = []
+    for i, g in enumerate(got):
+        vals = sorted({r[i] for r in runs})
+        if not vals[0] <= g <= vals[-1] and len(vals) > 1 and f32 is not None and f64 is not None \
+                and abs(g - f64[i]) <= abs(f32[i] - f64[i]):
+            out.append(i)
+    return out
+
+
 def test_elementwise_rule():
     fx = {"runs": {"fp32": {"rank_deltas": [1, 5, 3]}, "fp64": {"rank_deltas": [1, 6, 3]},
                    "fp32_perm": {"rank_deltas": [1, 5, 3]}}}
@@ -90,6 +106,7 @@ def test_elementwise_rule():
                     "fp32_perm": {"rank_deltas": [10, 4]}}}
     assert elementwise_misses(fx2, [8, 4]) == [] and elementwise_misses(fx2, [7, 4]) == [(0, 7, [9, 10])]
     assert elementwise_misses(fx2, [9, 5]) == [(1, 5, [4])]  # all variants agree: equal only
+    assert mirror_only(fx2, [8, 4]) == [0] and mirror_only(fx2, [9, 4]) == [] and mirror_only(fx, [1, 7, 3]) == [1]
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=IDS)

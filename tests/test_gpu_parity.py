@@ -29,7 +29,7 @@ def test_sufficient_vs_reference_goldens(name):
 
 
 @pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny", "conve60_tiny"])
-@pytest.mark.parametrize("window", [1, 32])
+@pytest.mark.parametrize("window", [1, 32, "auto"])
 def test_builder_vs_reference_goldens(name, window):
     check_builder(name, "gpu", window=window)
 

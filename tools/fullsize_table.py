@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def main():
     import bench
-    from test_fullsize_reference import elementwise_misses
+    from test_fullsize_reference import elementwise_misses, mirror_only
     from kelpie_amd import NecessaryPostTrainingEngine, SufficientPostTrainingEngine
     args = [a for a in sys.argv[1:] if a != "all"]  # "all" (or nothing): every fixture
     names = args or sorted(os.path.basename(p)[:-5]
@@ -44,6 +44,10 @@ def main():
         par["fixture"] = name
         par["elements"] = len(par["gpu_rank_deltas"])
         par["elementwise_misses"] = elementwise_misses(fx, par["gpu_rank_deltas"])
+        # accepted only through the rule's mirror clause (reported apart)
+        par["mirror_only"] = mirror_only(fx, par["gpu_rank_deltas"])
+        f64 = fx["runs"]["fp64"]["rank_deltas"]
+        par["gpu_vs_fp64_equal"] = sum(a == b for a, b in zip(par["gpu_rank_deltas"], f64))
         r32 = fx["runs"]["fp32"]["rank_deltas"]
         par["ref_fp32_vs_perm_match"] = sum(a == b for a, b in zip(r32, fx["runs"]["fp32_perm"]["rank_deltas"])) \
             / len(r32) if "fp32_perm" in fx["runs"] else None
