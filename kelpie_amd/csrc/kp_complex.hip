@@ -230,17 +230,48 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
   // rows keeps the sequential chain (the choice is block-uniform).
   constexpr int UPD_WIDE = 4;
 #if KP_CX_UPD64
-  // diagnostic / A-B: the slot's gradient assembled in fp64 (sums, 1/B, regulariser term),
-  // rounded once to fp32 before the optimizer (12.8 KiB of LDS at D = 400 instead of 6.4)
+  // the slot's gradient assembled in fp64 (row sums, 1/B, regulariser term) and rounded
+  // once to fp32 before the optimizer; the four wave partials meet in two rounds through
+  // 2 x DP doubles, the LDS of the fp32 form (6.4 KiB at D = 400: it still fits beside a
+  // resident kp_attn3<25> workgroup)
   typedef double acc_t;
+  __shared__ double red[2][DP];
+  if (nc > UPD_WIDE) {
+    const int w = tid >> 6, lane = tid & 63;
+    double part[(DP + 63) / 64];
+#pragma unroll
+    for (int k = 0; k < (DP + 63) / 64; ++k) {
+      const int d = lane + 64 * k;
+      part[k] = 0.0;
+      if (d >= 2 * half) continue;
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      int j = w;
+      for (; j + 12 < nc; j += 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += crow(j + 4 * q)[d];
+      }
+      if (j < nc) acc[0] += crow(j)[d];  // at most three rows are left
+      if (j + 4 < nc) acc[1] += crow(j + 4)[d];
+      if (j + 8 < nc) acc[2] += crow(j + 8)[d];
+      part[k] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      if (w >= 2) red[w - 2][d] = part[k];
+    }
+    __syncthreads();
+    if (w < 2)
+#pragma unroll
+      for (int k = 0; k < (DP + 63) / 64; ++k) {
+        const int d = lane + 64 * k;
+        if (d < 2 * half) red[w][d] = part[k] + red[w][d];
+      }
+    __syncthreads();
+  }
 #else
   typedef float acc_t;
-#endif
-  __shared__ acc_t red[4][DP];
+  __shared__ float red[4][DP];
   if (nc > UPD_WIDE) {
     const int w = tid >> 6, lane = tid & 63;
     for (int d = lane; d < 2 * half; d += 64) {
-      acc_t acc[4] = {0.f, 0.f, 0.f, 0.f};
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
       int j = w;
       for (; j + 12 < nc; j += 16) {
 #pragma unroll
@@ -253,6 +284,7 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
     }
     __syncthreads();
   }
+#endif
   // N2 (regularizers.py:25-35): the factor of each batch row holding the kelpie entity
   // is ||f||^3 with f_i = |x_i| (complex modulus, complex.py:80-84), so its gradient is
   // 3 w / B * ||f|| * x per such row; ||f|| over the whole row, before the update
@@ -276,8 +308,13 @@ __global__ __launch_bounds__(256) void kp_cx_update(int half, const int4* __rest
     if (i >= half) continue;
     acc_t gv[2] = {0.f, 0.f};
     if (nc > UPD_WIDE) {
+#if KP_CX_UPD64
+      gv[0] = red[0][i] + red[1][i];
+      gv[1] = red[0][i + half] + red[1][i + half];
+#else
       gv[0] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
       gv[1] = (red[0][i + half] + red[1][i + half]) + (red[2][i + half] + red[3][i + half]);
+#endif
     } else {
       for (int j = 0; j < nc; ++j) {
         const float* c = crow(j);

@@ -60,20 +60,21 @@ run_step() {
       grep -v stamps $O/micro_$v$tagx.jsonl | cut -c1-260 | tail -$(( reps * ${#shapes[@]} )) || true
       grep stamps $O/micro_$v$tagx.jsonl | tail -2 || true ;;
     pmcmicro)
-      local v=${a[1]} i=0 envs=()
+      # pmcmicro:<variant>[:<envs>[:<shape index into MICRO_SHAPES, default 0 = ComplEx FB15k-237>]]
+      local v=${a[1]} i=0 envs=() si=${a[3]:-0}
       [ -n "${a[2]}" ] && IFS=',' read -r -a envs <<< "${a[2]}"
       for e in "${envs[@]}"; do export "$e"; done
       export TMPDIR=/tmp
       for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
                "GRBM_GUI_ACTIVE GRBM_COUNT TCC_HIT_sum TCC_MISS_sum" \
                "SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_VALU_MFMA_COEXEC_CYCLES"; do
-        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $P -d $R/$O/pmc_${v}_p$i -o run -- \
-          $R/variants/attn_micro_$v ${MICRO_SHAPES[0]} 0.05 > $R/$O/pmc_${v}_p$i.log 2>&1) || return 1
-        python3 tools/pmc_dump.py $O/pmc_${v}_p$i/run_results.db kp_attn >> $O/pmc_$v.txt 2>&1 || return 1
-        rm -rf $O/pmc_${v}_p$i
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $P -d $R/$O/pmc_${v}_s${si}_p$i -o run -- \
+          $R/variants/attn_micro_$v ${MICRO_SHAPES[$si]} 0.05 > $R/$O/pmc_${v}_s${si}_p$i.log 2>&1) || return 1
+        python3 tools/pmc_dump.py $O/pmc_${v}_s${si}_p$i/run_results.db kp_attn >> $O/pmc_${v}_s$si.txt 2>&1 || return 1
+        rm -rf $O/pmc_${v}_s${si}_p$i
         i=$((i + 1))
       done
-      cat $O/pmc_$v.txt ;;
+      cat $O/pmc_${v}_s$si.txt ;;
     bench)
       local w=${a[1]} st=${a[2]:-3} wu=${a[3]:-1} envs=() tagx=""
       if [ -n "${a[4]}" ]; then IFS=',' read -r -a envs <<< "${a[4]}"; tagx="_$(echo ${a[4]} | tr ',=/' '___')"; fi
