@@ -563,6 +563,12 @@ class SchedBatch:
         check(self._lib.kp_sched_batch_create(C.byref(h)))
         self.h = h.value
         self.views = []  # the NativeViews its slots point into (kept alive with the batch)
+        # the engine's TransE fast path (kelpie_amd/engine.py _flush_fused / _pack_native):
+        # slots created so far, one record per flush, the per-slot arrays built from them
+        self.n_slots = 0
+        self.recs = []
+        self.packed = None
+        self.dim = 0
 
     def __del__(self):
         h = getattr(self, "h", None)

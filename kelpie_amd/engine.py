@@ -292,12 +292,15 @@ class PostTrainingEngine(RelevanceEngine):
             own_pt = pt_owner == self.sharding.rank
         else:
             own_pt = True
+        sb = self._sched_batch()
         base = None
         if need_base:
             pending_base[pred] = len(slots)
-            base = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_base, owner=base_owner)
+            base = _Slot(None, None, None, kp, None, None, own_base, base_owner, (sb, sb.n_slots))
+            sb.n_slots += 1
             slots.append(base)
-        pt = _Slot(x0=None, rows=None, rng=None, pred=kp, filt=None, own=own_pt, owner=pt_owner)
+        pt = _Slot(None, None, None, kp, None, None, own_pt, pt_owner, (sb, sb.n_slots))
+        sb.n_slots += 1
         slots.append(pt)
         # a queued call: (view, kelpie triple, rule triples, flags, base slot, pt slot)
         self._fused.append((view, kp, [(int(a), int(b), int(c)) for a, b, c in triples],
@@ -322,8 +325,12 @@ class PostTrainingEngine(RelevanceEngine):
         sh = self.sharding
         nb = view.n_base_rows
         sufficient = mode == "sufficient"
-        fused, flush_at = self._fused, self._FUSED_FLUSH if self._sched is not None else self._FUSED_FIRST
+        first = self._sched is None
+        sb = self._sched_batch()
+        fused, flush_at = self._fused, self._FUSED_FIRST if first else self._FUSED_FLUSH
         out = []
+        suf = 8 if sufficient else 0
+        append = slots.append
         for rule in rules:
             triples = [(int(a), int(b), int(c)) for a, b, c in rule]
             need_base = pred not in self.base_pt_results and pred not in pending_base
@@ -338,20 +345,29 @@ class PostTrainingEngine(RelevanceEngine):
             else:
                 own_pt = True
             base = None
+            j = sb.n_slots
             if need_base:
                 pending_base[pred] = len(slots)
-                base = _Slot(None, None, None, kp, None, None, own_base, base_owner)
-                slots.append(base)
-            pt = _Slot(None, None, None, kp, None, None, own_pt, pt_owner)
-            slots.append(pt)
-            fused.append((view, kp, triples,
-                          (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
-                          | (8 if sufficient else 0), base, pt))
+                base = _Slot(None, None, None, kp, None, None, own_base, base_owner, (sb, j))
+                append(base)
+                j += 1
+            pt = _Slot(None, None, None, kp, None, None, own_pt, pt_owner, (sb, j))
+            append(pt)
+            sb.n_slots = j + 1
+            fused.append((view, kp, triples, (1 if need_base else 0) | (2 if own_base else 0) | (4 if own_pt else 0)
+                          | suf, base, pt))
             out.append((len(slots) - 1, pred))
             if len(fused) >= flush_at:
                 self._flush_fused()
                 fused, flush_at = self._fused, self._FUSED_FLUSH
         return out
+
+    def _sched_batch(self):
+        """This batch's native scheduler batch (created on its first TransE call)."""
+        if self._sched is None:
+            self._sched = _lib.SchedBatch()
+            self._sched.dim = self.model.dimension
+        return self._sched
 
     # queued TransE calls per library call (KELPIE_TE_FLUSH: A/B of the per-flush overhead
     # against how early the draws reach the workers).  Alternating on two boxes, 30 steps
@@ -373,40 +389,43 @@ class PostTrainingEngine(RelevanceEngine):
         return ValueError("list.remove(x): x not in list")
 
     def _flush_fused(self):
+        """Make the queued TransE calls' edits, rank filters (kp_sched_add_calls) and draws
+        (kp_rng_transe_calls, asynchronous) and record them with the scheduler batch: one
+        record per flush, whose arrays the pack reads by slot (:meth:`_pack_native`), so no
+        per-call Python work is left here beyond building the call arrays."""
         calls, self._fused = self._fused, []
         if not calls:
             return
         m, hp = self.model, self.hp
-        if self._sched is None:
-            self._sched = _lib.SchedBatch()
-        sb = self._sched
+        sb = self._sched_batch()
         nviews = [c[0].native for c in calls]
         sb.views.extend(nviews)  # its C++ slots point into these views: they live as long as the batch
         off = np.zeros(len(calls) + 1, np.int32)
-        off[1:] = np.cumsum([len(c[2]) for c in calls])
-        idx, rows, nf, (fc, code, k) = sb.add_calls([v.h for v in nviews], [c[1][1] for c in calls],
-                                                   [c[3] for c in calls], off,
+        np.cumsum([len(c[2]) for c in calls], out=off[1:])
+        flags = np.fromiter((c[3] for c in calls), np.int32, len(calls))
+        idx, rows, nf, (fc, code, k) = sb.add_calls([v.h for v in nviews], [c[1][1] for c in calls], flags, off,
                                                    [t for c in calls for t in c[2]])
+        n = len(calls) if fc < 0 else fc + 1  # the reference stops at the failing call
+        has_base = (flags[:n] & 1) != 0
+        r_base = np.where(has_base, rows[:n, 0], -1)
+        r_pt = rows[:n, 1].copy()
         if fc >= 0:
-            calls = calls[:fc + 1]  # the reference stops at the failing call
-        # plain ints once per flush (numpy scalar indexing per element costs ~0.2 us each)
-        idx, rows, nf = idx.tolist(), rows.tolist(), nf.tolist()
-        r_base = [rows[i][0] if c[3] & 1 else -1 for i, c in enumerate(calls)]
-        r_pt = [rows[i][1] if i != fc else -1 for i in range(len(calls))]
-        want = [(c[3] >> 1) & 3 for c in calls] if self._sharded() else None
-        xb, xp, draws = self.rng.transe_calls(m.dimension, m.dimension, r_base, r_pt, int(hp["epochs"]),
-                                              int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1,
-                                              want=want)
-        for i, c in enumerate(calls):
-            db, dp = draws[i]
-            ii, ri, ni = idx[i], rows[i], nf[i]
-            base, pt = c[4], c[5]
-            if base is not None:
-                base.x0, base.rng = xb[i], db
-                base.native = (sb, ii[0], ri[0], ni[0])
-            if i != fc:
-                pt.x0, pt.rng = xp[i], dp
-                pt.native = (sb, ii[1], ri[1], ni[1])
+            r_pt[fc] = -1
+        want = ((flags[:n] >> 1) & 3) if self._sharded() else None
+        xb, xp, out, sz = self.rng.transe_calls(m.dimension, m.dimension, r_base, r_pt, int(hp["epochs"]),
+                                                int(hp["negative_triples_ratio"]), m.dataset.num_entities + 1,
+                                                want=want, raw=True)
+        # the flush's slots in creation order: per call its base slot (if any), then its pt slot
+        first = calls[0][4] if calls[0][4] is not None else calls[0][5]
+        present = np.empty((n, 2), bool)
+        present[:, 0] = has_base
+        present[:, 1] = True
+        if fc >= 0:
+            present[fc, 1] = False
+        sb.recs.append({"j0": first.native[1], "present": present.ravel(), "idx": idx[:n].ravel(),
+                        "rows": rows[:n].ravel(), "nf": nf[:n].ravel(), "sz": sz.ravel(), "xb": xb, "xp": xp,
+                        "out": out})
+        sb.packed = None
         if fc >= 0:
             raise self._edit_error(calls[fc], code, k)
 
@@ -492,9 +511,9 @@ class PostTrainingEngine(RelevanceEngine):
     def _pack(self, slots, ctx=None):
         """The library call's batch arrays (x0, row_off, rows, rng_off, rng, pred, filt_off, filt)."""
         n = len(slots)
-        x0 = np.stack([s.x0 for s in slots]).astype(np.float32)
         if slots and slots[0].native is not None:
-            return (x0, *self._pack_native(slots, ctx))
+            return self._pack_native(slots, ctx)
+        x0 = np.stack([s.x0 for s in slots]).astype(np.float32)
         row_off = np.zeros(n + 1, np.int32)
         row_off[1:] = np.cumsum([len(s.rows) for s in slots])
         rows = np.concatenate([s.rows.reshape(-1, 3) for s in slots]).astype(np.int32) if row_off[-1] \
@@ -510,24 +529,93 @@ class PostTrainingEngine(RelevanceEngine):
         assert x0.shape == (n, self.model.dimension)
         return x0, row_off, rows, rng_off, rng, pred, filt_off, filt
 
+    @staticmethod
+    def _native_arrays(sb):
+        """The scheduler batch's flush records as per-slot arrays (indexed by the slot's
+        creation number j): scheduler slot index, row and filter counts, draw count and
+        offset, and the kelpie init row.  Read after the batch's draws are complete."""
+        if sb.packed is not None and sb.packed[0] == len(sb.recs):
+            return sb.packed[1]
+        N = sb.n_slots
+        idx = np.full(N, -1, np.int32)
+        nrow = np.zeros(N, np.int32)
+        nfl = np.zeros(N, np.int32)
+        nsz = np.zeros(N, np.int64)
+        x0 = np.zeros((N, sb.dim), np.float32)
+        outs, spans = [], []
+        for r in sb.recs:
+            pres = r["present"]
+            m = int(pres.sum())
+            js = r["j0"] + np.arange(m)
+            idx[js] = r["idx"][pres]
+            nrow[js] = r["rows"][pres]
+            nfl[js] = r["nf"][pres]
+            nsz[js] = r["sz"][pres]
+            n = len(pres) // 2
+            both = np.empty((n, 2, sb.dim), np.float32)
+            both[:, 0] = r["xb"][:n]
+            both[:, 1] = r["xp"][:n]
+            x0[js] = both.reshape(2 * n, sb.dim)[pres]
+            outs.append(r["out"])
+            spans.append((int(js[0]) if m else r["j0"], m))
+        # draw offsets per slot within the batch's concatenated draws (records in order)
+        doff = np.zeros(N + 1, np.int64)
+        np.cumsum(nsz, out=doff[1:])
+        arrays = {"idx": idx, "nrow": nrow, "nfl": nfl, "nsz": nsz, "doff": doff, "x0": x0, "outs": outs}
+        sb.packed = (len(sb.recs), arrays)
+        return arrays
+
     def _pack_native(self, slots, ctx=None):
-        """_pack's rows and filters written by the library's scheduler (kp_sched_pack)."""
+        """_pack for the TransE fast path: rows and filters written by the library's
+        scheduler (kp_sched_pack), kelpie init rows and draws taken from the flush
+        records by slot number."""
         n = len(slots)
         nat = [s.native for s in slots]
         sb = nat[0][0]
-        assert all(t is not None and t[0] is sb for t in nat), "one scheduler batch per device batch"
+        assert all(t[0] is sb for t in nat), "one scheduler batch per device batch"
+        a = self._native_arrays(sb)
+        js = np.fromiter((t[1] for t in nat), np.int64, n)
+        full = n == sb.n_slots and bool(np.all(js == np.arange(n)))
         row_off = np.zeros(n + 1, np.int32)
-        row_off[1:] = np.cumsum([t[2] for t in nat])
+        np.cumsum(a["nrow"][js], out=row_off[1:])
         filt_off = np.zeros(n + 1, np.int32)
-        filt_off[1:] = np.cumsum([t[3] for t in nat])
+        np.cumsum(a["nfl"][js], out=filt_off[1:])
         rows = np.empty((int(row_off[-1]), 3), np.int32)
         filt = np.empty(max(1, int(filt_off[-1])), np.int32)
-        sb.pack([t[1] for t in nat], rows, filt)
+        sb.pack(a["idx"][js], rows, filt)
         rng_off = np.zeros(n + 1, np.int64)
-        rng_off[1:] = np.cumsum([s.rng.size for s in slots])
-        rng = _contiguous_draws(slots, int(rng_off[-1]), ctx)
+        np.cumsum(a["nsz"][js], out=rng_off[1:])
+        rng = self._native_draws(a, js, full, int(rng_off[-1]), ctx)
+        x0 = a["x0"] if full else a["x0"][js]
         pred = np.array([s.pred for s in slots], np.int32)
-        return row_off, rows, rng_off, rng, pred, filt_off, filt
+        return x0, row_off, rows, rng_off, rng, pred, filt_off, filt
+
+    @staticmethod
+    def _native_draws(a, js, full, total, ctx):
+        """The draws of slots ``js`` back to back: the span of the page-locked arena the
+        flushes' draws were written into when they lie there in slot order (the usual
+        case: handed to the library as it is, uploaded by DMA), else a gather."""
+        if total == 0:
+            return np.zeros(1, np.int32)
+        outs = [o for o in a["outs"] if o is not None and o.size]
+        if full and outs:
+            lease = _lib.arena_of(outs[0])
+            start = outs[0].__array_interface__["data"][0]
+            pos = start
+            for o in outs:
+                if lease is None or _lib.arena_of(o) is not lease or o.__array_interface__["data"][0] != pos:
+                    break
+                pos += 4 * o.size
+            else:
+                if (pos - start) // 4 == total:
+                    off = (start - lease.__array_interface__["data"][0]) // 4
+                    return lease[off:off + total]
+        flat = np.concatenate(outs) if outs else np.zeros(0, np.int32)
+        if full:
+            return np.ascontiguousarray(flat[:total], np.int32)
+        doff, nsz = a["doff"], a["nsz"]
+        parts = [flat[doff[j]:doff[j] + nsz[j]] for j in js.tolist() if nsz[j]]
+        return np.concatenate(parts).astype(np.int32, copy=False) if parts else np.zeros(1, np.int32)
 
     def _run_slots(self, slots, ctx, fill):
         t_run = time.perf_counter()

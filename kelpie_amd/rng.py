@@ -305,7 +305,8 @@ class ReferenceRNG:
         _set_state(st)
         return out
 
-    def transe_calls(self, D: int, d: int, R_base, R_pt, epochs: int, ratio: int, n_entities: int, want=None):
+    def transe_calls(self, D: int, d: int, R_base, R_pt, epochs: int, ratio: int, n_entities: int, want=None,
+                     raw=False):
         """Every draw of n TransE compute_relevance calls in one library call
         (kp_rng_transe_calls).  Per call: ``torch.rand(1, D)``, the base row's
         ``xavier_normal_``, the base post-training's epoch draws (``R_base[i]`` >= 0),
@@ -313,16 +314,25 @@ class ReferenceRNG:
         Returns ``(x_base [n][d], x_pt [n][d], [(draws_base, draws_pt)] * n)``; the draws
         are complete on leaving :meth:`deferred` (or at once outside it).  ``want[i]``
         (bit 0 base, bit 1 pt; default all): an unwanted post-training's draws are not
-        made, only the generators advance past them (its entry is an empty array)."""
+        made, only the generators advance past them (its entry is an empty array).
+        ``raw``: return ``(x_base, x_pt, out, sizes)`` instead, with ``sizes`` [n][2] the
+        draw counts of each call's base and pt post-training, laid out back to back in
+        ``out`` in call order (no per-call arrays: the engine's TransE fast path packs
+        from them directly)."""
         _check_poison()
         global _outstanding, _torch_async
         addr = _np_mt_state_address()
-        w = [3] * len(R_base) if want is None else list(want)
-        sizes = [(epochs * 3 * max(rb, 0) if wi & 1 else 0, epochs * 3 * max(rp, 0) if wi & 2 else 0)
-                 for rb, rp, wi in zip(R_base, R_pt, w)]
-        total = sum(a + b for a, b in sizes)
+        rbv = np.maximum(np.asarray(R_base, np.int64), 0)
+        rpv = np.maximum(np.asarray(R_pt, np.int64), 0)
+        wa = None if want is None else np.array(want, np.uint8)
+        sz = np.empty((len(rbv), 2), np.int64)
+        sz[:, 0] = epochs * 3 * rbv
+        sz[:, 1] = epochs * 3 * rpv
+        if wa is not None:
+            sz[:, 0] *= (wa & 1) != 0
+            sz[:, 1] *= (wa & 2) != 0
+        total = int(sz.sum())
         std = float(np.float32(math.sqrt(2.0 / float(d + 1))))
-        wa = None if want is None else np.array(w, np.uint8)
         if self._defer_depth and _ASYNC:
             # the torch-stream walk runs on the library's walker thread; a walk already
             # carrying the stream continues it (the state passed is then not read)
@@ -352,8 +362,10 @@ class ReferenceRNG:
             if not self._defer_depth:
                 sync()
             _set_state(st)
+        if raw:
+            return xb, xp, out, sz
         draws, off, empty = [], 0, np.zeros(0, np.int32)
-        for a, b in sizes:
+        for a, b in sz.tolist():
             draws.append((out[off:off + a] if a else empty, out[off + a:off + a + b] if b else empty))
             off += a + b
         return xb, xp, draws

@@ -9,9 +9,10 @@ for 20 epochs, and -- the cases this file exists for -- the N3 or N2 regulariser
 weight 0.05 (ref ``regularizers.py:25-46``, ``multiclass_nll_optimizer.py:45-48``).
 This script runs the *reference itself* on exactly those inputs (seeds 42 once, then
 ``set_cache()`` and the sequential ``compute_relevance`` calls of each prediction) in the
-two ``tools/conditioning.py`` variants, fp32 (as it runs) and fp64 (tables, optimizer
+three ``tools/conditioning.py`` variants, fp32 (as it runs), fp64 (tables, optimizer
 state and arithmetic in float64, the random draws made in float32 as the fp32 run makes
-them), and records every post-training's target rank and score.
+them) and fp32_perm (fp32 with the coordinates' reduction order permuted), and records
+every post-training's target rank and score.
 
     python tests/golden/make_reg_fullwidth_golden.py
 writes tests/golden/complex200_reg_fullwidth.json (data only)
@@ -52,13 +53,18 @@ def case():
     return g, ds, w, preds, cands
 
 
-def run(src, g, w, preds, cands, hp, fp64):
-    from conditioning import _Patches, to_double
+def run(src, g, w, preds, cands, hp, fp64, perm=False):
+    from conditioning import _Patches, permuted_weights, to_double
     from noise_floor import reference_model
     from src.relevance_engines import NecessaryPostTrainingEngine
     wl = {"model": "ComplEx", "shape": "small", "dim": DIM}
+    cols = None
+    if perm:  # the same function with the coordinates' reduction order permuted
+        w, cols = permuted_weights(wl, w)
     dataset, model = reference_model(src, wl, g, w)
     patches = _Patches(fp64=True, dim=2 * DIM).__enter__() if fp64 else None
+    if cols is not None:
+        patches = _Patches(init_cols=cols, dim=2 * DIM).__enter__()
     try:
         if fp64:
             to_double(model)
@@ -96,14 +102,21 @@ def main():
            "graph": {"shape": "small", "seed": SEED}, "weights": {"dim": DIM, "seed": SEED, "trained_scale": SCALE},
            "init_scale": 1e-3, "hp": HP, "seed": 42, "preds": [list(p) for p in preds],
            "candidates": [[list(c) for c in cs] for cs in cands], "runs": {}}
+    path = os.path.join(HERE, "complex200_reg_fullwidth.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            rec["runs"] = json.load(f)["runs"]
     for reg in ("none", "N3", "N2"):
         hp = dict(HP) if reg == "none" else dict(HP, regularizer_name=reg, regularizer_weight=0.05)
-        for variant in ("fp32", "fp64"):
+        for variant in ("fp32", "fp64", "fp32_perm"):
+            if f"{reg}_{variant}" in rec["runs"]:
+                continue
             t0 = time.time()
-            rec["runs"][f"{reg}_{variant}"] = run(src, g, w, preds, cands, hp, variant == "fp64")
+            rec["runs"][f"{reg}_{variant}"] = run(src, g, w, preds, cands, hp, variant == "fp64",
+                                                  perm=variant == "fp32_perm")
             print(reg, variant, f"{time.time() - t0:.0f}s",
                   [[c["relevance"] for c in b["calls"]] for b in rec["runs"][f"{reg}_{variant}"]], flush=True)
-    with open(os.path.join(HERE, "complex200_reg_fullwidth.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(rec, f, indent=0)
 
 

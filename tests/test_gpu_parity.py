@@ -101,20 +101,27 @@ def test_complex_vs_oracle_full_width(dim, hot, part, reg, monkeypatch):
             res.append((rels, [(pt["target_rank"], pt["target_score"], b["target_rank"], b["target_score"])
                                for pt, b in eng.last_results]))
         out[backend] = res
-    # with a regulariser the oracle makes its gradient term in fp64 and Adagrad amplifies
-    # the difference on the coordinates it has not saturated: up to ~1e-3 of the score and
-    # one place (N3, measured); the reference golden complex200_n3_small pins the device
-    # against the reference itself at this width (test_necessary_vs_reference_goldens)
-    tol, slack = (1e-3, 1) if reg else (1e-4, 0)
-    n = match = 0
+    # The oracle computes the ComplEx step in fp64 and equals the reference's fp64 run on
+    # this exact case, regularised or not (tests/test_reg_fullwidth.py, from the reference
+    # itself): ranks exact and scores within 1e-4 on every post-training, except where the
+    # reference cannot meet 1e-4 itself -- its fp32 runs more than 1e-4 from its fp64 run
+    # (N3: one post-training of 12, fp32 1.5e-3 off) -- which test_reg_fullwidth holds to
+    # the reference's own spread instead
+    loose = set()
+    if reg:
+        from test_reg_fullwidth import GOLD, ill_conditioned
+        import json
+        with open(GOLD) as f:
+            loose = ill_conditioned(json.load(f), reg)
+    i = -1
     for (rg, dg), (rc, dc) in zip(out["gpu"], out["cpu"]):
         for a, b in zip(dg, dc):
-            n += 1
-            match += int(a[0] == b[0] and a[2] == b[2])
-            assert abs(a[0] - b[0]) <= slack and abs(a[2] - b[2]) <= slack, (a, b)
-            assert abs(a[1] - b[1]) <= tol * max(1.0, abs(b[1])), (a, b)
-            assert abs(a[3] - b[3]) <= tol * max(1.0, abs(b[3])), (a, b)
-    assert match >= n - slack * (n // 4), f"rank match {match}/{n}"
+            i += 1
+            if i in loose:
+                continue
+            assert a[0] == b[0] and a[2] == b[2], (i, a, b)
+            assert abs(a[1] - b[1]) <= 1e-4 * max(1.0, abs(b[1])), (i, a, b)
+            assert abs(a[3] - b[3]) <= 1e-4 * max(1.0, abs(b[3])), (i, a, b)
 
 
 TE_HP = {"batch_size": 2048, "epochs": 30, "lr": 0.01, "margin": 5, "negative_triples_ratio": 5,

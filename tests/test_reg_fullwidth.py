@@ -14,8 +14,12 @@ normalised first step turns into a full step), which is what the device test all
 
 The GPU test holds the device to the reference element by element, as the full-size
 fixtures are held (tests/test_fullsize_reference.py): ranks equal to the reference where
-its fp32 and fp64 runs agree, else between them; scores within 1e-4 relative of the fp64
-run where the fp32 run is within 1e-4 of it, else no farther from it than the fp32 run.
+its variants (fp32, fp64, fp32 with a permuted reduction order) agree, else between them;
+scores within 1e-4 relative of the fp64 run, or no farther from it than an fp32 variant.
+Where the reference itself misses 1e-4 (an fp32 variant more than 1e-4 from fp64: one
+post-training of the 36, N3's, whose fp32 run is 1.5e-3 off) the score is held to that
+spread and the rank to one place around the variants' ranks -- the rank an exact fp64
+count gives for a score inside that spread.
 """
 import json
 import os
@@ -70,18 +74,38 @@ def _run(rec, ds, w, reg, backend):
     return out
 
 
-def misses(got, r32, r64, tol=1e-4):
-    """Elements of ``got`` outside the reference's own fp32 / fp64 spread."""
+def ill_conditioned(rec, reg, tol=1e-4):
+    """Post-trainings where the reference cannot meet the north star's 1e-4 itself: one of
+    its fp32 runs (as it runs, or with a permuted reduction order) lies more than ``tol``
+    (relative) from its fp64 run in the pt or base score."""
+    r64 = _ref(rec, reg, "fp64")
+    fp32s = [_ref(rec, reg, v) for v in ("fp32", "fp32_perm") if f"{reg}_{v}" in rec["runs"]]
+    out = set()
+    for i, b in enumerate(r64):
+        for r in fp32s:
+            if abs(r[i][1] - b[1]) > tol * abs(b[1]) or abs(r[i][3] - b[3]) > tol * abs(b[3]):
+                out.add(i)
+    return out
+
+
+def misses(got, r32, r64, tol=1e-4, others=(), loose=()):
+    """Elements of ``got`` outside the reference's own spread: ranks between the smallest
+    and the largest of the reference variants (fp32, fp64, and the fp32 run with a
+    permuted reduction order when recorded), scores within ``tol`` of fp64 or no farther
+    from it than the farthest fp32 variant."""
     bad = []
     for i, (g, a, b) in enumerate(zip(got, r32, r64)):
+        vs = [a, b] + [o[i] for o in others]
+        slack = 1 if i in loose else 0  # an ill-conditioned post-training: one place either way
         for k in (0, 2):  # ranks
-            lo, hi = min(a[k], b[k]), max(a[k], b[k])
-            if not lo <= g[k] <= hi:
-                bad.append((i, "rank", g[k], a[k], b[k]))
+            lo, hi = min(v[k] for v in vs), max(v[k] for v in vs)
+            if not lo - slack <= g[k] <= hi + slack:
+                bad.append((i, "rank", g[k], [v[k] for v in vs]))
         for k in (1, 3):  # scores, against fp64
-            err, ref_err = abs(g[k] - b[k]) / abs(b[k]), abs(a[k] - b[k]) / abs(b[k])
+            err = abs(g[k] - b[k]) / abs(b[k])
+            ref_err = max(abs(v[k] - b[k]) / abs(b[k]) for v in vs)
             if err > max(tol, ref_err):
-                bad.append((i, "score", g[k], a[k], b[k]))
+                bad.append((i, "score", g[k], [v[k] for v in vs]))
     return bad
 
 
@@ -102,7 +126,10 @@ def test_device_within_reference_spread(reg):
     rec, ds, w = _case()
     got = _run(rec, ds, w, reg, "gpu")
     r32, r64 = _ref(rec, reg, "fp32"), _ref(rec, reg, "fp64")
-    print(json.dumps({"reg": reg, "gpu": got, "ref_fp32": r32, "ref_fp64": r64}))
-    assert not misses(got, r32, r64), misses(got, r32, r64)
+    others = [_ref(rec, reg, "fp32_perm")] if f"{reg}_fp32_perm" in rec["runs"] else []
+    print(json.dumps({"reg": reg, "gpu": got, "ref_fp32": r32, "ref_fp64": r64, "ref_other": others}))
+    loose = ill_conditioned(rec, reg)
+    bad = misses(got, r32, r64, others=others, loose=loose)
+    assert not bad, bad
     # and the ranks match the fp64 reference on all but at most one element
     assert sum(g[0] == b[0] and g[2] == b[2] for g, b in zip(got, r64)) >= len(got) - 1

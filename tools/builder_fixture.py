@@ -13,9 +13,10 @@ bench's synthetic graph and weights (``bench.build``), over a sequence of the be
 predictions in one process, seeds 42 once before the first (``explain.py:144``), so the
 generators carry over from one prediction to the next as they do in the reference.
 
-Two variants (``tools/conditioning.py`` patches): ``fp32`` (the reference as it runs)
-and ``fp64`` (tables, layers and optimizer state in float64, the random draws taken in
-float32 exactly as the fp32 run takes them).
+Three variants (``tools/conditioning.py`` patches): ``fp32`` (the reference as it runs),
+``fp64`` (tables, layers and optimizer state in float64, the random draws taken in
+float32 exactly as the fp32 run takes them) and ``fp32_perm`` (fp32 with the reduction
+order permuted: the ComplEx coordinates, or the ConvE filters).
 
 Recorded per prediction and variant: the prefiltered candidates, every
 ``compute_relevance`` call in order (rule, relevance, seconds), the target rank / score
@@ -64,7 +65,7 @@ def main():
     ap.add_argument("--workload", required=True, choices=sorted(bench.WORKLOADS))
     ap.add_argument("--preds", type=int, nargs="+", required=True,
                     help="indices into bench.pick_preds(seed=1234), explained in this order")
-    ap.add_argument("--variant", choices=["fp32", "fp64"], default="fp32")
+    ap.add_argument("--variant", choices=["fp32", "fp64", "fp32_perm"], default="fp32")
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--prefilter-k", type=int, default=20)
     ap.add_argument("--max-calls", type=int, default=400,
@@ -86,6 +87,12 @@ def main():
     all_preds = bench.pick_preds(ds, n_pick, seed=1234)
     preds = [all_preds[i] for i in args.preds]
 
+    cols = None
+    if args.variant == "fp32_perm":
+        # the same function with other reduction orders (tools/conditioning.py): ComplEx
+        # coordinates permuted in the tables and the kelpie init, ConvE filters permuted
+        from conditioning import permuted_weights
+        w, cols = permuted_weights(wl, w)
     dataset, model = noise_floor.reference_model(src, wl, g, w)
     if wl["mode"] == "sufficient":
         # synthetic graphs have entities with no training triple; the reference's degree
@@ -97,6 +104,8 @@ def main():
     if args.variant == "fp64":
         patches = _Patches(fp64=True, dim=D).__enter__()
         to_double(model)
+    elif cols is not None:
+        patches = _Patches(init_cols=cols, dim=D).__enter__()
 
     ref_harness.seed_all(42)  # explain.py:144, once for the whole sequence
     pipeline = build_pipeline(model, dataset, wl["hp"], wl["mode"], None, None, args.xsi, None)

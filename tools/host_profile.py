@@ -75,7 +75,8 @@ def main():
         if prof:
             prof.disable()
         dt = time.perf_counter() - t0
-        rows = sum(s.native[2] if s.native is not None else len(s.rows) for s in slots)
+        rows = (int(eng._native_arrays(slots[0].native[0])["nrow"].sum()) if slots and slots[0].native is not None
+                else sum(len(s.rows) for s in slots))
         t1 = time.perf_counter()
         eng._pack(slots)
         dp = time.perf_counter() - t1
