@@ -13,6 +13,12 @@ summarisation), restructured for a batched engine:
   numpy generators are rewound to the state right after the last rule the
   reference would have evaluated, so every later draw is unchanged.
 
+With ``pipelined`` (default) the next window is scheduled and started on a second
+device context before the current one's results are replayed (its draws follow the
+current window's; a stop inside the current window rewinds past both and the next
+window's device work is discarded), so the host's scheduling of a window overlaps the
+device's post-training of the previous one.
+
 Window sizes: a fixed ``window``, or ``window="auto"``: the rules before index 10
 of a length (the sliding window's size: no stochastic stop can happen there, only
 the early exit on ``xsi``) go as one window, and after that each window holds about
@@ -32,7 +38,8 @@ import time
 class StochasticBuilder:
     AUTO_MIN, AUTO_MAX = 4, 32
 
-    def __init__(self, xsi, engine, summarization: str = None, max_explanation_length: int = 4, window=32):
+    def __init__(self, xsi, engine, summarization: str = None, max_explanation_length: int = 4, window=32,
+                 pipelined=True):
         if summarization is not None:
             raise NotImplementedError("summarisation (simulation / bisimulation) is out of scope")
         self.xsi = xsi
@@ -41,6 +48,7 @@ class StochasticBuilder:
         self.length_cap = max_explanation_length
         self.window_size = 10  # the reference's sliding window (stochastic_builder.py:24)
         self.auto = window == "auto"
+        self.pipelined = bool(pipelined) and hasattr(engine, "submit_batch")
         self.spec_window = self.AUTO_MAX if self.auto else max(1, int(window))
         self.summarization = None
         self.stats = {"batches": 0, "evaluated": 0, "wasted": 0}
@@ -91,10 +99,33 @@ class StochasticBuilder:
         rule_to_relevance = {}
         computed = 0
         i = 0
-        while i < len(rules) and not terminate:
-            chunk = [r for r, _ in rules[i:i + self._window(i, window, best)]]
+        eng = self.engine
+        ahead = None  # the next window, scheduled and started speculatively: (rules, checkpoints, batch)
+
+        def submit(at):
+            chunk = [r for r, _ in rules[at:at + self._window(at, window, best)]]
             cps = []
-            rels = self.engine.compute_relevance_batch(pred, [list(r) for r in chunk], checkpoints=cps)
+            if self.pipelined:
+                return chunk, cps, eng.submit_batch(pred, [list(r) for r in chunk], checkpoints=cps)
+            return chunk, cps, None
+
+        while i < len(rules) and not terminate:
+            if ahead is not None:
+                chunk, cps, batch = ahead
+                ahead = None
+            else:
+                chunk, cps, batch = submit(i)
+            if self.pipelined:
+                if i + len(chunk) < len(rules):
+                    ahead = submit(i + len(chunk))  # scheduled while `batch` runs on the device
+                try:
+                    rels = eng.finish_batch(batch)
+                except BaseException:
+                    if ahead is not None:
+                        eng.finish_batch(ahead[2], discard=True)  # leave no device work behind
+                    raise
+            else:
+                rels = eng.compute_relevance_batch(pred, [list(r) for r in chunk], checkpoints=cps)
             self.stats["batches"] += 1
             self.stats["evaluated"] += len(chunk)
             stop_at = None
@@ -115,8 +146,17 @@ class StochasticBuilder:
                     if random.random() > thr:
                         stop_at, terminate = j, True
                         break
-            if stop_at is not None and stop_at + 1 < len(chunk):
-                cps[stop_at].restore()  # rewind the speculative draws
+            if stop_at is not None:
+                if ahead is not None:
+                    # the speculative next window: wait for its device work, drop its results
+                    eng.finish_batch(ahead[2], discard=True)
+                    self.stats["batches"] += 1
+                    self.stats["evaluated"] += len(ahead[0])
+                    self.stats["wasted"] += len(ahead[0])
+                    ahead = None
+                    cps[stop_at].restore()  # rewind past this window's later rules and the next one
+                elif stop_at + 1 < len(chunk):
+                    cps[stop_at].restore()  # rewind the speculative draws
                 self.stats["wasted"] += len(chunk) - stop_at - 1
             i += len(chunk)
         return rule_to_relevance, computed
@@ -127,6 +167,10 @@ class StochasticBuilder:
             return self.spec_window
         if i < self.window_size:
             return self.window_size - i
+        if any(v is None for v in window) or best == 0:
+            # a window scheduled before the replay has filled the sliding window (the
+            # pipelined builder's look-ahead), or a best of zero: no estimate
+            return 2 * self.AUTO_MIN
         if best == 0:
             return self.AUTO_MIN
         thr = (sum(window) / self.window_size) / best

@@ -670,6 +670,60 @@ class PostTrainingEngine(RelevanceEngine):
         self._raise_deferred(slots, pending)
         return outs
 
+    def _batch_items(self, pred, rules):
+        """compute_relevance_batch's one-item batch (the sufficient engine adds its
+        conversion entities)."""
+        return [(pred, rules)]
+
+    def submit_batch(self, pred, rules, checkpoints: list | None = None):
+        """The first half of ``compute_relevance_batch``: schedule the rules' reference-order
+        draws on this thread (with ``checkpoints`` as there) and start their device work on
+        the next of two pipeline contexts, without waiting; :meth:`finish_batch` returns the
+        relevances.  A later submit may be scheduled while this batch runs -- the
+        builder's next speculative window (kelpie_amd/builder.py) -- and rewinding the
+        generators to one of this batch's checkpoints undoes both."""
+        import threading
+
+        from . import rng as _rng_mod
+        ctxs = self.model.contexts(2)
+        self._submit_n = getattr(self, "_submit_n", -1) + 1
+        ctx = ctxs[self._submit_n % len(ctxs)]
+        busy = getattr(self, "_ctx_last", {}).get(id(ctx))
+        if busy is not None:
+            busy["thread"].join()  # a context runs one batch at a time (one context: no overlap)
+        self._deferred_error = None
+        with self.rng.deferred(detach=True) as d:
+            slots, pending, jobs = self._schedule_all(self._batch_items(pred, rules), checkpoints)
+        st = {"slots": slots, "pending": pending, "jobs": jobs, "deferred": self._deferred_error,
+              "ticket": d.last_ticket, "error": None, "stats": None}
+        self._deferred_error = None
+
+        def run():
+            try:
+                _rng_mod.wait_ticket(st["ticket"])
+                st["stats"] = dict(self._run(slots, ctx=ctx))
+            except BaseException as e:  # re-raised by finish_batch
+                st["error"] = e
+
+        st["thread"] = threading.Thread(target=run, daemon=True)
+        st["thread"].start()
+        self._ctx_last = {**getattr(self, "_ctx_last", {}), id(ctx): st}
+        return st
+
+    def finish_batch(self, st, discard=False):
+        """Wait for a :meth:`submit_batch` batch and return its relevances (``discard``: only
+        wait -- a speculative window the builder does not use -- and return None)."""
+        st["thread"].join()
+        if discard:
+            return None
+        if st["error"] is not None:
+            raise st["error"]
+        self._collect(st["slots"], st["stats"])
+        outs = self._finalize_multi(st["slots"], st["pending"], st["jobs"])
+        self._deferred_error = st["deferred"]
+        self._raise_deferred(st["slots"], st["pending"])
+        return outs[0]
+
     def _raise_deferred(self, slots, pending):
         """Re-raise the reference's error of a call the batch stopped at, after caching
         the base post-training it had already run (post_training_engine.py:46-62)."""
@@ -1010,6 +1064,9 @@ class SufficientPostTrainingEngine(PostTrainingEngine):
 
     def compute_relevance_batch(self, pred, rules, checkpoints: list | None = None):
         return self.compute_relevance_multi([(pred, rules, self.entities_to_convert)], checkpoints)[0]
+
+    def _batch_items(self, pred, rules):
+        return [(pred, rules, self.entities_to_convert)]
 
     def compute_relevance_multi(self, items, checkpoints: list | None = None):
         """[(pred, rules, entities_to_convert), ...] in ONE device batch."""
