@@ -379,7 +379,9 @@ def builder_leg(model, ds, wl, n_preds, sharding=None):
     torch.manual_seed(42)
     # speculative windows: "auto" (kelpie_amd.builder) or a fixed size (KELPIE_BUILDER_WINDOW, A/B)
     win = os.environ.get("KELPIE_BUILDER_WINDOW", "auto")
-    pipe = build_pipeline(model, ds, wl["hp"], wl["mode"], window=win if win == "auto" else int(win))
+    pipelined = os.environ.get("KELPIE_BUILDER_PIPELINED", "1") == "1"  # A/B: 0 = one window at a time
+    pipe = build_pipeline(model, ds, wl["hp"], wl["mode"], window=win if win == "auto" else int(win),
+                          pipelined=pipelined)
     pipe.engine.sharding = sharding
     preds = pick_preds(ds, n_preds, seed=1234)
     exs = []
@@ -393,6 +395,7 @@ def builder_leg(model, ds, wl, n_preds, sharding=None):
            "relevances": n_rel, "execution_time_s": t, "evaluated": st["evaluated"], "wasted": st["wasted"],
            "engine_batches": st["batches"], "xsi": pipe.builder.xsi, "prefilter_k": 20,
            "speculative_window": "auto" if pipe.builder.auto else pipe.builder.spec_window,
+           "windows_pipelined": pipe.builder.pipelined,
            "per_prediction": [{"#relevances": ex["#relevances"], "execution_time_s": ex["execution_time"]}
                               for ex in exs]}
     fx = load_builder_fixture(wl["_name"])

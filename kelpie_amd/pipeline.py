@@ -51,7 +51,8 @@ class SufficientPipeline(Pipeline):
         return result
 
 
-def build_pipeline(model, dataset, hp, mode, prefilter=None, xsi=None, window="auto", entity_classes=None):
+def build_pipeline(model, dataset, hp, mode, prefilter=None, xsi=None, window="auto", entity_classes=None,
+                   pipelined=True):
     """explain.py:49-89 for the post-training engines (baseline=None, no summarisation)."""
     if prefilter == TYPE_PREFILTER:
         raise NotImplementedError("type_based prefilter: out of scope (kelpie_amd/prefilters.py)")
@@ -60,11 +61,11 @@ def build_pipeline(model, dataset, hp, mode, prefilter=None, xsi=None, window="a
     if mode == "necessary":
         xsi = 5 if xsi is None else xsi
         engine = NecessaryPostTrainingEngine(model, dataset, hp)
-        return NecessaryPipeline(dataset, pf, StochasticBuilder(xsi, engine, window=window))
+        return NecessaryPipeline(dataset, pf, StochasticBuilder(xsi, engine, window=window, pipelined=pipelined))
     if mode == "sufficient":
         xsi = 0.9 if xsi is None else xsi
         engine = SufficientPostTrainingEngine(model, dataset, hp)
-        return SufficientPipeline(dataset, pf, StochasticBuilder(xsi, engine, window=window))
+        return SufficientPipeline(dataset, pf, StochasticBuilder(xsi, engine, window=window, pipelined=pipelined))
     raise ValueError(f"unknown mode {mode!r}")
 
 

@@ -78,7 +78,7 @@ run_step() {
     bench)
       local w=${a[1]} st=${a[2]:-3} wu=${a[3]:-1} envs=() tagx=""
       if [ -n "${a[4]}" ]; then IFS=',' read -r -a envs <<< "${a[4]}"; tagx="_$(echo ${a[4]} | tr ',=/' '___')"; fi
-      env "${envs[@]}" timeout -k 10 600 python bench.py --workload $w --steps $st --warmup $wu --no-cpu-baseline \
+      env "${envs[@]}" timeout -k 10 600 python bench.py --workload $w --steps $st --warmup $wu --no-cpu-baseline --builder-preds 0 \
         > $O/bench_$w$tagx.json 2> $O/bench_$w$tagx.err || { tail -5 $O/bench_$w$tagx.err; return 1; }
       python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], round(d['value'],1), 'cand/s', round(d['ms_per_step'],2), 'ms', 'frac', d['roofline']['frac'], 'fp64', d.get('rank_delta_match_rate_ref_fp64'))" $O/bench_$w$tagx.json "$w$tagx" ;;
     benchcpu)
@@ -88,13 +88,13 @@ run_step() {
       local w=${a[1]} st=${a[2]:-5}
       export TMPDIR=/tmp
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof_$w -o run -- \
-        python3 $R/bench.py --workload $w --steps $st --warmup 2 --no-cpu-baseline > $R/$O/prof_$w.log 2>&1) || return 1
+        python3 $R/bench.py --workload $w --steps $st --warmup 2 --no-cpu-baseline --builder-preds 0 > $R/$O/prof_$w.log 2>&1) || return 1
       (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $R/$O/pmcf_$w -o run -- \
-        python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline > $R/$O/pmcf_$w.log 2>&1) || return 1
+        python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --builder-preds 0 > $R/$O/pmcf_$w.log 2>&1) || return 1
       (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $R/$O/pmcw_$w -o run -- \
-        python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline > $R/$O/pmcw_$w.log 2>&1) || return 1
+        python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --builder-preds 0 > $R/$O/pmcw_$w.log 2>&1) || return 1
       (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS \
-        -d $R/$O/pmcq_$w -o run -- python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline > $R/$O/pmcq_$w.log 2>&1) || return 1
+        -d $R/$O/pmcq_$w -o run -- python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --builder-preds 0 > $R/$O/pmcq_$w.log 2>&1) || return 1
       python3 tools/prof_summary.py --stats $O/prof_$w/run_results.db --pmc $O/pmcf_$w/run_results.db \
         --pmc-write $O/pmcw_$w/run_results.db --pmc-sq $O/pmcq_$w/run_results.db --out $O/${TAG}_$w > $O/prof_summary_$w.txt 2>&1 || return 1
       python3 tools/timeline.py $O/prof_$w/run_results.db --window 0.4 --skip-end 0.05 --gaps > $O/timeline_$w.txt 2>&1
@@ -105,7 +105,7 @@ run_step() {
       export TMPDIR=/tmp
       (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
         --kernel-include-regex "$rx" -d $R/$O/pmcs_$w -o run -- \
-        python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline > $R/$O/pmcs_$w.log 2>&1) || return 1
+        python3 $R/bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --builder-preds 0 > $R/$O/pmcs_$w.log 2>&1) || return 1
       python3 tools/pmc_dump.py $O/pmcs_$w/run_results.db "$rx" > $O/pmcs_$w.txt 2>&1
       rm -rf $O/pmcs_$w
       cat $O/pmcs_$w.txt ;;
@@ -125,7 +125,7 @@ run_step() {
         for v in "${vals[@]}"; do
           local lib=$R/kelpie_amd/libkelpie_hip.so
           [ $v != base ] && lib=$R/variants/lib_$v.so
-          KELPIE_HIP_LIB=$lib timeout -k 10 600 python bench.py --workload $w --steps $st --warmup 1 --no-cpu-baseline \
+          KELPIE_HIP_LIB=$lib timeout -k 10 600 python bench.py --workload $w --steps $st --warmup 1 --no-cpu-baseline --builder-preds 0 \
             > $O/libab_${w}_${v}_$rep.json 2> $O/libab_${w}_${v}_$rep.err || { tail -5 $O/libab_${w}_${v}_$rep.err; return 1; }
           python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], round(d['value'],1), 'cand/s', round(d['ms_per_step'],2), 'ms', 'frac', d['roofline']['frac'], 'fp64', d.get('rank_delta_match_rate_ref_fp64'))" $O/libab_${w}_${v}_$rep.json "$w $v"
         done
