@@ -379,7 +379,7 @@ def builder_leg(model, ds, wl, n_preds, sharding=None):
     torch.manual_seed(42)
     # speculative windows: "auto" (kelpie_amd.builder) or a fixed size (KELPIE_BUILDER_WINDOW, A/B)
     win = os.environ.get("KELPIE_BUILDER_WINDOW", "auto")
-    pipelined = os.environ.get("KELPIE_BUILDER_PIPELINED", "1") == "1"  # A/B: 0 = one window at a time
+    pipelined = os.environ.get("KELPIE_BUILDER_PIPELINED", "0") == "1"  # A/B: 1 = look-ahead windows
     pipe = build_pipeline(model, ds, wl["hp"], wl["mode"], window=win if win == "auto" else int(win),
                           pipelined=pipelined)
     pipe.engine.sharding = sharding

@@ -13,11 +13,15 @@ summarisation), restructured for a batched engine:
   numpy generators are rewound to the state right after the last rule the
   reference would have evaluated, so every later draw is unchanged.
 
-With ``pipelined`` (default) the next window is scheduled and started on a second
-device context before the current one's results are replayed (its draws follow the
-current window's; a stop inside the current window rewinds past both and the next
-window's device work is discarded), so the host's scheduling of a window overlaps the
-device's post-training of the previous one.
+With ``pipelined`` the next window is scheduled and started on a second device context
+before the current one's results are replayed (its draws follow the current window's; a
+stop inside the current window rewinds past both and the next window's device work is
+discarded), so the host's scheduling of a window overlaps the device's post-training of
+the previous one.  Off by default: with adaptive windows a window runs to its end without
+a stop only about a third of the time, so the look-ahead is mostly discarded work that
+competes with the current window for the device (headline builder leg, alternating on
+one box: 392.5 / 394.7 relevances/s pipelined against 452.3 / 453.1, 663 against 503
+evaluations for the same 446 relevances; profiles/r06/r06i/).
 
 Window sizes: a fixed ``window``, or ``window="auto"``: the rules before index 10
 of a length (the sliding window's size: no stochastic stop can happen there, only
@@ -39,7 +43,7 @@ class StochasticBuilder:
     AUTO_MIN, AUTO_MAX = 4, 32
 
     def __init__(self, xsi, engine, summarization: str = None, max_explanation_length: int = 4, window=32,
-                 pipelined=True):
+                 pipelined=False):
         if summarization is not None:
             raise NotImplementedError("summarisation (simulation / bisimulation) is out of scope")
         self.xsi = xsi

@@ -52,7 +52,7 @@ class SufficientPipeline(Pipeline):
 
 
 def build_pipeline(model, dataset, hp, mode, prefilter=None, xsi=None, window="auto", entity_classes=None,
-                   pipelined=True):
+                   pipelined=False):
     """explain.py:49-89 for the post-training engines (baseline=None, no summarisation)."""
     if prefilter == TYPE_PREFILTER:
         raise NotImplementedError("type_based prefilter: out of scope (kelpie_amd/prefilters.py)")

@@ -89,7 +89,7 @@ def check_sufficient(name, backend, batched):
             assert abs(rel - call["relevance"]) <= TOL, (name, call["rule"], rel, call["relevance"])
 
 
-def check_builder(name, backend, window=32):
+def check_builder(name, backend, window=32, pipelined=False):
     rec, ds, model = build_product(name, backend)
     for key in ("builder", "builder_window"):
         b = rec.get(key)
@@ -97,7 +97,7 @@ def check_builder(name, backend, window=32):
             continue
         seed_all(rec["seed"])
         eng = ka.NecessaryPostTrainingEngine(model, ds, rec["hp"])
-        builder = ka.StochasticBuilder(b["xsi"], eng, window=window)
+        builder = ka.StochasticBuilder(b["xsi"], eng, window=window, pipelined=pipelined)
         eng.set_cache()
         out = builder.build_explanations(tuple(b["pred"]), [tuple(t) for t in b["candidates"]])
         assert out["#relevances"] == b["n_relevances"], (key, out["#relevances"], b["n_relevances"])

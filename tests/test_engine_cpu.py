@@ -31,6 +31,14 @@ def test_builder_speculative_windows(name, window):
     check_builder(name, "cpu", window=window)
 
 
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny", "conve60_tiny"])
+@pytest.mark.parametrize("window", [4, "auto"])
+def test_builder_pipelined_windows(name, window):
+    """The look-ahead window (submitted before the current one is replayed, rewound and
+    discarded on a stop) gives the sequential reference's explanations too."""
+    check_builder(name, "cpu", window=window, pipelined=True)
+
+
 @pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])
 def test_pipeline_host_protocol(name):
     check_pipeline(name, "cpu")

@@ -34,6 +34,11 @@ def test_builder_vs_reference_goldens(name, window):
     check_builder(name, "gpu", window=window)
 
 
+@pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny", "conve60_tiny"])
+def test_builder_pipelined_vs_reference_goldens(name):
+    check_builder(name, "gpu", window="auto", pipelined=True)
+
+
 @pytest.mark.parametrize("name", GPU_CASES)
 def test_pipeline_vs_reference_goldens(name):
     check_pipeline(name, "gpu")
