@@ -73,7 +73,7 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 // KP_DIAGNOSTIC_BUILD, which `make diag` sets for the variants/ libraries; the product
 // library can never carry one by a stray define.
 #if (defined(KP_DIAG_NO_S) || defined(KP_DIAG_NO_O) || defined(KP_ATTN_NODMA) || defined(KP_DIAG_DMA_LGKM0) || \
-     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE) || defined(KP_DIAG_NO_OSTORE) || defined(KP_DIAG_EARLY_EXIT) || defined(KP_DIAG_O_HALF) || defined(KP_DIAG_S_HALF)) && \
+     defined(KP_DMA_SPREAD_ALL) || defined(KP_DIAG_S4) || defined(KP_DIAG_DMA_VM0) || defined(KP_DIAG_M0SAVE) || defined(KP_DIAG_NO_OSTORE) || defined(KP_DIAG_EARLY_EXIT) || defined(KP_DIAG_O_HALF) || defined(KP_DIAG_S_HALF) || defined(KP_DIAG_XTILE_W)) && \
     !defined(KP_DIAGNOSTIC_BUILD)
 #error "kp_attn3 diagnostic define without KP_DIAGNOSTIC_BUILD (these builds compute wrong results: make diag)"
 #endif
@@ -496,6 +496,46 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
       if (ntiles > 0) issue(0, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+#ifdef KP_DIAG_XTILE_W
+      // diagnostic (wrong results, timing only): the upper bound of a cross-tile schedule.
+      // The previous tile's softmax weights and P split are computed in pieces in the
+      // S-phase MFMA gaps of this tile (as a schedule running S(t + 1) beside W(t) would),
+      // and this tile's O phase uses them; the instruction mix per tile is the product's
+      float scp[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      float pwn[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      float lacc = 0.f;
+      bf16x8 pbn[3];
+      // piece q of the previous tile's weights: 0..23 = value q / 3, step q % 3 (difference,
+      // exp, centred sum); 24..47 = split of value (q - 24) / 3 into its three pieces
+      float dtmp[8], htmp[8];
+      auto wpiece = [&](int q) {
+        if (q < 24) {
+          const int j = q / 3, st = q % 3;
+          if (st == 0) {
+            dtmp[j] = scp[j >> 2][j & 3] - m_ref;
+            m_seen = fmaxf(m_seen, scp[j >> 2][j & 3]);
+          } else if (st == 1) {
+            pwn[j] = __expf(dtmp[j]);
+          } else {
+            pwn[j] = __fsub_rn(pwn[j], csh);
+            lacc += pwn[j];
+          }
+        } else if (q < 48) {
+          const int j = (q - 24) / 3, st = (q - 24) % 3;
+          if (st == 0) {
+            const __bf16 h = (__bf16)pwn[j];
+            pbn[0][j] = h;
+            htmp[j] = __fsub_rn(pwn[j], (float)h);
+          } else if (st == 1) {
+            const __bf16 m = (__bf16)htmp[j];
+            pbn[1][j] = m;
+            htmp[j] = __fsub_rn(htmp[j], (float)m);
+          } else {
+            pbn[2][j] = (__bf16)htmp[j];
+          }
+        }
+      };
+#endif
 
       for (int t = 0; t < ntiles; ++t) {
         const int k0 = key_begin + t * KT;
@@ -596,6 +636,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
                   else
                     rt[uu][pp] = lds_rd_bf4<true>(rbt, (int)(uu * SUB_B) + pp * PART_B + 64 * NK);
                 }
+#ifdef KP_DIAG_XTILE_W
+                if (u == 1 && WITH_O) wpiece(6 * s + k);  // one piece per gap without a read
+#endif
                 __builtin_amdgcn_sched_barrier(0);
               }
             }
@@ -740,6 +783,9 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
         // (the asm read form only: on the compiler-visible read form of the ConvE width the
         // same branch gave wrong, run-to-run different partials, with or without a
         // lgkmcnt(0) before each asm LDS-DMA piece -- DESIGN.md section 5)
+#ifdef KP_DIAG_XTILE_W
+        if (t == 0 || !ILV || !WITH_O)
+#endif
         if (KP_ATTN_FULLTILE && (ASM || KP_ATTN_FULLTILE_ALL) && k0 + KT <= key_end)
           weights(std::true_type{});
         else
@@ -748,6 +794,15 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
           // P pieces in the B layout: element j of lane group g = entity 4g + j (j < 4)
           // or 16 + 4g + j - 4
           bf16x8 pb[3];
+#ifdef KP_DIAG_XTILE_W
+          if (ILV && t > 0) {
+            pb[0] = pbn[0];
+            pb[1] = pbn[1];
+            pb[2] = pbn[2];
+            l_run += lacc;
+            lacc = 0.f;
+          } else
+#endif
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             __bf16 h, m, l;
@@ -756,6 +811,12 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
             pb[1][j] = m;
             pb[2][j] = l;
           }
+#ifdef KP_DIAG_XTILE_W
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) scp[u][r] = sc[u][r];  // the next tile's gaps weight this tile
+#endif
           KP3_STAMP(st2);
 #pragma unroll
           for (int m = 0; m < DB; ++m) {
