@@ -85,6 +85,12 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #ifndef KP_DMA_SPREAD
 #define KP_DMA_SPREAD 1
 #endif
+#ifndef KP_DMA_SPREAD_BCE
+// the same choice for the ConvE (ATT_BCE_O) instantiation at two workgroups per CU: the
+// burst (0) -- settled-clock micro, YAGO3-10 shape, interleaved: 1.816 / 1.823 ms against
+// 1.830 / 1.838 (1, per O block), 1.847 / 1.850 (2), 1.829 / 1.836 (3, over the S steps)
+#define KP_DMA_SPREAD_BCE 0
+#endif
 #ifndef KP_ILV
 #define KP_ILV 1
 #endif
@@ -113,6 +119,11 @@ static_assert(KP_S_AHEAD >= 1 && KP_S_AHEAD <= 2, "KP_S_AHEAD: 1..2 (lgkmcnt hol
 #endif
 #ifndef KP_ASM_ALL
 #define KP_ASM_ALL 0  // 1: the asm read form for every DB (ConvE included)
+#endif
+#ifndef KP_ASM_MIN_DB
+// the asm read form from this width up (ConvE d = 200 is DB 13: asm since round 6, at two
+// workgroups per CU; the compiler-visible form stays for the narrow test widths)
+#define KP_ASM_MIN_DB 13
 #endif
 #ifndef KP_O_NT
 #define KP_O_NT 0  // 1: nontemporal stores of the O partials (A/B)
@@ -149,7 +160,7 @@ __host__ __device__ constexpr int split3_pieces(int DP) { return (split3_tile_by
 // the asm read form (see lds_rd_bf8) and, with it, the interleaved schedule and the
 // buffer-descriptor LDS-DMA (KP_BUF_DMA): every wave issues the same number of whole
 // pieces, so a tile buffer is rounded up to a multiple of 4 pieces
-__host__ __device__ constexpr bool attn3_asm(int DB) { return DB > 13 || KP_ASM_ALL; }
+__host__ __device__ constexpr bool attn3_asm(int DB) { return DB >= KP_ASM_MIN_DB || KP_ASM_ALL; }
 __host__ __device__ constexpr bool attn3_bufdma(int DB) { return attn3_asm(DB) && KP_ILV && KP_BUF_DMA; }
 __host__ __device__ constexpr int attn3_buf_pieces(int DB) {
   return attn3_bufdma(DB) ? (split3_pieces(16 * DB) + 3) / 4 * 4 : split3_pieces(16 * DB);
@@ -267,8 +278,13 @@ __global__ void kp_split3_table(const float* __restrict__ E, int n_ent, uint8_t*
   row[2 * DP + d + 1] = l[1];
 }
 
+// two workgroups per CU where the ConvE (BCE) form's two tile buffers fit twice in the LDS
+// (ConvE d = 200: 229 registers); one otherwise (wider BCE forms would spill at 256)
 template <int DB, int MODE>
-__global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E3, int n_ent,
+constexpr int attn3_min_wgs() { return (MODE == ATT_BCE_O && 2 * attn3_lds_bytes(DB) <= 163840) ? 2 : 1; }
+
+template <int DB, int MODE>
+__global__ __launch_bounds__(256, (attn3_min_wgs<DB, MODE>())) void kp_attn3(const uint8_t* __restrict__ E3, int n_ent,
                                                    const float* __restrict__ Qpre, int nq, AttnWork wk,
                                                    float* __restrict__ out_m, float* __restrict__ out_l,
                                                    float* __restrict__ out_O, const float* __restrict__ qscale,
@@ -388,17 +404,18 @@ __global__ __launch_bounds__(256, 1) void kp_attn3(const uint8_t* __restrict__ E
   // the wave's k-th piece of a tile's DMA (pieces w, w + 4, ...), for spreading the
   // copy over the O-phase MFMA stream (KP_DMA_SPREAD)
   constexpr int NPW = (PIECES + 3) / 4;
+  constexpr int SPM = MODE == ATT_BCE_O ? KP_DMA_SPREAD_BCE : KP_DMA_SPREAD;  // spread mode of this instantiation
 #ifdef KP_DMA_SPREAD_ALL
-  constexpr bool SPREAD = KP_DMA_SPREAD && WITH_O && KP_DIAG_O;  // diagnostic: every read form
+  constexpr bool SPREAD = SPM && WITH_O && KP_DIAG_O;  // diagnostic: every read form
 #else
-  constexpr bool SPREAD = KP_DMA_SPREAD && ASM && WITH_O && KP_DIAG_O;
+  constexpr bool SPREAD = SPM && ASM && WITH_O && KP_DIAG_O;
 #endif
   // KP_DMA_SPREAD == 2 (interleaved schedule): the pieces go out evenly over the S steps
   // and the O blocks (slot k of NSLOT), so the copy's LDS writes share the LDS with the
   // lighter S-phase reads instead of piling onto the O phase's transposed reads
   // (== 3: over the S steps only)
-  constexpr int NSLOT = (DP / 32 + (DP % 32) / 16) + (KP_DMA_SPREAD == 3 ? 0 : DB);
-  constexpr bool SPREAD2 = SPREAD && ILV && KP_DMA_SPREAD >= 2;
+  constexpr int NSLOT = (DP / 32 + (DP % 32) / 16) + (SPM == 3 ? 0 : DB);
+  constexpr bool SPREAD2 = SPREAD && ILV && SPM >= 2;
   auto issue_piece = [&](int tile, int buf, int k) {
     const int p = 4 * k + w;
     if constexpr (BUFDMA)
@@ -1063,17 +1080,21 @@ const double* tile_prefix(kp_ctx* c) {
   return c->e3pre.as<double>();
 }
 
-// Host: co-resident kp_attn3 workgroups per CU (registers and LDS), cached per context.
-template <int DB>
+// Host: co-resident kp_attn3 workgroups per CU (registers and LDS) of the instantiation a
+// caller launches (MODE: ATT_SOFTMAX_O for ComplEx, whose ATT_SOFTMAX launch is no larger;
+// ATT_BCE_O for ConvE), cached per context and mode.  Taking the smaller of the two modes
+// for both cost ConvE its second workgroup per CU once its read form was the asm one
+// (kp_attn3<13, ATT_SOFTMAX_O> holds 316 registers there, kp_attn3<13, ATT_BCE_O> 232).
+template <int DB, int MODE = ATT_SOFTMAX_O>
 int attn3_wpc(kp_ctx* c) {
-  if (c->attn3_wpc <= 0) {
+  static_assert(MODE == ATT_SOFTMAX_O || MODE == ATT_BCE_O, "attn3_wpc: the launched O mode");
+  int& slot = c->attn3_wpc[MODE == ATT_BCE_O ? 1 : 0];
+  if (slot <= 0) {
     int n = 0;
-    KP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kp_attn3<DB, ATT_SOFTMAX_O>, 256, attn3_lds_bytes(DB)));
-    int n2 = 0;
-    KP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n2, kp_attn3<DB, ATT_BCE_O>, 256, attn3_lds_bytes(DB)));
-    c->attn3_wpc = std::max(1, std::min(n, n2));
+    KP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kp_attn3<DB, MODE>, 256, attn3_lds_bytes(DB)));
+    slot = std::max(1, n);
   }
-  return c->attn3_wpc;
+  return slot;
 }
 
 // Host: the partition of the context's attention kernel.  kp_attn3 takes the XCD-grouped

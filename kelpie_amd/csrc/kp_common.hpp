@@ -137,7 +137,7 @@ struct kp_ctx {
   DevBuf cv_wlc;            // the kelpie rows' FC columns [dim][4608] (built once)
   bool cv_shared_ready = false;
   DevBuf cvs[14];           // per-batch ConvE workspaces (kp_conve.hip)
-  int attn3_wpc = 0;       // co-resident kp_attn3 workgroups per CU (occupancy API)
+  int attn3_wpc[2] = {0, 0};  // co-resident kp_attn3 workgroups per CU, [softmax, BCE] (occupancy API)
   kp_train_state* train = nullptr;  // kp_train_epoch's state (freed with the context)
   kp_cv_train* cvtrain = nullptr;   // kp_conve_train_*'s state (freed with the context)
   std::vector<hipEvent_t> evpool;

@@ -223,10 +223,10 @@ __device__ __forceinline__ float dot256_order2(const float* a, const float* b, f
 }
 
 // kp_cv_dx on two waves per pair with 16 bytes of LDS (NJ = ceil(dp / 128) row values per
-// lane, in registers): bitwise the same as the 256-thread form below, and small enough
-// (<= 32 VGPRs, 16 B of LDS) to run beside the other batch's attention workgroups, whose
-// two waves per SIMD leave 32 registers and 4 KiB of LDS per CU (kp_attn3<13>); the block
-// form (5 KiB of LDS, 35 VGPRs) could not, and waited for whole CUs under overlap
+// lane, in registers): bitwise the same as the 256-thread form below, and small (<= 32
+// VGPRs, 16 B of LDS).  It was sized to run beside the other batch's attention workgroups
+// when their compiler-visible form left 4 KiB of LDS per CU; the asm form of kp_attn3<13>
+// (round 6, two workgroups of 80 KiB) fills the LDS, so it now runs on CUs between them
 template <int NJ>
 __global__ __launch_bounds__(128) void kp_cv_dx2(int M, CvConst k, const CvInst* __restrict__ inst,
                                                  const float* __restrict__ Q, const float* __restrict__ O, int n_split,
@@ -1018,11 +1018,11 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
   int attn_slots = c->n_cu * (DBV <= 13 ? 2 : 1);  // co-resident attention workgroups
   if (c->attn_mode == 1) {
     switch (DBV) {
-      case 4: attn_slots = c->n_cu * attn3_wpc<4>(c); break;
-      case 8: attn_slots = c->n_cu * attn3_wpc<8>(c); break;
-      case 13: attn_slots = c->n_cu * attn3_wpc<13>(c); break;
-      case 16: attn_slots = c->n_cu * attn3_wpc<16>(c); break;
-      case 25: attn_slots = c->n_cu * attn3_wpc<25>(c); break;
+      case 4: attn_slots = c->n_cu * attn3_wpc<4, ATT_BCE_O>(c); break;
+      case 8: attn_slots = c->n_cu * attn3_wpc<8, ATT_BCE_O>(c); break;
+      case 13: attn_slots = c->n_cu * attn3_wpc<13, ATT_BCE_O>(c); break;
+      case 16: attn_slots = c->n_cu * attn3_wpc<16, ATT_BCE_O>(c); break;
+      case 25: attn_slots = c->n_cu * attn3_wpc<25, ATT_BCE_O>(c); break;
       default: throw KpError{KP_ENOTSUP, "ConvE: unsupported padded dimension"};
     }
   }

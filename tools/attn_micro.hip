@@ -156,10 +156,10 @@ static int run(int n_ent, int nq, int iters, float scale, int part) {
   bool use5 = std::getenv("KP_MICRO_ATTN5") && std::atoi(std::getenv("KP_MICRO_ATTN5")) == 1;
 #ifdef KP_MICRO_HAS_ATTN5
   use5 = use5 && DB == 25 && MODE != ATT_BCE_O;
-  const int slots = c.n_cu * (use5 ? attn5_wpc(&c) : attn3_wpc<DB>(&c));
+  const int slots = c.n_cu * (use5 ? attn5_wpc(&c) : attn3_wpc<DB, MODE == ATT_BCE_O ? ATT_BCE_O : ATT_SOFTMAX_O>(&c));
 #else
   use5 = false;
-  const int slots = c.n_cu * attn3_wpc<DB>(&c);
+  const int slots = c.n_cu * attn3_wpc<DB, MODE == ATT_BCE_O ? ATT_BCE_O : ATT_SOFTMAX_O>(&c);
 #endif
   const AttnPlan plan = attn_plan_ctx(&c, nq, n_ent, slots);
   const int parts = plan.wk.n_parts;

@@ -8,7 +8,7 @@ cmd=$1; shift
 if [ "$cmd" = build ]; then
   name=$1; src=$2; shift 2
   mkdir -p variants
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -I"$src" -Itools/attic/attn6 "$@" \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -I"$src" "$@" \
     tools/attn_micro.hip -o variants/attn_micro_$name
   exit 0
 fi

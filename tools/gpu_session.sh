@@ -6,7 +6,7 @@
 #   smoke                              __graft_entry__.smoke()
 #   tests[:<-k expr>]                  pytest -m gpu (optionally -k), verbose, 120 s per test
 #   micro:<variant>[:<reps>]           variants/attn_micro_<variant> on the three attention shapes
-#   microfb:<variant>[:<reps>]         the same, FB15k-237 ComplEx shape only
+#   microfb:<variant>[:<reps>]         the same, FB15k-237 ComplEx shape only (microcv: ConvE YAGO3-10 only)
 #   pmcmicro:<variant>                 settled-clock counter passes of the micro (FB15k-237 shape)
 #   bench:<workload>[:steps[:warmup[:VAR=val,...]]]   one bench line (no CPU baseline)
 #   benchcpu                           the default line as the driver runs it (with the CPU baseline)
@@ -46,12 +46,13 @@ run_step() {
       local rc=$?
       grep -E "^batch" $O/host_profile_${a[1]:-transe-fb15k237-necessary}.txt || true
       return $rc ;;
-    micro|microfb|microdb)
+    micro|microfb|microdb|microcv)
       local v=${a[1]} reps=${a[2]:-2} envs=() tagx=""
       if [ -n "${a[3]}" ]; then IFS=',' read -r -a envs <<< "${a[3]}"; tagx="_$(echo ${a[3]} | tr ',=' '__')"; fi
       local shapes=("${MICRO_SHAPES[@]}")
       [ $n = microfb ] && shapes=("${MICRO_SHAPES[0]}")
       [ $n = microdb ] && shapes=("${MICRO_SHAPES[0]}" "${MICRO_SHAPES[1]}")
+      [ $n = microcv ] && shapes=("${MICRO_SHAPES[2]}")
       for rep in $(seq 1 $reps); do
         for args in "${shapes[@]}"; do
           env "${envs[@]}" timeout -k 10 120 variants/attn_micro_$v $args 0.05 >> $O/micro_$v$tagx.jsonl || return 1
