@@ -131,7 +131,7 @@ int kp_ctx_create(int device, const kp_model_desc* m, kp_ctx** out) {
     // ConvE rank of the post-trained row on fp64 logits (sigmoid is monotone), as a fp64
     // reference ranks; KP_CV_RANK=f32 ranks the fp32 sigmoid scores (A/B)
     if (const char* a = std::getenv("KP_CV_RANK")) c->cv_rank64 = std::strcmp(a, "f32") != 0;
-    // ConvE dL/dfc: two waves per pair (kp_cv_dx2, co-resident with the attention) by
+    // ConvE dL/dfc: one wave per pair (kp_cv_dx1, no LDS: co-resident with the attention) by
     // default; KP_CV_DX=block selects the 256-thread form (A/B; bitwise the same)
     if (const char* a = std::getenv("KP_CV_DX")) c->cv_dx_block = std::strcmp(a, "block") == 0;
     // TransE rank of the post-trained row on fp64 squared distances (sqrt is monotone);

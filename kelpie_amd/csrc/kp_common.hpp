@@ -126,7 +126,7 @@ struct kp_ctx {
   bool eT_ready = false;
   int cv_fused = 1;        // ConvE d = 200: fused encoder kernels (kp_cv_fused.hpp), KP_CV_FUSED
   int cv_rank64 = 1;       // ConvE post-training rank on fp64 logits (KP_CV_RANK=f32: fp32 sigmoid scores)
-  int cv_dx_block = 0;     // ConvE: the 256-thread kp_cv_dx instead of kp_cv_dx2 (KP_CV_DX=block, A/B)
+  int cv_dx_block = 0;     // ConvE: the 256-thread kp_cv_dx instead of kp_cv_dx1 (KP_CV_DX=block, A/B)
   int te_norm = 2;         // TransE score norm p (kp_model_desc.norm_p): 2 or 1
   int te_rank64 = 1;       // TransE post-training rank on fp64 squared distances (KP_TE_RANK=f32: fp32 norms)
   DevBuf cvf_fw3, cvf_bw3;  // their permuted split images of the FC weight (built once)

@@ -197,44 +197,30 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 
 // kp_cv_dx's dot products in its summation order: a 256-thread block_sum of per-thread
 // partials over d = tid + 256 m, i.e. four wave sums (old wave w: d mod 256 in [64 w,
-// 64 w + 64)) added in wave order.  Two waves holding d = t + 128 j (t < 128) keep one
-// partial per parity of j: wave h, parity q covers old wave h + 2 q.  Their wave sums
-// meet in LDS and are added in old-wave order: bitwise the block's result.
+// 64 w + 64)) added in wave order.  One wave holding d = l + 64 j (lane l) keeps one
+// partial per j mod 4 -- partial w is old wave w's lane l, accumulated in the same m
+// order -- and adds the four wave sums in old-wave order: bitwise the block's result,
+// with no LDS.
 template <int NJ>
-__device__ __forceinline__ float dot256_order2(const float* a, const float* b, float* sh) {
-  float p0 = 0.f, p1 = 0.f;
+__device__ __forceinline__ float dot256_order1(const float* a, const float* b) {
+  float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    if (j & 1)
-      p1 += a[j] * b[j];
-    else
-      p0 += a[j] * b[j];
-  }
-  p0 = wave_sum(p0);
-  p1 = wave_sum(p1);
-  const int h = threadIdx.x >> 6;
-  __syncthreads();  // the previous sum's readers are done with sh
-  if ((threadIdx.x & 63) == 0) {
-    sh[h] = p0;
-    sh[h + 2] = p1;
-  }
-  __syncthreads();
-  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+  for (int j = 0; j < NJ; ++j) p[j & 3] += a[j] * b[j];
+  return ((wave_sum(p[0]) + wave_sum(p[1])) + wave_sum(p[2])) + wave_sum(p[3]);
 }
 
-// kp_cv_dx on two waves per pair with 16 bytes of LDS (NJ = ceil(dp / 128) row values per
-// lane, in registers): bitwise the same as the 256-thread form below, and small (<= 32
-// VGPRs, 16 B of LDS).  It was sized to run beside the other batch's attention workgroups
-// when their compiler-visible form left 4 KiB of LDS per CU; the asm form of kp_attn3<13>
-// (round 6, two workgroups of 80 KiB) fills the LDS, so it now runs on CUs between them
+// kp_cv_dx on one wave per pair (NJ = ceil(dp / 64) row values per lane, in registers),
+// bitwise the same as the 256-thread form below.  No LDS and <= 32 VGPRs, so it runs beside
+// the other batch's attention workgroups: two kp_attn3<13> workgroups (asm form, 80 KiB
+// each) fill a CU's LDS, and the round-5 two-wave form's 16 bytes of LDS then kept it off
+// every CU they held (354 us per launch against 65 us, profiles/r06/r06y)
 template <int NJ>
-__global__ __launch_bounds__(128) void kp_cv_dx2(int M, CvConst k, const CvInst* __restrict__ inst,
-                                                 const float* __restrict__ Q, const float* __restrict__ O, int n_split,
-                                                 const int32_t* __restrict__ tails, const float* __restrict__ E,
-                                                 const float* __restrict__ X, const int32_t* __restrict__ bits,
-                                                 const float* __restrict__ bna, float* __restrict__ dfc,
-                                                 float* __restrict__ gk, __bf16* __restrict__ g3) {
-  __shared__ float sh[4];
+__global__ __launch_bounds__(64) void kp_cv_dx1(int M, CvConst k, const CvInst* __restrict__ inst,
+                                                const float* __restrict__ Q, const float* __restrict__ O, int n_split,
+                                                const int32_t* __restrict__ tails, const float* __restrict__ E,
+                                                const float* __restrict__ X, const int32_t* __restrict__ bits,
+                                                const float* __restrict__ bna, float* __restrict__ dfc,
+                                                float* __restrict__ gk, __bf16* __restrict__ g3) {
   const int i = blockIdx.x;
   if (i >= M) return;
   const int t = threadIdx.x;
@@ -242,20 +228,20 @@ __global__ __launch_bounds__(128) void kp_cv_dx2(int M, CvConst k, const CvInst*
   float xi[NJ], xk[NJ], dx[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int d = t + 128 * j;
+    const int d = t + 64 * j;
     const bool in = d < k.dim;
     xi[j] = in ? Q[(size_t)i * k.dp + d] : 0.f;
     xk[j] = in ? X[(size_t)I.slot * k.dp + d] : 0.f;
   }
   const float gs = 1.0f / (float)((long long)I.b * (long long)(k.n_ent + 1));
-  const float sk = dot256_order2<NJ>(xi, xk, sh);  // kelpie column
+  const float sk = dot256_order1<NJ>(xi, xk);  // kelpie column
   bool k_is_tail = false;
   for (int u = 0; u < I.tail_count; ++u) k_is_tail |= (tails[I.tail_begin + u] == k.n_ent);
   const float Gk = bce_g(sk, k_is_tail ? k.yhi : k.ylo, gs);
   if (t == 0) gk[i] = Gk;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int d = t + 128 * j;
+    const int d = t + 64 * j;
     float v = 0.f;
     if (d < k.dim)
       for (int sp = 0; sp < n_split; ++sp) v += O[((size_t)sp * M + i) * k.dp + d];
@@ -268,10 +254,10 @@ __global__ __launch_bounds__(128) void kp_cv_dx2(int M, CvConst k, const CvInst*
     float er[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int d = t + 128 * j;
+      const int d = t + 64 * j;
       er[j] = d < k.dim ? E[(size_t)e * k.dp + d] : 0.f;
     }
-    const float st = dot256_order2<NJ>(xi, er, sh);
+    const float st = dot256_order1<NJ>(xi, er);
     const float corr = bce_g(st, k.yhi, gs) - bce_g(st, k.ylo, gs);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) dx[j] += corr * er[j];
@@ -279,7 +265,7 @@ __global__ __launch_bounds__(128) void kp_cv_dx2(int M, CvConst k, const CvInst*
   const float* a3 = bna + 33;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int d = t + 128 * j;
+    const int d = t + 64 * j;
     if (d < k.dim) {
       const float nz = k.has_mask ? noise_at(bits, I.mb.hid, d, k.scale) : 1.0f;
       const float relu = xi[j] > 0.f ? 1.0f : 0.0f;
@@ -296,7 +282,7 @@ __global__ __launch_bounds__(128) void kp_cv_dx2(int M, CvConst k, const CvInst*
     }
   }
   if (g3)
-    for (int d = k.dim + t; d < kpcvf::KB; d += 128) {
+    for (int d = k.dim + t; d < kpcvf::KB; d += 64) {
       const size_t o = (size_t)i * kpcvf::KB + d, ps = (size_t)M * kpcvf::KB;
       g3[o] = g3[ps + o] = g3[2 * ps + o] = (__bf16)0.f;
     }
@@ -1135,22 +1121,22 @@ void conve_posttrain_rank(kp_ctx* c, const kp_hp* hp, const kp_batch* bt) {
       ++launches;
       {
         __bf16* g3p = shared ? nullptr : dG3;
-        const int nj = (c->dp + 127) / 128;
-#define CV_DX2(J)                                                                                                   \
-  hipLaunchKernelGGL(kp_cv_dx2<J>, dim3(nk), dim3(128), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE, dX, \
+        const int nj = (c->dp + 63) / 64;
+#define CV_DX1(J)                                                                                                  \
+  hipLaunchKernelGGL(kp_cv_dx1<J>, dim3(nk), dim3(64), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE, dX, \
                      dBits, c->d_bn_a, ddfc, dgk, g3p)
-        if (!c->cv_dx_block && nj == 2)
-          CV_DX2(2);
-        else if (!c->cv_dx_block && nj == 1)
-          CV_DX2(1);
-        else if (!c->cv_dx_block && nj == 3)
-          CV_DX2(3);
-        else if (!c->cv_dx_block && nj == 4)
-          CV_DX2(4);
+        if (!c->cv_dx_block && nj <= 2)
+          CV_DX1(2);
+        else if (!c->cv_dx_block && nj <= 4)
+          CV_DX1(4);
+        else if (!c->cv_dx_block && nj <= 6)
+          CV_DX1(6);
+        else if (!c->cv_dx_block && nj <= 8)
+          CV_DX1(8);
         else
           hipLaunchKernelGGL(kp_cv_dx, dim3(nk), dim3(256), 0, c->stream, nk, kc, KI, dQ, dO, n_split, dTails, c->dE,
                              dX, dBits, c->d_bn_a, ddfc, dgk, g3p);
-#undef CV_DX2
+#undef CV_DX1
       }
       KP_HIP(hipGetLastError());
       if (shared) {
