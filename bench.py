@@ -396,6 +396,9 @@ def builder_leg(model, ds, wl, n_preds, sharding=None):
            "engine_batches": st["batches"], "xsi": pipe.builder.xsi, "prefilter_k": 20,
            "speculative_window": "auto" if pipe.builder.auto else pipe.builder.spec_window,
            "windows_pipelined": pipe.builder.pipelined,
+           # where the builder's time goes: engine batches (wall), and inside them the host
+           # schedule (reference-order draws, slot assembly), packing and the library call
+           "time_split_s": {k: round(st[k], 4) for k in ("batch_s", "schedule_s", "pack_s", "lib_s")},
            "per_prediction": [{"#relevances": ex["#relevances"], "execution_time_s": ex["execution_time"]}
                               for ex in exs]}
     fx = load_builder_fixture(wl["_name"])

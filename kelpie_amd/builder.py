@@ -13,15 +13,19 @@ summarisation), restructured for a batched engine:
   numpy generators are rewound to the state right after the last rule the
   reference would have evaluated, so every later draw is unchanged.
 
-With ``pipelined`` the next window is scheduled and started on a second device context
-before the current one's results are replayed (its draws follow the current window's; a
-stop inside the current window rewinds past both and the next window's device work is
-discarded), so the host's scheduling of a window overlaps the device's post-training of
-the previous one.  Off by default: with adaptive windows a window runs to its end without
-a stop only about a third of the time, so the look-ahead is mostly discarded work that
-competes with the current window for the device (headline builder leg, alternating on
-one box: 392.5 / 394.7 relevances/s pipelined against 452.3 / 453.1, 663 against 503
-evaluations for the same 446 relevances; profiles/r06/r06i/).
+With ``pipelined`` the next window is scheduled while the current one runs on the device
+(its draws follow the current window's, on this thread; its slots are packed on its batch
+thread), but it is held: its device work starts only once the replay of the current
+window has gone through without a stop (``engine.submit_batch(hold=True)``,
+``release_batch``).  A stop inside the current window cancels it with no device work and
+rewinds the generators past both, so only host work is ever thrown away.  Off by default:
+the look-ahead's size is chosen before the current window's relevances are known, so its
+windows run past more stops (273 against 245 evaluations for the same 224 relevances), and
+that costs more device time than overlapping the host schedule saves (the schedule is 11 %
+of the builder's time, the library call 85 %): headline builder leg, alternating on one
+box, 439.8 / 456.9 relevances/s held look-ahead against 485.1 / 480.8 sequential
+(profiles/r06/r06y/r06y7_*).  A first form started the look-ahead at once on the second
+context: 392.5 / 394.7 against 452.3 / 453.1 (profiles/r06/r06i/).
 
 Window sizes: a fixed ``window``, or ``window="auto"``: the rules before index 10
 of a length (the sliding window's size: no stochastic stop can happen there, only
@@ -55,7 +59,16 @@ class StochasticBuilder:
         self.pipelined = bool(pipelined) and hasattr(engine, "submit_batch")
         self.spec_window = self.AUTO_MAX if self.auto else max(1, int(window))
         self.summarization = None
-        self.stats = {"batches": 0, "evaluated": 0, "wasted": 0}
+        self.stats = {"batches": 0, "evaluated": 0, "wasted": 0, "batch_s": 0.0, "schedule_s": 0.0, "pack_s": 0.0,
+                      "lib_s": 0.0}
+
+    def _account(self, t0):
+        """Wall time of one engine batch and the engine's host / library split of it."""
+        self.stats["batch_s"] += time.perf_counter() - t0
+        bs = getattr(self.engine, "last_batch_stats", None)
+        if isinstance(bs, dict):
+            for k in ("schedule_s", "pack_s", "lib_s"):
+                self.stats[k] += float(bs.get(k, 0.0) or 0.0)
 
     def build_explanations(self, pred, candidate_triples: list, k: int = 10):
         start = time.time()
@@ -85,7 +98,9 @@ class StochasticBuilder:
     def explore_singleton_rules(self, pred, triples: list):
         # one engine batch for every singleton; a duplicated candidate is evaluated
         # once per occurrence and the last value wins, like the dict of :113-123
+        t0 = time.perf_counter()
         rels = self.engine.compute_relevance_batch(pred, [[t] for t in triples])
+        self._account(t0)
         self.stats["batches"] += 1
         self.stats["evaluated"] += len(triples)
         out = {}
@@ -106,30 +121,37 @@ class StochasticBuilder:
         eng = self.engine
         ahead = None  # the next window, scheduled and started speculatively: (rules, checkpoints, batch)
 
-        def submit(at):
+        def submit(at, hold=False):
             chunk = [r for r, _ in rules[at:at + self._window(at, window, best)]]
             cps = []
             if self.pipelined:
-                return chunk, cps, eng.submit_batch(pred, [list(r) for r in chunk], checkpoints=cps)
+                return chunk, cps, eng.submit_batch(pred, [list(r) for r in chunk], checkpoints=cps, hold=hold)
             return chunk, cps, None
 
         while i < len(rules) and not terminate:
             if ahead is not None:
                 chunk, cps, batch = ahead
                 ahead = None
+                eng.release_batch(batch)  # the previous window ran through: start its device work
             else:
                 chunk, cps, batch = submit(i)
             if self.pipelined:
+                t0 = time.perf_counter()
                 if i + len(chunk) < len(rules):
-                    ahead = submit(i + len(chunk))  # scheduled while `batch` runs on the device
+                    # scheduled and packed while `batch` runs on the device, held until the
+                    # replay below has gone through `batch` without a stop
+                    ahead = submit(i + len(chunk), hold=True)
                 try:
                     rels = eng.finish_batch(batch)
                 except BaseException:
                     if ahead is not None:
-                        eng.finish_batch(ahead[2], discard=True)  # leave no device work behind
+                        eng.finish_batch(ahead[2], discard=True)  # cancelled: no device work
                     raise
+                self._account(t0)
             else:
+                t0 = time.perf_counter()
                 rels = eng.compute_relevance_batch(pred, [list(r) for r in chunk], checkpoints=cps)
+                self._account(t0)
             self.stats["batches"] += 1
             self.stats["evaluated"] += len(chunk)
             stop_at = None
@@ -152,13 +174,12 @@ class StochasticBuilder:
                         break
             if stop_at is not None:
                 if ahead is not None:
-                    # the speculative next window: wait for its device work, drop its results
+                    # the held next window: cancelled before any device work (its host
+                    # schedule is all that is lost); rewind past it and this window's later rules
                     eng.finish_batch(ahead[2], discard=True)
-                    self.stats["batches"] += 1
-                    self.stats["evaluated"] += len(ahead[0])
-                    self.stats["wasted"] += len(ahead[0])
+                    self.stats["lookahead_cancelled"] = self.stats.get("lookahead_cancelled", 0) + 1
                     ahead = None
-                    cps[stop_at].restore()  # rewind past this window's later rules and the next one
+                    cps[stop_at].restore()
                 elif stop_at + 1 < len(chunk):
                     cps[stop_at].restore()  # rewind the speculative draws
                 self.stats["wasted"] += len(chunk) - stop_at - 1

@@ -464,12 +464,16 @@ class PostTrainingEngine(RelevanceEngine):
         finally:
             self._flush_fused()
 
-    def _run(self, slots, ctx=None):
+    def _run(self, slots, ctx=None, gate=None):
         """Post-train and rank ``slots`` on the device.  With ``self.sharding`` only this
-        rank's share runs; ``_collect`` then gathers every rank's results."""
+        rank's share runs; ``_collect`` then gathers every rank's results.  ``gate``: called
+        (blocking) before the library call, after the batch is packed; False cancels the
+        batch (no device work, None returned) -- a held look-ahead window (submit_batch)."""
         if not slots:
             return {}
         if self._sharded():
+            if gate is not None and not gate():
+                return None
             # the slots this rank claimed while scheduling; a failure is reported to the
             # other ranks through the gather (_collect) instead of leaving them waiting in it
             mine = [i for i, s in enumerate(slots) if s.own]
@@ -489,7 +493,7 @@ class PostTrainingEngine(RelevanceEngine):
             stats["_local"] = (mine, score, rank, len(slots), err, counts)
             self.last_batch_stats = stats
             return stats
-        return self._run_slots(slots, ctx, fill=True)
+        return self._run_slots(slots, ctx, fill=True, gate=gate)
 
     def _collect(self, slots, stats):
         """All-gather the ranks' slot results of a sharded batch (in batch order on every rank)."""
@@ -617,11 +621,13 @@ class PostTrainingEngine(RelevanceEngine):
         parts = [flat[doff[j]:doff[j] + nsz[j]] for j in js.tolist() if nsz[j]]
         return np.concatenate(parts).astype(np.int32, copy=False) if parts else np.zeros(1, np.int32)
 
-    def _run_slots(self, slots, ctx, fill):
+    def _run_slots(self, slots, ctx, fill, gate=None):
         t_run = time.perf_counter()
         n = len(slots)
         ctx = ctx or self.model.ctx
         packed = self._pack(slots, ctx)
+        if gate is not None and not gate():
+            return None
         t_lib = time.perf_counter()
         score, rank, _ = ctx.posttrain_rank(self._kp_hp, *packed)
         t_end = time.perf_counter()
@@ -675,13 +681,17 @@ class PostTrainingEngine(RelevanceEngine):
         conversion entities)."""
         return [(pred, rules)]
 
-    def submit_batch(self, pred, rules, checkpoints: list | None = None):
+    def submit_batch(self, pred, rules, checkpoints: list | None = None, hold=False):
         """The first half of ``compute_relevance_batch``: schedule the rules' reference-order
         draws on this thread (with ``checkpoints`` as there) and start their device work on
         the next of two pipeline contexts, without waiting; :meth:`finish_batch` returns the
         relevances.  A later submit may be scheduled while this batch runs -- the
         builder's next speculative window (kelpie_amd/builder.py) -- and rewinding the
-        generators to one of this batch's checkpoints undoes both."""
+        generators to one of this batch's checkpoints undoes both.
+
+        ``hold``: the batch's draws wait and its slots are packed on the batch thread, but
+        its library call waits for :meth:`release_batch` (or :meth:`finish_batch`); a
+        ``finish_batch(discard=True)`` before that cancels it without any device work."""
         import threading
 
         from . import rng as _rng_mod
@@ -695,13 +705,20 @@ class PostTrainingEngine(RelevanceEngine):
         with self.rng.deferred(detach=True) as d:
             slots, pending, jobs = self._schedule_all(self._batch_items(pred, rules), checkpoints)
         st = {"slots": slots, "pending": pending, "jobs": jobs, "deferred": self._deferred_error,
-              "ticket": d.last_ticket, "error": None, "stats": None}
+              "ticket": d.last_ticket, "error": None, "stats": None, "go": threading.Event(), "cancel": False}
         self._deferred_error = None
+        if not hold:
+            st["go"].set()
+
+        def gate():
+            st["go"].wait()
+            return not st["cancel"]
 
         def run():
             try:
                 _rng_mod.wait_ticket(st["ticket"])
-                st["stats"] = dict(self._run(slots, ctx=ctx))
+                stats = self._run(slots, ctx=ctx, gate=gate)
+                st["stats"] = dict(stats) if stats is not None else None
             except BaseException as e:  # re-raised by finish_batch
                 st["error"] = e
 
@@ -710,9 +727,17 @@ class PostTrainingEngine(RelevanceEngine):
         self._ctx_last = {**getattr(self, "_ctx_last", {}), id(ctx): st}
         return st
 
+    def release_batch(self, st):
+        """Let a held :meth:`submit_batch` batch start its device work."""
+        st["go"].set()
+
     def finish_batch(self, st, discard=False):
         """Wait for a :meth:`submit_batch` batch and return its relevances (``discard``: only
-        wait -- a speculative window the builder does not use -- and return None)."""
+        wait -- a speculative window the builder does not use -- and return None; a held
+        batch not yet released is cancelled instead, with no device work)."""
+        if discard and not st["go"].is_set():
+            st["cancel"] = True
+        st["go"].set()
         st["thread"].join()
         if discard:
             return None

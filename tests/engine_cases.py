@@ -90,7 +90,23 @@ def check_sufficient(name, backend, batched):
 
 
 def check_builder(name, backend, window=32, pipelined=False):
+    """The builder's explanations equal the reference's; returns the library calls made
+    and the builder's stats per recorded builder case."""
     rec, ds, model = build_product(name, backend)
+    calls = [0]
+    seen = set()
+    for ctx in model.contexts(2):
+        if id(ctx) in seen:
+            continue
+        seen.add(id(ctx))
+        orig = ctx.posttrain_rank
+
+        def counted(*a, _orig=orig, **k):
+            calls[0] += 1
+            return _orig(*a, **k)
+
+        ctx.posttrain_rank = counted
+    out_stats = []
     for key in ("builder", "builder_window"):
         b = rec.get(key)
         if not b:
@@ -105,6 +121,9 @@ def check_builder(name, backend, window=32, pipelined=False):
         for (rule, rel), (erule, erel) in zip(out["rule_to_relevance"], b["rule_to_relevance"]):
             assert [list(t) for t in rule] == [list(t) for t in erule]
             assert abs(rel - erel) <= TOL
+        out_stats.append((calls[0], dict(builder.stats)))
+        calls[0] = 0
+    return out_stats
 
 
 def _two_stand_in_contexts(model):

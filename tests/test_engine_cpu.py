@@ -34,9 +34,11 @@ def test_builder_speculative_windows(name, window):
 @pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny", "conve60_tiny"])
 @pytest.mark.parametrize("window", [4, "auto"])
 def test_builder_pipelined_windows(name, window):
-    """The look-ahead window (submitted before the current one is replayed, rewound and
-    discarded on a stop) gives the sequential reference's explanations too."""
-    check_builder(name, "cpu", window=window, pipelined=True)
+    """The look-ahead window (scheduled before the current one is replayed and held; on a
+    stop cancelled and rewound) gives the sequential reference's explanations too, and a
+    cancelled look-ahead makes no library call: one call per evaluated engine batch."""
+    for calls, st in check_builder(name, "cpu", window=window, pipelined=True):
+        assert calls == st["batches"], (calls, st)
 
 
 @pytest.mark.parametrize("name", ["complex_tiny", "transe_tiny"])

@@ -10,6 +10,8 @@
 #   pmcmicro:<variant>                 settled-clock counter passes of the micro (FB15k-237 shape)
 #   bench:<workload>[:steps[:warmup[:VAR=val,...]]]   one bench line (no CPU baseline)
 #   benchcpu                           the default line as the driver runs it (with the CPU baseline)
+#   builderab:<VAR>:<v1,..>[:reps[:preds]]  builder leg A/B over an env switch
+#   builderprof[:preds]               kernel trace + device timeline of the builder leg
 #   prof:<workload>[:steps]            rocprofv3 kernel trace + FETCH_SIZE/WRITE_SIZE passes + summary
 #   pmcbench:<workload>:<regex>        SQ counter pass of one bench workload's kernels
 #   ab:<workload>:<VAR>:<v1,v2,..>[:reps[:steps]]    alternating env A/B of the bench
@@ -85,6 +87,27 @@ run_step() {
     benchcpu)
       timeout -k 10 500 python bench.py --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err || return 1
       cut -c1-400 $O/bench_default.json ;;
+    builderab)
+      # builderab:<VAR>:<v1,v2,..>[:reps[:preds]]: the default line's builder leg, alternating env values
+      local var=${a[1]} reps=${a[3]:-2} np=${a[4]:-4}
+      IFS=',' read -r -a vals <<< "${a[2]}"
+      for rep in $(seq 1 $reps); do
+        for v in "${vals[@]}"; do
+          env "$var=$v" timeout -k 10 400 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --builder-preds $np \
+            > $O/builderab_${var}_${v}_$rep.json 2> $O/builderab_${var}_${v}_$rep.err || { tail -5 $O/builderab_${var}_${v}_$rep.err; return 1; }
+          python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);b=d['builder'];print(sys.argv[2], round(b['value'],1), 'rel/s', b['relevances'], 'rel', b['evaluated'], 'eval', b['engine_batches'], 'batches', b.get('time_split_s'), {k: v['#relevances_equal'] and v['top10_rules_equal'] for k, v in b.get('reference_match_first_prediction', {}).items() if k != 'fixture'})" $O/builderab_${var}_${v}_$rep.json "$var=$v"
+        done
+      done ;;
+    builderprof)
+      # builderprof[:<preds>]: kernel trace of the default line's builder leg (the run's last kernels)
+      local np=${a[1]:-4}
+      export TMPDIR=/tmp
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace -d $R/$O/bprof -o run -- \
+        python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --builder-preds $np > $R/$O/bprof.json 2> $R/$O/bprof.err) || return 1
+      local win=$(python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(d['builder']['execution_time_s'])" $O/bprof.json)
+      python3 tools/timeline.py $O/bprof/run_results.db --window $win --skip-end 0 --gaps > $O/builder_timeline.txt 2>&1
+      rm -rf $O/bprof
+      head -30 $O/builder_timeline.txt ;;
     prof)
       local w=${a[1]} st=${a[2]:-5}
       export TMPDIR=/tmp
