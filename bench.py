@@ -453,7 +453,9 @@ def main():
     if world > 1:
         eng.sharding = kd.SlotSharding()
     n_steps = args.warmup + args.steps
-    per_step = (args.preds_per_step or wl.get("preds_per_step", 1)) * world  # weak scaling
+    # --preds-per-step, or KELPIE_PREDS_PER_STEP (A/B through tools/gpu_session.sh), overrides the workload's
+    pps = args.preds_per_step or int(os.environ.get("KELPIE_PREDS_PER_STEP", "0") or 0) or None
+    per_step = (pps or wl.get("preds_per_step", 1)) * world  # weak scaling
     my_preds = pick_preds(ds, n_steps * per_step, seed=1234)  # every rank schedules every batch
     import random
     random.seed(42)

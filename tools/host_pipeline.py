@@ -38,6 +38,9 @@ class NullContext:
     def last_timing(self):
         return {}
 
+    def convertible(self, ents, p, o, filt_off, filt):
+        return np.ones(len(ents), bool)  # every candidate entity converts (host cost only)
+
 
 def main():
     ap = argparse.ArgumentParser()
