@@ -1,17 +1,19 @@
 """Tripwire for the LDS-DMA hazard of the attention kernels.
 
-Two non-shipped variants of the compiler-visible read form of ``kp_attn3`` (the one the
-ConvE instantiation ``kp_attn3<13, ATT_BCE_O>`` ships in) gave wrong partials that
-changed from run to run.  The shipped form passes, but nothing else would notice the
-hazard returning after a compiler or layout change, so this test reruns the ConvE
-post-training batch at the YAGO3-10 shape (123,182 entities: 3,850 key tiles, the
-bench's own ConvE workload, 20 candidates of one prediction, 109 Adam steps each) and
-asserts that every relevance, rank and post-trained score is bitwise equal across
-reruns on fresh contexts, and equal to the same batch with the fp32 attention
-(``KP_ATTN=f32``, ``kp_attn``, no LDS-DMA of the split image) within the
-accumulation-order spread of the two contractions (the fp64 check proper is the
-full-size fixtures' test against the fp64 reference, tests/test_fullsize_reference.py).  The ComplEx instantiation
-(``kp_attn3<25>``, inline-asm reads) gets the same rerun check on the headline workload.
+Two non-shipped variants of the compiler-visible read form of ``kp_attn3`` (the form the
+ConvE instantiation ``kp_attn3<13, ATT_BCE_O>`` shipped in until round 6; it now ships in
+the inline-asm read form at two workgroups per CU) gave wrong partials that changed from
+run to run.  The shipped forms pass, but nothing else would notice the hazard returning
+after a compiler or layout change, so this test reruns the ConvE post-training batch at
+the YAGO3-10 shape (123,182 entities: 3,850 key tiles, the bench's own ConvE workload, 20
+candidates of one prediction, 109 Adam steps each) and asserts that every relevance, rank
+and post-trained score is bitwise equal across reruns on fresh contexts, and equal to the
+same batch with the fp32 attention (``KP_ATTN=f32``, ``kp_attn``, no LDS-DMA of the split
+image) within the accumulation-order spread of the two contractions (the fp64 check
+proper is the full-size fixtures' test against the fp64 reference,
+tests/test_fullsize_reference.py).  The ComplEx instantiation (``kp_attn3<25>``) gets the
+same rerun check on the headline workload.  The one-wave ConvE ``kp_cv_dx1`` is held
+bitwise to the 256-thread ``kp_cv_dx`` whose summation order it keeps.
 """
 import numpy as np
 import pytest
@@ -58,3 +60,13 @@ def test_conve_attention_matches_fp32_contraction(monkeypatch):
     assert np.allclose(got[2], ref[2], rtol=1e-5, atol=0)
     assert np.abs(got[1] - ref[1]).max() <= 6
     assert np.mean(got[1] == ref[1]) >= 0.9
+
+
+def test_conve_dx_one_wave_bitwise_block(monkeypatch):
+    """kp_cv_dx1 (one wave per pair, no LDS) against the block form (KP_CV_DX=block): the
+    same partial sums in the same order, so the whole batch is bitwise the same."""
+    got = _run("conve-yago310-necessary", 8)
+    monkeypatch.setenv("KP_CV_DX", "block")
+    ref = _run("conve-yago310-necessary", 8)
+    for x, y in zip(got, ref):
+        assert x.tobytes() == y.tobytes()
