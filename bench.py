@@ -82,10 +82,12 @@ WORKLOADS = {
                                       hp=COMPLEX_DB100K_HP, candidates=20, convert=10, preds_per_step=1,
                                       cpu_conversions=2, depth=3),
     # BASELINE.json configs[4]
-    # six predictions per step (round 6): with the two-workgroup attention, alternating on one box
-    # 498.6 / 518.6 / 510.8 cand/s against 486.5 / 485.0 / 487.6 at eight (profiles/r06/r06z6/)
+    # eight predictions per step.  (Round 6 measured six against eight: 498.6 / 518.6 / 510.8
+    # against 486.5 / 485.0 / 487.6 cand/s, profiles/r06/r06z6/ -- but at a fixed step count
+    # the two time different predictions, and eight's are 7.5 % heavier per candidate (65.7
+    # against 61.1 training rows): per row eight is as fast, 32.0k against 31.2k rows/s.)
     "conve-yago310-necessary": dict(model="ConvE", shape="YAGO3-10", dim=200, mode="necessary", hp=CONVE_HP,
-                                    candidates=20, preds_per_step=6, hidden_dropout=0.2, depth=3),
+                                    candidates=20, preds_per_step=8, hidden_dropout=0.2, depth=3),
     # the same with all three ConvE dropouts in post-training at the rates of the reference's
     # ConvE YAGO4-20 config (configs/ConvE_YAGO4-20_training.json: input 0.2, feature map 0.3,
     # hidden 0.1; conve.py:142,147,151): the frozen-head pairs are re-encoded every step
