@@ -128,13 +128,24 @@ class StochasticBuilder:
                 return chunk, cps, eng.submit_batch(pred, [list(r) for r in chunk], checkpoints=cps, hold=hold)
             return chunk, cps, None
 
+        prev_cps = None
         while i < len(rules) and not terminate:
             if ahead is not None:
                 chunk, cps, batch = ahead
                 ahead = None
-                eng.release_batch(batch)  # the previous window ran through: start its device work
+                if len(chunk) > self._window(i, window, best):
+                    # sized before the previous window's relevances were known and larger than
+                    # the window the sequential search now takes here: cancel it (no device
+                    # work), rewind to its start and schedule the sequential one
+                    eng.finish_batch(batch, discard=True)
+                    self.stats["lookahead_resized"] = self.stats.get("lookahead_resized", 0) + 1
+                    prev_cps[-1].restore()
+                    chunk, cps, batch = submit(i)
+                else:
+                    eng.release_batch(batch)  # the previous window ran through: start its device work
             else:
                 chunk, cps, batch = submit(i)
+            prev_cps = cps
             if self.pipelined:
                 t0 = time.perf_counter()
                 if i + len(chunk) < len(rules):
